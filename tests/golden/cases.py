@@ -1,0 +1,146 @@
+"""Golden-case definitions shared by make_golden.py (generation, reference side) and
+the tests (replay, build side): model geometry, inputs and injected RNG draws.
+
+All random draws of one reference training step (SURVEY §8c "RNG sources") are
+replaced by deterministic hash streams so that the reference, the oracle and the
+HIP path see identical values:
+  orders      numpy shuffle per sample       mar_con_unified.py:414-422
+  mask_rate   scipy truncnorm.rvs            mar_con_unified.py:428
+  text_drop   torch.rand(B) (label drop)     mar_con_unified.py:629
+  t_*/noise_* torch.randint / randn_like     diffusion_loss.py:51-56, gaussian_diffusion.py:761
+  vae_eps_*   torch.randn (posterior.sample) vaekl.py:414-416
+  task_mode   random.choice                  unified_video_action_policy.py:408
+"""
+import math
+
+import numpy as np
+
+from hashinit import hash_normal, hash_tensor, uniform_pm1
+
+# Reduced MAR at FULL token geometry (4 frames x 256 tokens, 16-ch latents).
+MAR_GOLDEN = dict(
+    encoder_embed_dim=128, encoder_depth=1, encoder_num_heads=2,
+    decoder_embed_dim=128, decoder_depth=1, decoder_num_heads=2, mlp_ratio=4,
+)
+MAR_KW = dict(
+    img_size=256, vae_stride=16, patch_size=1, vae_embed_dim=16, mask_ratio_min=0.7,
+    label_drop_prob=0.1, attn_dropout=0.0, proj_dropout=0.0, diffloss_d=2, diffloss_w=64,
+    diffloss_act_d=2, diffloss_act_w=64, num_sampling_steps="100", diffusion_batch_mul=1,
+    grad_checkpointing=False, predict_video=True, act_diff_training_steps=1000,
+    act_diff_testing_steps="100", use_history_action=False, action_mask_ratio=0.5,
+    predict_wrist_img=False,
+)
+
+ALL_MODES = ["video_model", "dynamic_model", "policy_model", "inverse_model", "full_dynamic_model"]
+
+VARIANTS = {
+    "pusht": dict(task_name="pusht", Da=2, clip=False, use_proprioception=False,
+                  predict_proprioception=False, different_history_freq=False, modes=ALL_MODES),
+    "libero": dict(task_name="libero_10", Da=10, clip=True, use_proprioception=False,
+                   predict_proprioception=False, different_history_freq=False, modes=ALL_MODES),
+    "umi": dict(task_name="umi", Da=10, clip=True, use_proprioception=True,
+                predict_proprioception=True, different_history_freq=True,
+                modes=["policy_model", "full_dynamic_model"]),
+}
+B_MAR = 2
+
+
+def mar_kwargs(variant):
+    v = VARIANTS[variant]
+    kw = dict(MAR_KW)
+    kw.update(
+        task_name=v["task_name"], use_proprioception=v["use_proprioception"],
+        predict_proprioception=v["predict_proprioception"],
+        different_history_freq=v["different_history_freq"],
+        language_emb_model="clip" if v["clip"] else None,
+        action_model_params=dict(predict_action=True, act_model_type="conv_fc"),
+        shape_meta={"action": {"shape": [v["Da"]]}},
+    )
+    return kw
+
+
+def uses_video(mode):
+    return mode in ("video_model", "dynamic_model", "full_dynamic_model")
+
+
+def uses_action(mode):
+    return mode in ("policy_model", "inverse_model", "full_dynamic_model")
+
+
+def orders(tag, B, L=256):
+    return np.stack([np.argsort(uniform_pm1(f"{tag}/orders/{b}", L), kind="stable")
+                     for b in range(B)]).astype(np.int64)
+
+
+def t_steps(tag, n, T=1000):
+    u = (uniform_pm1(f"{tag}/t", n) + 1.0) * 0.5
+    t = np.minimum((u * T).astype(np.int64), T - 1)
+    t[:3] = [0, 1, T - 1]  # always exercise the t==0 decoder-NLL branch and both ends
+    return t
+
+
+def mask_rate(tag):
+    u = (uniform_pm1(f"{tag}/rate", 1)[0] + 1.0) * 0.5
+    return 0.7 + 0.3 * float(u)
+
+
+def mar_inputs(variant, B=B_MAR):
+    v = VARIANTS[variant]
+    tag = f"mar/{variant}"
+    d = {
+        "z": hash_normal(f"{tag}/z", (B, 4, 16, 16, 16)),
+        "c": hash_normal(f"{tag}/c", (B, 4, 16, 16, 16)),
+        "nactions": hash_tensor(f"{tag}/nactions", (B, 16, v["Da"])),
+    }
+    if v["clip"]:
+        d["text_latents"] = hash_normal(f"{tag}/text", (B, 512))
+    if v["use_proprioception"]:
+        d["robot0_eef_pos"] = hash_tensor(f"{tag}/p0", (B, 4, 3))
+        d["robot0_eef_rot_axis_angle"] = hash_tensor(f"{tag}/p1", (B, 4, 6))
+        d["robot0_gripper_width"] = hash_tensor(f"{tag}/p2", (B, 4, 1))
+        d["robot0_eef_rot_axis_angle_wrt_start"] = hash_tensor(f"{tag}/p3", (B, 4, 6))
+        d["robot0_eef_rot_axis_angle_wrt_start_pred"] = hash_tensor(f"{tag}/p4", (B, 16, 6))
+    return d
+
+
+def mar_rng(variant, mode, B=B_MAR):
+    """Injected draws for one MAR.forward call, in the reference's call order."""
+    v = VARIANTS[variant]
+    tag = f"mar/{variant}/{mode}"
+    r = {"orders": orders(tag, B), "mask_rate": mask_rate(tag), "randint": [], "randn_like": []}
+    if v["clip"]:
+        r["text_drop_u"] = np.array([0.05] + [0.5] * (B - 1), dtype=np.float32)  # sample 0 dropped
+    if uses_video(mode):
+        r["randint"].append(t_steps(tag + "/video", B * 1024))
+        r["randn_like"].append(hash_normal(tag + "/video/noise", (B * 1024, 16)))
+    if uses_action(mode):
+        r["randint"].append(t_steps(tag + "/act", B * 16))
+        r["randn_like"].append(hash_normal(tag + "/act/noise", (B * 16, v["Da"])))
+    if v["predict_proprioception"]:
+        r["randint"].append(t_steps(tag + "/prop", B * 16))
+        r["randn_like"].append(hash_normal(tag + "/prop/noise", (B * 16, 6)))
+    return r
+
+
+def num_masked(rate, L=256):
+    return int(math.ceil(L * rate))
+
+
+# ---- policy-level (config 1 semantics, B=1, full VAE, reduced MAR) -----------------
+POLICY_B = 1
+POLICY_MODES = ["full_dynamic_model", "video_model"]
+
+
+def policy_batch(B=POLICY_B):
+    img = (hash_tensor("policy/image", (B, 32, 3, 96, 96)) + 1.0) * 0.5
+    pos = (hash_tensor("policy/agent_pos", (B, 32, 2)) + 1.0) * 256.0
+    act = (hash_tensor("policy/action", (B, 32, 2)) + 1.0) * 256.0
+    return {"image": img, "agent_pos": pos, "action": act}
+
+
+def policy_rng(mode, B=POLICY_B):
+    tag = f"policy/{mode}"
+    r = mar_rng("pusht", mode, B)
+    r["vae_eps_x"] = hash_normal(tag + "/eps_x", (B * 4, 16, 16, 16))
+    r["vae_eps_c"] = hash_normal(tag + "/eps_c", (B * 4, 16, 16, 16))
+    return r

@@ -1,0 +1,335 @@
+"""Generate the golden fixtures under tests/golden/ by running the REFERENCE
+(/root/reference, imported read-only with ref_shims) on hash-initialised weights
+and hash-generated inputs with injected RNG (cases.py).
+
+Run in the build container only:   python tests/golden/make_golden.py
+The outputs are small .npz files of inputs-free data (the inputs are
+regenerated from cases.py by name) holding expected outputs / checksums.
+"""
+import contextlib
+import os
+import random
+import sys
+from functools import partial
+
+import numpy as np
+import torch
+import torch.nn as nn
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, HERE)
+import ref_shims  # noqa: E402
+
+ref_shims.install()
+from hashinit import hash_init_, hash_normal, hash_tensor  # noqa: E402
+import cases  # noqa: E402
+
+import unified_video_action.model.autoregressive.mar_con_unified as ref_mar  # noqa: E402
+from unified_video_action.model.autoregressive.diffusion import create_diffusion  # noqa: E402
+from unified_video_action.model.autoregressive.diffusion_loss import SimpleMLPAdaLN  # noqa: E402
+from unified_video_action.model.autoregressive.ema_model import EMAModel  # noqa: E402
+from unified_video_action.vae import vaekl  # noqa: E402
+from unified_video_action.utils import data_utils  # noqa: E402
+
+torch.set_num_threads(8)
+OUT = HERE
+
+
+def checksum(t):
+    a = t.detach().double().reshape(-1)
+    return np.array([a.sum().item(), (a * a).sum().item(), a.abs().max().item()], np.float64)
+
+
+def grad_table(module):
+    names, sums, heads = [], [], []
+    for n, p in module.named_parameters():
+        if p.grad is None:
+            continue
+        names.append(n)
+        sums.append(checksum(p.grad))
+        h = np.zeros(4, np.float64)
+        g = p.grad.detach().double().reshape(-1)[:4].numpy()
+        h[: len(g)] = g
+        heads.append(h)
+    return np.array(names), np.stack(sums), np.stack(heads)
+
+
+@contextlib.contextmanager
+def injected(rng):
+    """Replace the reference's RNG call sites by queues of pre-drawn values."""
+    q_int = [torch.from_numpy(x) for x in rng.get("randint", [])]
+    q_nrm = [torch.from_numpy(x) for x in rng.get("randn_like", [])]
+    q_eps = [torch.from_numpy(rng[k]) for k in ("vae_eps_x", "vae_eps_c") if k in rng]
+    saved = (torch.randint, torch.randn_like, torch.randn, torch.rand, random.choice,
+             ref_mar.MAR.sample_orders)
+
+    def fake_randint(*a, **k):
+        v = q_int.pop(0)
+        assert tuple(a[2]) == tuple(v.shape), (a, v.shape)
+        return v
+
+    def fake_randn_like(x, *a, **k):
+        v = q_nrm.pop(0)
+        assert v.shape == x.shape, (v.shape, x.shape)
+        return v.to(x.dtype)
+
+    def fake_randn(*shape, **k):
+        v = q_eps.pop(0)
+        shp = shape[0] if len(shape) == 1 and not isinstance(shape[0], int) else shape
+        assert tuple(shp) == tuple(v.shape), (shp, v.shape)
+        return v
+
+    def fake_rand(*shape, **k):
+        return torch.from_numpy(rng["text_drop_u"])
+
+    torch.randint, torch.randn_like, torch.randn, torch.rand = (
+        fake_randint, fake_randn_like, fake_randn, fake_rand)
+    if "task_mode" in rng:
+        random.choice = lambda seq: rng["task_mode"]
+    ref_mar.MAR.sample_orders = lambda self, bsz: torch.from_numpy(rng["orders"])
+    try:
+        yield
+    finally:
+        (torch.randint, torch.randn_like, torch.randn, torch.rand, random.choice,
+         ref_mar.MAR.sample_orders) = saved
+    assert not q_int and not q_nrm and not q_eps, "unconsumed injected draws"
+
+
+def build_mar(variant):
+    m = ref_mar.MAR(norm_layer=partial(nn.LayerNorm, eps=1e-6), **cases.MAR_GOLDEN,
+                    **cases.mar_kwargs(variant))
+    hash_init_(m, "mar.")
+    m.train()
+    return m
+
+
+def mar_call(m, variant, mode, inp):
+    v = cases.VARIANTS[variant]
+    t = {k: torch.from_numpy(x) for k, x in inp.items()}
+    prop = {}
+    if v["use_proprioception"]:
+        prop = {k: t[k] for k in t if k.startswith("robot0_")}
+    return m(t["z"], t["c"], None, t["nactions"], t.get("text_latents"), task_mode=mode,
+             proprioception_input=prop)
+
+
+def gen_mar():
+    for variant, v in cases.VARIANTS.items():
+        inp = cases.mar_inputs(variant)
+        for mode in v["modes"]:
+            m = build_mar(variant)
+            rng = cases.mar_rng(variant, mode)
+            m.mask_ratio_generator = type("G", (), {"rvs": staticmethod(
+                lambda n, r=rng["mask_rate"]: np.array([r]))})()
+            with injected(rng):
+                loss, lv, la = mar_call(m, variant, mode, inp)
+            loss.backward()
+            names, sums, heads = grad_table(m)
+            np.savez(os.path.join(OUT, f"g2_mar_{variant}_{mode}.npz"),
+                     loss=np.array([loss.item(), lv.item(), la.item()], np.float64),
+                     grad_names=names, grad_sums=sums, grad_heads=heads)
+            print(f"mar {variant} {mode}: loss={loss.item():.6f} Lv={lv.item():.6f} "
+                  f"La={la.item():.6f} ngrads={len(names)}")
+
+
+def gen_indexing():
+    d = {}
+    x = torch.arange(32).float().reshape(1, 32, 1, 1, 1)
+    _, idx = data_utils.select_frames(x, 32, eval=False)
+    d["frames_train"] = idx.numpy()
+    _, idx = data_utils.select_frames(x, 32, eval=True)
+    d["frames_eval"] = idx.numpy()
+    d["history_combinations"] = np.array(data_utils.combinations, np.int64)
+    na = torch.arange(32 * 3).float().reshape(1, 32, 3)
+    h, tr = data_utils.get_trajectory(na, 32, True)
+    d["traj_shift"] = tr.numpy()
+    h, tr = data_utils.get_trajectory(na, 32, False)
+    d["traj_noshift_hist"], d["traj_noshift"] = h.numpy(), tr.numpy()
+    # masks for every (orders, rate) golden case
+    m = build_mar("pusht")
+    for mode in cases.ALL_MODES:
+        rng = cases.mar_rng("pusht", mode)
+        m.mask_ratio_generator = type("G", (), {"rvs": staticmethod(
+            lambda n, r=rng["mask_rate"]: np.array([r]))})()
+        mask = m.random_masking(torch.zeros(2, 4, 256, 8), torch.from_numpy(rng["orders"]))
+        d[f"mask_{mode}"] = mask.numpy().astype(np.uint8)
+    img = torch.arange(2 * 16 * 16 * 16).float().reshape(2, 16, 16, 16)
+    d["patchify"] = m.patchify(img).numpy()
+    np.savez(os.path.join(OUT, "g1_indexing.npz"), **d)
+    print("indexing done")
+
+
+def gen_block():
+    from ref_shims import Block
+    d = {}
+    for n_tok in (1024, 1088):
+        blk = Block(768, 12, 4.0, qkv_bias=True, norm_layer=partial(nn.LayerNorm, eps=1e-6))
+        hash_init_(blk, "blk.")
+        x = torch.from_numpy(hash_normal(f"blk/x{n_tok}", (2, n_tok, 768))).requires_grad_(True)
+        y = blk(x)
+        gy = torch.from_numpy(hash_normal(f"blk/gy{n_tok}", (2, n_tok, 768)))
+        y.backward(gy)
+        names, sums, heads = grad_table(blk)
+        d[f"y{n_tok}"] = checksum(y)
+        d[f"y{n_tok}_rows"] = y.detach()[:, ::97].numpy()
+        d[f"gx{n_tok}"] = checksum(x.grad)
+        d[f"gx{n_tok}_rows"] = x.grad[:, ::97].numpy()
+        d[f"gnames{n_tok}"], d[f"gsums{n_tok}"], d[f"gheads{n_tok}"] = names, sums, heads
+    np.savez(os.path.join(OUT, "g3_block.npz"), **d)
+    print("block done")
+
+
+def gen_mlp():
+    net = SimpleMLPAdaLN(16, 1024, 32, 768, 6)
+    hash_init_(net, "mlp.")
+    rows = 512
+    x = torch.from_numpy(hash_normal("mlp/x", (rows, 16))).requires_grad_(True)
+    c = torch.from_numpy(hash_normal("mlp/c", (rows, 768))).requires_grad_(True)
+    t = torch.from_numpy(cases.t_steps("mlp", rows))
+    y = net(x, t, c)
+    gy = torch.from_numpy(hash_normal("mlp/gy", (rows, 32)))
+    y.backward(gy)
+    names, sums, heads = grad_table(net)
+    np.savez(os.path.join(OUT, "g3_mlp.npz"), y=y.detach().numpy(), gx=x.grad.numpy(),
+             gc=checksum(c.grad), gc_rows=c.grad[::16].numpy(), gnames=names, gsums=sums, gheads=heads)
+    print("mlp done")
+
+
+def gen_diffusion_math():
+    d = {}
+    for tag, C in (("video", 16), ("act", 2), ("act10", 10)):
+        diff = create_diffusion(timestep_respacing="", noise_schedule="cosine")
+        rows = 512
+        x0 = torch.from_numpy(hash_tensor(f"dm/{tag}/x0", (rows, C)))
+        out = torch.from_numpy(hash_tensor(f"dm/{tag}/out", (rows, 2 * C)))
+        t = torch.from_numpy(cases.t_steps(f"dm/{tag}", rows))
+        noise = torch.from_numpy(hash_normal(f"dm/{tag}/noise", (rows, C)))
+        out.requires_grad_(True)
+        terms = diff.training_losses(lambda xt, tt, **k: out, x0, t, {}, noise=noise)
+        terms["loss"].sum().backward()
+        d[f"{tag}_loss"] = terms["loss"].detach().numpy()
+        d[f"{tag}_mse"] = terms["mse"].detach().numpy()
+        d[f"{tag}_vb"] = terms["vb"].detach().numpy()
+        d[f"{tag}_gout"] = out.grad.numpy()
+    diff = create_diffusion(timestep_respacing="", noise_schedule="cosine")
+    for k in ("betas", "alphas_cumprod", "posterior_log_variance_clipped",
+              "posterior_mean_coef1", "posterior_mean_coef2", "sqrt_alphas_cumprod",
+              "sqrt_one_minus_alphas_cumprod"):
+        d[f"table_{k}"] = getattr(diff, k)
+    np.savez(os.path.join(OUT, "g3_diffusion_math.npz"), **d)
+    print("diffusion math done")
+
+
+def gen_vae():
+    class DD:
+        vae_embed_dim = 16
+        ch_mult = (1, 1, 2, 2, 4)
+
+    ae = vaekl.AutoencoderKL(autoencoder_path=None, ddconfig=DD())
+    hash_init_(ae, "vae.")
+    x = torch.from_numpy(hash_tensor("vae/x", (1, 3, 256, 256)))
+    eps = torch.from_numpy(hash_normal("vae/eps", (1, 16, 16, 16)))
+    with torch.no_grad():
+        h = ae.encoder(x)
+        moments = ae.quant_conv(h)
+        saved = torch.randn
+        torch.randn = lambda *s, **k: eps
+        try:
+            z = ae.encode(x).sample().mul_(0.2325)
+        finally:
+            torch.randn = saved
+    np.savez(os.path.join(OUT, "g3_vae.npz"), moments=moments.numpy(), z=z.numpy())
+    print("vae done")
+
+
+def gen_resize():
+    import torch.nn.functional as F
+    d = {}
+    for H in (96, 128, 224):
+        x = torch.from_numpy((hash_tensor(f"resize/{H}", (2, 3, H, H)) + 1) * 0.5)
+        y = F.interpolate(x, size=(256, 256), mode="bilinear", align_corners=False)
+        d[f"y{H}"] = checksum(y)
+        d[f"y{H}_rows"] = y[:, :, ::37].numpy()
+    np.savez(os.path.join(OUT, "g3_resize.npz"), **d)
+    print("resize done")
+
+
+def gen_ema():
+    ema = EMAModel(nn.Linear(2, 2), update_after_step=0, inv_gamma=1.0, power=0.75,
+                   min_value=0.0, max_value=0.9999)
+    dec = np.array([ema.get_decay(s) for s in range(2001)], np.float64)
+    np.savez(os.path.join(OUT, "g4_ema.npz"), decay=dec)
+    print("ema done")
+
+
+def gen_policy():
+    from unified_video_action.policy.unified_video_action_policy import UnifiedVideoActionPolicy
+    from unified_video_action.model.common.normalizer import LinearNormalizer
+
+    class AD(dict):
+        def __getattr__(self, k):
+            v = self[k]
+            return AD(v) if isinstance(v, dict) else v
+
+    ref_mar.mar_golden = lambda **kw: ref_mar.MAR(
+        norm_layer=partial(nn.LayerNorm, eps=1e-6), **cases.MAR_GOLDEN, **kw)
+    amp = dict(pretrained_model_path=None, model_size="mar_golden")
+    for k in ("img_size", "vae_stride", "patch_size", "vae_embed_dim", "mask_ratio_min",
+              "label_drop_prob", "attn_dropout", "proj_dropout", "diffloss_d", "diffloss_w",
+              "diffloss_act_d", "diffloss_act_w", "num_sampling_steps", "diffusion_batch_mul",
+              "grad_checkpointing", "predict_video", "act_diff_training_steps",
+              "act_diff_testing_steps"):
+        amp[k] = cases.MAR_KW[k]
+    out = {}
+    for mode in cases.POLICY_MODES:
+        pol = UnifiedVideoActionPolicy(
+            vae_model_params=AD(autoencoder_path=None,
+                                ddconfig=AD(vae_embed_dim=16, ch_mult=[1, 1, 2, 2, 4])),
+            autoregressive_model_params=AD(amp),
+            action_model_params=AD(predict_action=True, act_model_type="conv_fc"),
+            shape_meta=AD(action=AD(shape=[2])), n_action_steps=8, shift_action=True,
+            language_emb_model=None, task_name="pusht", task_modes=[],
+            normalizer_type="all", selected_training_mode=None, use_history_action=False,
+            use_proprioception=False, action_mask_ratio=0.5, different_history_freq=False,
+            predict_wrist_img=False, predict_proprioception=False, debug=False)
+        hash_init_(pol.vae_model, "vae.")
+        hash_init_(pol.model, "mar.")
+        pol.train()
+        norm = LinearNormalizer()
+        lim = torch.zeros(2, 2)
+        lim[1] = 512.0
+        norm.fit({"action": lim, "agent_pos": lim})
+        pol.set_normalizer(norm)
+        b = cases.policy_batch()
+        batch = {"obs": {"image": torch.from_numpy(b["image"]),
+                         "agent_pos": torch.from_numpy(b["agent_pos"])},
+                 "action": torch.from_numpy(b["action"])}
+
+        class Cfg:
+            class task:
+                name = "pusht"
+
+        batch = data_utils.resize_image(Cfg, batch)
+        rng = cases.policy_rng(mode)
+        rng["task_mode"] = mode
+        pol.model.mask_ratio_generator = type("G", (), {"rvs": staticmethod(
+            lambda n, r=rng["mask_rate"]: np.array([r]))})()
+        with injected(rng):
+            loss, (lv, la) = pol.compute_loss(batch)
+        loss.backward()
+        names, sums, heads = grad_table(pol.model)
+        out[f"{mode}_loss"] = np.array([loss.item(), lv.item(), la.item()], np.float64)
+        out[f"{mode}_gnames"], out[f"{mode}_gsums"], out[f"{mode}_gheads"] = names, sums, heads
+        dec, nod = pol.add_weight_decay(pol.model, 0.02)[1], None
+        print(f"policy {mode}: loss={loss.item():.6f} Lv={lv.item():.6f} La={la.item():.6f}")
+    decay_names = [n for n, p in pol.model.named_parameters()
+                   if p.requires_grad and not (len(p.shape) == 1 or n.endswith(".bias"))]
+    out["decay_names"] = np.array(decay_names)
+    np.savez(os.path.join(OUT, "g2_policy_pusht.npz"), **out)
+
+
+if __name__ == "__main__":
+    which = sys.argv[1:] or ["indexing", "mar", "block", "mlp", "diffusion_math", "vae",
+                             "resize", "ema", "policy"]
+    for w in which:
+        globals()[f"gen_{w}"]()

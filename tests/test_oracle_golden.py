@@ -1,0 +1,158 @@
+"""Pin the CPU oracle against the fixtures produced by the reference itself.
+
+Tolerances: fp32 loss 1e-4 relative (north_star); grads 1e-3 (checksum metric,
+replay.grad_rel_errors); bit-exact for every integer/index quantity.
+"""
+import math
+
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+import cases
+import replay
+import uva_oracle as O
+from hashinit import hash_init_, hash_normal, hash_tensor
+
+torch.set_num_threads(min(8, torch.get_num_threads()))
+
+
+def test_indexing_bit_exact():
+    g = replay.load("g1_indexing.npz")
+    assert np.array_equal(O.train_frame_indices().numpy(), g["frames_train"])
+    na = torch.arange(32 * 3).float().reshape(1, 32, 3)
+    assert np.array_equal(O.trajectory(na).numpy(), g["traj_shift"])
+    assert np.array_equal(O.trajectory(na, shift_action=False).numpy(), g["traj_noshift"])
+    for mode in cases.ALL_MODES:
+        rng = cases.mar_rng("pusht", mode)
+        m = O.MAR.token_mask(torch.from_numpy(rng["orders"]), rng["mask_rate"])
+        assert np.array_equal(m.numpy().astype(np.uint8), g[f"mask_{mode}"])
+        assert int(m[0, 0].sum()) == cases.num_masked(rng["mask_rate"])
+    img = torch.arange(2 * 16 * 16 * 16).float().reshape(2, 16, 16, 16)
+    assert np.array_equal(O.MAR.patchify(img).numpy(), g["patchify"])
+    # different_history_freq combinations: 4-tuples from range(16) ending in 15
+    combos = g["history_combinations"]
+    assert combos.shape == (816, 4) and (combos[:, -1] == 15).all()
+
+
+def test_diffusion_tables_and_math():
+    g = replay.load("g3_diffusion_math.npz")
+    tb = O.DiffusionTables(1000)
+    np.testing.assert_allclose(tb.betas, g["table_betas"], rtol=1e-12, atol=0)
+    np.testing.assert_allclose(tb.alphas_cumprod, g["table_alphas_cumprod"], rtol=1e-12)
+    np.testing.assert_allclose(tb.plvc, g["table_posterior_log_variance_clipped"], rtol=1e-12)
+    np.testing.assert_allclose(tb.coef1, g["table_posterior_mean_coef1"], rtol=1e-12)
+    np.testing.assert_allclose(tb.coef2, g["table_posterior_mean_coef2"], rtol=1e-12)
+    for tag, C in (("video", 16), ("act", 2), ("act10", 10)):
+        rows = 512
+        x0 = torch.from_numpy(hash_tensor(f"dm/{tag}/x0", (rows, C)))
+        out = torch.from_numpy(hash_tensor(f"dm/{tag}/out", (rows, 2 * C))).requires_grad_(True)
+        t = torch.from_numpy(cases.t_steps(f"dm/{tag}", rows))
+        noise = torch.from_numpy(hash_normal(f"dm/{tag}/noise", (rows, C)))
+        loss, mse, vb = O.diffusion_training_loss(tb, lambda xt, tt: out, x0, t, noise)
+        loss.sum().backward()
+        np.testing.assert_allclose(loss.detach().numpy(), g[f"{tag}_loss"], rtol=1e-5, atol=1e-5)
+        np.testing.assert_allclose(vb.detach().numpy(), g[f"{tag}_vb"], rtol=1e-5, atol=1e-5)
+        np.testing.assert_allclose(out.grad.numpy(), g[f"{tag}_gout"], rtol=1e-4, atol=1e-6)
+
+
+@pytest.mark.parametrize("variant,mode", [(v, m) for v in cases.VARIANTS
+                                          for m in cases.VARIANTS[v]["modes"]])
+def test_mar_loss_and_grads(variant, mode):
+    g = replay.load(f"g2_mar_{variant}_{mode}.npz")
+    m = O.MAR(**replay.mar_ctor_kwargs(variant))
+    hash_init_(m, "mar.")
+    inp, rng = replay.mar_case(variant, mode)
+    prop = {k: v for k, v in inp.items() if k.startswith("robot0_")} or None
+    loss, lv, la = m(inp["z"], inp["c"], inp["nactions"], inp.get("text_latents"), mode, rng, prop)
+    ref = g["loss"]
+    for got, want in zip((loss.item(), float(lv), float(la)), ref):
+        assert abs(got - want) <= 1e-4 * max(abs(want), 1e-6), (got, want)
+    loss.backward()
+    errs = replay.grad_rel_errors(m.named_parameters(), g, "grad_names", "grad_sums", "grad_heads")
+    worst = max(errs.items(), key=lambda kv: kv[1])
+    assert worst[1] < 3e-3, worst  # fp32 op-order noise; semantic errors are O(1)
+
+
+def test_block_full_geometry():
+    g = replay.load("g3_block.npz")
+    for n_tok in (1024, 1088):
+        blk = O.Block(768, 12)
+        hash_init_(blk, "blk.")
+        x = torch.from_numpy(hash_normal(f"blk/x{n_tok}", (2, n_tok, 768))).requires_grad_(True)
+        y = blk(x)
+        y.backward(torch.from_numpy(hash_normal(f"blk/gy{n_tok}", (2, n_tok, 768))))
+        np.testing.assert_allclose(y.detach()[:, ::97].numpy(), g[f"y{n_tok}_rows"], rtol=1e-4, atol=1e-4)
+        np.testing.assert_allclose(x.grad[:, ::97].numpy(), g[f"gx{n_tok}_rows"], rtol=1e-4, atol=1e-4)
+        errs = replay.grad_rel_errors(blk.named_parameters(), g, f"gnames{n_tok}",
+                                      f"gsums{n_tok}", f"gheads{n_tok}")
+        assert max(errs.values()) < 1e-3
+
+
+def test_diffusion_mlp():
+    g = replay.load("g3_mlp.npz")
+    net = O.SimpleMLPAdaLN(16, 1024, 32, 768, 6)
+    hash_init_(net, "mlp.")
+    x = torch.from_numpy(hash_normal("mlp/x", (512, 16))).requires_grad_(True)
+    c = torch.from_numpy(hash_normal("mlp/c", (512, 768))).requires_grad_(True)
+    t = torch.from_numpy(cases.t_steps("mlp", 512))
+    y = net(x, t, c)
+    y.backward(torch.from_numpy(hash_normal("mlp/gy", (512, 32))))
+    np.testing.assert_allclose(y.detach().numpy(), g["y"], rtol=1e-4, atol=1e-5)
+    np.testing.assert_allclose(x.grad.numpy(), g["gx"], rtol=1e-4, atol=1e-5)
+    np.testing.assert_allclose(c.grad[::16].numpy(), g["gc_rows"], rtol=1e-4, atol=1e-5)
+
+
+def test_vae_encoder_full_size():
+    g = replay.load("g3_vae.npz")
+    vae = O.AutoencoderKLEncoder()
+    hash_init_(vae, "vae.")
+    x = torch.from_numpy(hash_tensor("vae/x", (1, 3, 256, 256)))
+    eps = torch.from_numpy(hash_normal("vae/eps", (1, 16, 16, 16)))
+    with torch.no_grad():
+        mom = vae.moments(x)
+        z = vae.sample(x, eps)
+    np.testing.assert_allclose(mom.numpy(), g["moments"], rtol=1e-4, atol=1e-4)
+    np.testing.assert_allclose(z.numpy(), g["z"], rtol=1e-4, atol=1e-5)
+
+
+def test_resize():
+    g = replay.load("g3_resize.npz")
+    for H in (96, 128, 224):
+        x = torch.from_numpy((hash_tensor(f"resize/{H}", (2, 3, H, H)) + 1) * 0.5)
+        y = O.resize_256(x[:, None])[:, 0]
+        np.testing.assert_allclose(y[:, :, ::37].numpy(), g[f"y{H}_rows"], rtol=1e-6, atol=1e-6)
+
+
+def test_ema_decay_and_lr():
+    g = replay.load("g4_ema.npz")
+    got = np.array([O.ema_decay(s) for s in range(2001)])
+    np.testing.assert_allclose(got, g["decay"], rtol=0, atol=0)
+    # LR: diffusers absent -> restatement only (parity unpinned); sanity of the shape
+    assert O.cosine_lr_factor(0, 1000, 10000) == 0.0
+    assert O.cosine_lr_factor(1000, 1000, 10000) == pytest.approx(1.0)
+    assert O.cosine_lr_factor(10000, 1000, 10000) == pytest.approx(0.0, abs=1e-12)
+
+
+def test_policy_compute_loss_end_to_end():
+    """resize -> normalize -> frame select -> full-size VAE -> reduced MAR -> loss+grads."""
+    g = replay.load("g2_policy_pusht.npz")
+    for mode in cases.POLICY_MODES:
+        mar = O.MAR(**replay.mar_ctor_kwargs("pusht"))
+        hash_init_(mar, "mar.")
+        vae = O.AutoencoderKLEncoder()
+        hash_init_(vae, "vae.")
+        pol = O.PolicyOracle(mar, vae, [2 / 512, 2 / 512], [-1.0, -1.0])
+        b = cases.policy_batch()
+        rng = cases.policy_rng(mode)
+        loss, (lv, la) = pol.compute_loss(torch.from_numpy(b["image"]),
+                                          torch.from_numpy(b["action"]), mode, rng)
+        for got, want in zip((loss.item(), float(lv), float(la)), g[f"{mode}_loss"]):
+            assert abs(got - want) <= 1e-4 * max(abs(want), 1e-6), (mode, got, want)
+        loss.backward()
+        errs = replay.grad_rel_errors(mar.named_parameters(), g, f"{mode}_gnames",
+                                      f"{mode}_gsums", f"{mode}_gheads")
+        assert max(errs.values()) < 1e-3, max(errs.items(), key=lambda kv: kv[1])
+    decay, _ = O.weight_decay_split(mar.named_parameters())
+    assert decay == [str(n) for n in g["decay_names"]]
