@@ -1,0 +1,265 @@
+"""Unit numerics of every HIP kernel against a plain PyTorch fp32 reference of the same op
+(or the oracle, for the diffusion math).  Tolerances are written per test:
+fp32 kernels 1e-5..1e-4 relative; bf16-input kernels are compared with the fp32
+reference of the SAME bf16-rounded inputs, tolerance 2e-2 relative to the output scale."""
+import math
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _lib():
+    from unified_video_action_amd.native import ops  # noqa: F401 -- fails loudly without the .so
+    torch.manual_seed(0)
+
+
+def rel_err(a, b):
+    a, b = a.double(), b.double()
+    return ((a - b).abs().max() / (b.abs().max() + 1e-12)).item()
+
+
+def _stored(op, t_flag):
+    """stored layout of an [R, K] logical operand."""
+    return op.t().contiguous() if t_flag else op.contiguous()
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("ta,tb", [(0, 0), (0, 1), (1, 0), (1, 1)])
+@pytest.mark.parametrize("M,N,K", [(256, 384, 192), (300, 200, 72), (130, 136, 520), (64, 48, 2)])
+def test_gemm_layouts(dtype, ta, tb, M, N, K):
+    from unified_video_action_amd.native import ops
+    if dtype == torch.bfloat16 and ((ta and M % 8) or (tb and N % 8)):
+        pytest.skip("m-contiguous bf16 operands need 8-aligned dims (host pads these)")
+    a = torch.randn(M, K, device=DEV).to(dtype)
+    b = torch.randn(N, K, device=DEV).to(dtype)
+    A, B = _stored(a, ta), _stored(b, tb)
+    C = torch.empty(M, N, device=DEV, dtype=torch.float32)
+    ops.gemm(A, B, C, M, N, K, A.stride(0), B.stride(0), C.stride(0), ta, tb)
+    ref = a.float() @ b.float().t()
+    tol = 1e-5 if dtype == torch.float32 else 5e-3
+    assert rel_err(C, ref) < tol
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_gemm_epilogue_bias_gelu_aux_residual_beta(dtype):
+    from unified_video_action_amd.native import ops
+    M, N, K = 512, 256, 128
+    x = torch.randn(M, K, device=DEV).to(dtype)
+    w = torch.randn(N, K, device=DEV).to(dtype) * 0.1
+    bias = torch.randn(N, device=DEV)
+    out = torch.empty(M, N, device=DEV, dtype=dtype)
+    aux = torch.empty_like(out)
+    ops.linear(x, w, out, bias=bias, act="gelu", aux=aux)
+    pre = x.float() @ w.float().t() + bias
+    tol = 1e-5 if dtype == torch.float32 else 2e-2
+    assert rel_err(aux.float(), pre) < tol
+    assert rel_err(out.float(), torch.nn.functional.gelu(pre)) < tol
+    # residual + beta accumulate, fp32 output
+    res = torch.randn(M, N, device=DEV)
+    c = torch.randn(M, N, device=DEV)
+    c0 = c.clone()
+    ops.gemm(x, w, c, M, N, K, K, K, N, 0, 0, residual=res, ldr=N, beta=1.0)
+    assert rel_err(c, c0 + res + x.float() @ w.float().t()) < (1e-5 if dtype == torch.float32 else 1e-2)
+
+
+def test_gemm_dropout_matches_act_bwd_mask():
+    from unified_video_action_amd.native import ops
+    M, N, K = 256, 512, 64
+    x = torch.randn(M, K, device=DEV)
+    w = torch.randn(N, K, device=DEV)
+    out = torch.empty(M, N, device=DEV)
+    ops.linear(x, w, out, drop_p=0.1, seed=1234)
+    ref = x @ w.t()
+    kept = out != 0
+    frac = kept.float().mean().item()
+    assert abs(frac - 0.9) < 0.01
+    assert rel_err(out[kept], ref[kept] / 0.9) < 1e-5
+    # backward mask (act none) reproduces the same keep pattern
+    g = torch.ones(M, N, device=DEV)
+    dg = torch.empty(M, N, device=DEV)
+    ops.act_bwd(None, g, dg, "none", drop_p=0.1, seed=1234)
+    assert torch.equal(dg != 0, kept)
+
+
+def test_gemm_batched_two_level_strides():
+    from unified_video_action_amd.native import ops
+    Bn, H, N, Dh = 2, 3, 96, 64
+    qkv = torch.randn(Bn, N, 3, H, Dh, device=DEV).to(torch.bfloat16)
+    S = torch.empty(Bn, H, N, N, device=DEV, dtype=torch.float32)
+    q = qkv[:, :, 0]
+    k = qkv[:, :, 1]
+    ld = 3 * H * Dh
+    ops.gemm(q, k, S, N, N, Dh, ld, ld, N, 0, 0, batch=Bn * H, inner=H, sA=(N * ld, Dh), sB=(N * ld, Dh),
+             sC=(H * N * N, N * N))
+    ref = torch.einsum("bihd,bjhd->bhij", q.float(), k.float())
+    assert rel_err(S, ref) < 5e-3
+
+
+@pytest.mark.parametrize("D", [64, 128, 768, 1024])
+@pytest.mark.parametrize("io", [(torch.float32, torch.float32), (torch.float32, torch.bfloat16)])
+def test_layernorm_affine_fwd_bwd(D, io):
+    from unified_video_action_amd.native import ops
+    tin, tout = io
+    rows = 300
+    x = torch.randn(rows, D, device=DEV).to(tin)
+    w = torch.randn(D, device=DEV) * 0.1 + 1
+    b = torch.randn(D, device=DEV) * 0.1
+    y = torch.empty(rows, D, device=DEV, dtype=tout)
+    mean = torch.empty(rows, device=DEV)
+    rstd = torch.empty(rows, device=DEV)
+    ops.layernorm_fwd(x, w, b, y, mean, rstd)
+    xr = x.float().clone().requires_grad_(True)
+    wr, br = w.clone().requires_grad_(True), b.clone().requires_grad_(True)
+    yr = torch.nn.functional.layer_norm(xr, (D,), wr, br, eps=1e-6)
+    tol = 1e-5 if tout == torch.float32 else 1e-2
+    assert rel_err(y.float(), yr) < tol
+    dy = torch.randn(rows, D, device=DEV)
+    yr.backward(dy)
+    dx = torch.full((rows, D), 0.5, device=DEV)
+    dw = torch.zeros(D, device=DEV)
+    db = torch.zeros(D, device=DEV)
+    ops.layernorm_bwd(x, w, dy, mean, rstd, dx, accum=True, dw=dw, db=db)
+    assert rel_err(dx - 0.5, xr.grad) < 1e-4
+    assert rel_err(dw, wr.grad) < 1e-4
+    assert rel_err(db, br.grad) < 1e-4
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_layernorm_modulated_fwd_bwd(dtype):
+    from unified_video_action_amd.native import ops
+    rows, D = 257, 1024
+    x = torch.randn(rows, D, device=DEV)
+    mod = (torch.randn(rows, 3 * D, device=DEV) * 0.3).to(dtype)
+    shift, scale = mod[:, :D], mod[:, D:2 * D]
+    y = torch.empty(rows, D, device=DEV, dtype=dtype)
+    mean = torch.empty(rows, device=DEV)
+    rstd = torch.empty(rows, device=DEV)
+    ops.layernorm_fwd(x, None, None, y, mean, rstd, scale=scale, shift=shift, ldm=3 * D)
+    xr = x.clone().requires_grad_(True)
+    sc = scale.float().clone().requires_grad_(True)
+    sh = shift.float().clone().requires_grad_(True)
+    yr = torch.nn.functional.layer_norm(xr, (D,), eps=1e-6) * (1 + sc) + sh
+    tol = 1e-5 if dtype == torch.float32 else 1e-2
+    assert rel_err(y.float(), yr) < tol
+    dy = torch.randn(rows, D, device=DEV)
+    yr.backward(dy)
+    dx = torch.empty(rows, D, device=DEV)
+    dmod = torch.zeros(rows, 3 * D, device=DEV, dtype=dtype)
+    ops.layernorm_bwd(x, None, dy, mean, rstd, dx, accum=False, scale=scale, ldm=3 * D,
+                      dscale=dmod[:, D:2 * D], dshift=dmod[:, :D])
+    assert rel_err(dx, xr.grad) < (1e-4 if dtype == torch.float32 else 2e-2)
+    assert rel_err(dmod[:, D:2 * D].float(), sc.grad) < tol
+    assert rel_err(dmod[:, :D].float(), sh.grad) < tol
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_softmax_fwd_bwd(dtype):
+    from unified_video_action_amd.native import ops
+    rows, L = 96, 1088
+    S = torch.randn(rows, L, device=DEV).to(dtype) * 3
+    P = torch.empty_like(S)
+    ops.softmax_fwd(S, P, None, L, 0.125)
+    Sr = S.float().clone().requires_grad_(True)
+    Pr = torch.softmax(Sr * 0.125, dim=-1)
+    tol = 1e-5 if dtype == torch.float32 else 1e-2
+    assert rel_err(P.float(), Pr) < tol
+    dP = torch.randn(rows, L, device=DEV).to(dtype)
+    Pr.backward(dP.float())
+    dS = torch.empty_like(S)
+    ops.softmax_bwd(P, dP, dS, L, 0.125)
+    assert rel_err(dS.float(), Sr.grad) < (1e-4 if dtype == torch.float32 else 3e-2)
+
+
+def test_colsum_and_cast():
+    from unified_video_action_amd.native import ops
+    x = torch.randn(5000, 300, device=DEV)
+    out = torch.ones(300, device=DEV)
+    ops.colsum(x, out, accum=True)
+    assert rel_err(out - 1, x.sum(0)) < 1e-5
+    xb = torch.empty(5000, 300, device=DEV, dtype=torch.bfloat16)
+    ops.cast(x, xb)
+    assert torch.equal(xb, x.to(torch.bfloat16))
+
+
+def test_act_fwd_bwd():
+    from unified_video_action_amd.native import ops
+    x = torch.randn(1000, 64, device=DEV)
+    for act, fn in (("silu", torch.nn.functional.silu), ("gelu", torch.nn.functional.gelu),
+                    ("relu", torch.relu)):
+        y = torch.empty_like(x)
+        ops.act_fwd(x, y, act)
+        assert rel_err(y, fn(x)) < 1e-5
+        xr = x.clone().requires_grad_(True)
+        dy = torch.randn_like(x)
+        fn(xr).backward(dy)
+        dx = torch.empty_like(x)
+        ops.act_bwd(x, dy, dx, act)
+        assert rel_err(dx, xr.grad) < 1e-5
+
+
+def test_diffusion_loss_matches_oracle_golden():
+    import cases
+    import replay
+    import uva_oracle as O
+    from hashinit import hash_normal, hash_tensor
+    from unified_video_action_amd.native import ops
+    from unified_video_action_amd.model.autoregressive.diffusion import DiffusionSchedule
+    g = replay.load("g3_diffusion_math.npz")
+    sched = DiffusionSchedule(1000, DEV)
+    for tag, C in (("video", 16), ("act", 2), ("act10", 10)):
+        rows = 512
+        x0 = torch.from_numpy(hash_tensor(f"dm/{tag}/x0", (rows, C))).to(DEV)
+        out = torch.from_numpy(hash_tensor(f"dm/{tag}/out", (rows, 2 * C))).to(DEV)
+        t = torch.from_numpy(cases.t_steps(f"dm/{tag}", rows)).to(DEV)
+        noise = torch.from_numpy(hash_normal(f"dm/{tag}/noise", (rows, C))).to(DEV)
+        lr = torch.empty(rows, device=DEV)
+        dl = torch.empty(rows, 2 * C, device=DEV)
+        ops.diffusion_loss(x0, noise, t, out, sched.tables, lr, dl)
+        np.testing.assert_allclose(lr.cpu().numpy(), g[f"{tag}_loss"], rtol=1e-4, atol=1e-5)
+        np.testing.assert_allclose(dl.cpu().numpy(), g[f"{tag}_gout"], rtol=1e-3, atol=1e-6)
+        xt = torch.empty(rows, C, device=DEV)
+        ops.q_sample(x0, noise, t, sched.tables, xt)
+        tb = O.DiffusionTables(1000)
+        ref = tb.gather("sqrt_ac", t.cpu()) * x0.cpu() + tb.gather("sqrt_1mac", t.cpu()) * noise.cpu()
+        assert rel_err(xt.cpu(), ref) < 1e-6
+
+
+def test_timestep_features():
+    import uva_oracle as O
+    from unified_video_action_amd.native import ops
+    from unified_video_action_amd.model.autoregressive.diffusion import timestep_freqs
+    t = torch.arange(0, 1000, 7, device=DEV)
+    out = torch.empty(t.numel(), 256, device=DEV)
+    ops.timestep_features(t, timestep_freqs(DEV), out)
+    ref = O.timestep_features(t.cpu())
+    assert (out.cpu() - ref).abs().max().item() < 2e-5
+
+
+def test_adamw_ema_matches_torch():
+    from unified_video_action_amd.native import ops
+    n, n_decay = 10000, 6000
+    p0 = torch.randn(n, device=DEV)
+    pa, pb = p0[:n_decay].clone(), p0[n_decay:].clone()
+    opt = torch.optim.AdamW([{"params": [pa], "weight_decay": 0.02},
+                             {"params": [pb], "weight_decay": 0.0}], lr=1e-3, betas=(0.9, 0.95))
+    p = p0.clone()
+    m = torch.zeros(n, device=DEV)
+    v = torch.zeros(n, device=DEV)
+    ema = p0.clone()
+    pbf = torch.empty(n, device=DEV, dtype=torch.bfloat16)
+    ema_ref = p0.clone()
+    for step in range(1, 4):
+        g = torch.randn(n, device=DEV)
+        pa.grad, pb.grad = g[:n_decay].clone(), g[n_decay:].clone()
+        opt.step()
+        ops.adamw_ema(p, g * 2.0, m, v, ema, pbf, n_decay, 1e-3, 0.9, 0.95, 1e-8, 0.02, step, 0.5, 0.7)
+        ema_ref = ema_ref * 0.7 + torch.cat([pa, pb]).detach() * 0.3
+        assert rel_err(p, torch.cat([pa, pb]).detach()) < 1e-6
+    assert rel_err(ema, ema_ref) < 1e-6
+    assert torch.equal(pbf, p.to(torch.bfloat16))

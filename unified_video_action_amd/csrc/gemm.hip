@@ -1,0 +1,354 @@
+// Dense contractions for the UVA training step: every nn.Linear forward/backward,
+// the materialised attention products of the fp32 parity path and of the VAE
+// mid-block attention, and im2col convolutions.
+//
+//   C[z][m][n] = epilogue( alpha * sum_k opA[z][m][k] * opB[z][n][k] )
+//   ta = 0: A stored [M][K] (lda)       ta = 1: A stored [K][M]
+//   tb = 0: B stored [N][K] (ldb)       tb = 1: B stored [K][N]
+// so Linear fwd = (ta0,tb0), dX = (ta0,tb1), dW = (ta1,tb1).
+//
+// Two kernels:
+//  * gemm_mfma_bf16  -- bf16 in, fp32 accumulate on v_mfma_f32_16x16x32_bf16;
+//    128x128x64 block tile, 4 waves of 64x64, register-staged double-buffered LDS
+//    (loads for tile k+1 issued before the MFMAs of tile k, written after), XOR
+//    swizzled K-major images read with ds_read_b128 and M-major images read with
+//    ds_read_b64_tr_b16 (hardware transpose) so no operand is ever transposed in HBM.
+//  * gemm_generic    -- fp32 FMA on the VALU, any shape / dtype; the fp32 parity
+//    path and the tiny-K/N projections (K = 2, 4, 10 ...).
+#include "common.h"
+
+struct EpiParams {
+  const float* bias;      // [N] fp32 or null
+  const void* residual;   // same dtype/layout as C (ldr) or null
+  void* aux;              // pre-activation copy (dtype of C, ldc) or null
+  int act;
+  float alpha, beta;
+  uint32_t drop_thresh;   // 0 => no dropout
+  float drop_scale;
+  uint64_t drop_seed;
+  long long ldr;
+  long long sRo, sRi;     // residual batch strides
+};
+
+struct BatchStrides {
+  long long sAo, sAi, sBo, sBi, sCo, sCi;
+  int binner;
+};
+
+template <typename TC>
+__device__ __forceinline__ void epi_store(TC* C, long long ldc, long long coff, const EpiParams& ep,
+                                          long long roff, int row, int col, int N, long long didx, float acc) {
+  float v = ep.alpha * acc;
+  if (ep.bias) v += ep.bias[col];
+  long long ci = coff + (long long)row * ldc + col;
+  if (ep.aux) ((TC*)ep.aux)[ci] = from_f32<TC>(v);
+  v = apply_act(ep.act, v);
+  if (ep.drop_thresh) v = dropout_keep(ep.drop_seed, (uint64_t)didx, ep.drop_thresh) ? v * ep.drop_scale : 0.f;
+  if (ep.residual) v += to_f32(((const TC*)ep.residual)[roff + (long long)row * ep.ldr + col]);
+  if (ep.beta != 0.f) v += ep.beta * to_f32(C[ci]);
+  C[ci] = from_f32<TC>(v);
+}
+
+// =====================================================================================
+// generic VALU kernel: 64x64 tile, BK=16, 256 threads x (4x4) outputs
+// =====================================================================================
+template <typename TI, typename TC, int TA, int TB>
+__global__ __launch_bounds__(256) void gemm_generic(const TI* __restrict__ A, const TI* __restrict__ B,
+                                                    TC* __restrict__ C, int M, int N, int K, long long lda,
+                                                    long long ldb, long long ldc, BatchStrides bs, EpiParams ep) {
+  __shared__ float As[16][64 + 4];
+  __shared__ float Bs[16][64 + 4];
+  const int z = blockIdx.z, zo = z / bs.binner, zi = z % bs.binner;
+  A += zo * bs.sAo + zi * bs.sAi;
+  B += zo * bs.sBo + zi * bs.sBi;
+  const long long coff = zo * bs.sCo + zi * bs.sCi;
+  const long long roff = zo * ep.sRo + zi * ep.sRi;
+  const int m0 = blockIdx.y * 64, n0 = blockIdx.x * 64;
+  const int t = threadIdx.x, tx = t & 15, ty = t >> 4;
+  float acc[4][4] = {};
+  for (int k0 = 0; k0 < K; k0 += 16) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      int e = t + i * 256;  // 0..1023 over a 64x16 tile
+      int mm, kk;
+      if (TA == 0) { mm = e >> 4; kk = e & 15; } else { kk = e >> 6; mm = e & 63; }
+      int gm = m0 + mm, gk = k0 + kk;
+      float v = 0.f;
+      if (gm < M && gk < K) v = to_f32(TA == 0 ? A[(long long)gm * lda + gk] : A[(long long)gk * lda + gm]);
+      As[kk][mm] = v;
+      int nn;
+      if (TB == 0) { nn = e >> 4; kk = e & 15; } else { kk = e >> 6; nn = e & 63; }
+      int gn = n0 + nn;
+      gk = k0 + kk;
+      v = 0.f;
+      if (gn < N && gk < K) v = to_f32(TB == 0 ? B[(long long)gn * ldb + gk] : B[(long long)gk * ldb + gn]);
+      Bs[kk][nn] = v;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int kk = 0; kk < 16; ++kk) {
+      float a[4], b[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) { a[i] = As[kk][ty * 4 + i]; b[i] = Bs[kk][tx * 4 + i]; }
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = fmaf(a[i], b[j], acc[i][j]);
+    }
+    __syncthreads();
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      int r = m0 + ty * 4 + i, c = n0 + tx * 4 + j;
+      if (r < M && c < N)
+        epi_store<TC>(C, ldc, coff, ep, roff, r, c, N, (long long)z * M * N + (long long)r * N + c, acc[i][j]);
+    }
+}
+
+// =====================================================================================
+// MFMA bf16 kernel
+// =====================================================================================
+#define MB_M 128
+#define MB_N 128
+#define MB_K 64
+#define LDK_ROW 64    // K-major image: [rows][64] bf16, 16-B chunks XOR-swizzled by row
+#define LDM_ROW 144   // M-major image: [64 k][128 rows + 16 pad] bf16, column XOR 64 by k bit 3
+#define STAGE_K_ELEMS (MB_M * LDK_ROW)
+#define STAGE_M_ELEMS (MB_K * LDM_ROW)
+
+template <int T>
+struct OperandImage {
+  static constexpr int elems = (T == 0) ? STAGE_K_ELEMS : STAGE_M_ELEMS;
+};
+
+// global -> registers for one 128x64 operand tile (4 chunks of 8 bf16 per thread)
+template <int T>
+__device__ __forceinline__ void tile_load(const bf16* __restrict__ P, long long ld, int row0, int nrows, int k0, int K,
+                                          bf16x8 (&r)[4]) {
+  const int t = threadIdx.x;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    int id = t + i * 256;
+    int row, k;
+    if (T == 0) { row = id >> 3; k = (id & 7) * 8; } else { k = id >> 4; row = (id & 15) * 8; }
+    int gr = row0 + row, gk = k0 + k;
+    bool ok = (T == 0) ? (gr < nrows && gk < K) : (gr < nrows && gk < K);
+    if (ok) {
+      const bf16* src = (T == 0) ? P + (long long)gr * ld + gk : P + (long long)gk * ld + gr;
+      r[i] = *(const bf16x8*)src;
+    } else {
+      r[i] = (bf16x8){};
+    }
+  }
+}
+
+template <int T>
+__device__ __forceinline__ void tile_store(bf16* lds, const bf16x8 (&r)[4]) {
+  const int t = threadIdx.x;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    int id = t + i * 256;
+    if (T == 0) {
+      int row = id >> 3, c = id & 7;
+      *(bf16x8*)(lds + row * LDK_ROW + ((c ^ (row & 7)) * 8)) = r[i];
+    } else {
+      int k = id >> 4, col = (id & 15) * 8;
+      *(bf16x8*)(lds + k * LDM_ROW + (col ^ ((k & 8) << 3))) = r[i];
+    }
+  }
+}
+
+// MFMA 16x16x32 operand fragment: rows row0..row0+15 (lane&15), k = ks*32 + 8*(lane>>4) + j
+template <int T>
+__device__ __forceinline__ bf16x8 frag_load(const bf16* lds, int row0, int ks) {
+  const int l = threadIdx.x & 63;
+  if (T == 0) {
+    int row = row0 + (l & 15);
+    int c = ks * 4 + (l >> 4);
+    return *(const bf16x8*)(lds + row * LDK_ROW + ((c ^ (row & 7)) * 8));
+  } else {
+    const int g = l >> 4, q = (l >> 2) & 3, p = l & 3;
+    int k = ks * 32 + g * 8 + q;
+    int col = row0 + 4 * p;
+    const bf16* a0 = lds + k * LDM_ROW + (col ^ ((k & 8) << 3));
+    const bf16* a1 = lds + (k + 4) * LDM_ROW + (col ^ (((k + 4) & 8) << 3));
+    s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(s16x4, a0));
+    s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(s16x4, a1));
+    s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+    return __builtin_bit_cast(bf16x8, v);
+  }
+}
+
+__device__ __forceinline__ int xcd_remap(int bid, int nblk) {
+  // bijective: blocks that share an XCD (bid % 8) get a contiguous range of logical ids
+  int q = nblk / 8, r = nblk % 8, x = bid % 8;
+  return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + bid / 8;
+}
+
+template <int TA, int TB, typename TC>
+__global__ __launch_bounds__(256, 2) void gemm_mfma_bf16(const bf16* __restrict__ A, const bf16* __restrict__ B,
+                                                         TC* __restrict__ C, int M, int N, int K, long long lda,
+                                                         long long ldb, long long ldc, BatchStrides bs,
+                                                         EpiParams ep) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  bf16* sA = (bf16*)smem;
+  bf16* sB = sA + 2 * OperandImage<TA>::elems;
+  const int z = blockIdx.z, zo = z / bs.binner, zi = z % bs.binner;
+  A += zo * bs.sAo + zi * bs.sAi;
+  B += zo * bs.sBo + zi * bs.sBi;
+  const long long coff = zo * bs.sCo + zi * bs.sCi;
+  const long long roff = zo * ep.sRo + zi * ep.sRi;
+
+  // tile order: XCD-contiguous logical ids, then groups of 8 row-tiles share B panels
+  const int tm = (M + MB_M - 1) / MB_M, tn = (N + MB_N - 1) / MB_N;
+  const int nblk = tm * tn;
+  int pid = xcd_remap(blockIdx.x, nblk);
+  const int GROUP = 8;
+  int group = pid / (GROUP * tn), first_m = group * GROUP;
+  int gsz = min(tm - first_m, GROUP);
+  int bm = first_m + (pid % (GROUP * tn)) % gsz;
+  int bn = (pid % (GROUP * tn)) / gsz;
+  const int m0 = bm * MB_M, n0 = bn * MB_N;
+
+  const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int wm = wid >> 1, wn = wid & 1;
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+  bf16x8 ra[4], rb[4];
+  const int nk = (K + MB_K - 1) / MB_K;
+  tile_load<TA>(A, lda, m0, M, 0, K, ra);
+  tile_load<TB>(B, ldb, n0, N, 0, K, rb);
+  tile_store<TA>(sA, ra);
+  tile_store<TB>(sB, rb);
+  __syncthreads();
+  int cur = 0;
+  for (int kt = 0; kt < nk; ++kt) {
+    const bool more = kt + 1 < nk;
+    if (more) {
+      tile_load<TA>(A, lda, m0, M, (kt + 1) * MB_K, K, ra);
+      tile_load<TB>(B, ldb, n0, N, (kt + 1) * MB_K, K, rb);
+    }
+    const bf16* cA = sA + cur * OperandImage<TA>::elems;
+    const bf16* cB = sB + cur * OperandImage<TB>::elems;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      bf16x8 fa[4], fb[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) fa[i] = frag_load<TA>(cA, wm * 64 + i * 16, ks);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) fb[j] = frag_load<TB>(cB, wn * 64 + j * 16, ks);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+    }
+    if (more) {
+      tile_store<TA>(sA + (cur ^ 1) * OperandImage<TA>::elems, ra);
+      tile_store<TB>(sB + (cur ^ 1) * OperandImage<TB>::elems, rb);
+    }
+    __syncthreads();
+    cur ^= 1;
+  }
+  // epilogue: acc[i][j] lane -> (row (lane>>4)*4 + r, col lane&15)
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        int row = m0 + wm * 64 + i * 16 + (lane >> 4) * 4 + r;
+        int col = n0 + wn * 64 + j * 16 + (lane & 15);
+        if (row < M && col < N)
+          epi_store<TC>(C, ldc, coff, ep, roff, row, col, N, (long long)z * M * N + (long long)row * N + col,
+                        acc[i][j][r]);
+      }
+}
+
+// =====================================================================================
+// host launcher
+// =====================================================================================
+template <typename TI, typename TC>
+static int launch_generic(int ta, int tb, const void* A, const void* B, void* C, int M, int N, int K, long long lda,
+                          long long ldb, long long ldc, int batch, const BatchStrides& bs, const EpiParams& ep,
+                          hipStream_t s) {
+  dim3 grid((N + 63) / 64, (M + 63) / 64, batch);
+#define GG(a, b) gemm_generic<TI, TC, a, b><<<grid, 256, 0, s>>>((const TI*)A, (const TI*)B, (TC*)C, M, N, K, lda, ldb, ldc, bs, ep)
+  if (ta == 0 && tb == 0) GG(0, 0);
+  else if (ta == 0 && tb == 1) GG(0, 1);
+  else if (ta == 1 && tb == 0) GG(1, 0);
+  else GG(1, 1);
+#undef GG
+  UVA_LAUNCH_CHECK();
+  return 0;
+}
+
+template <typename TC>
+static int launch_mfma(int ta, int tb, const void* A, const void* B, void* C, int M, int N, int K, long long lda,
+                       long long ldb, long long ldc, int batch, const BatchStrides& bs, const EpiParams& ep,
+                       hipStream_t s) {
+  const int nblk = ((M + MB_M - 1) / MB_M) * ((N + MB_N - 1) / MB_N);
+  dim3 grid(nblk, 1, batch);
+  size_t lds = 2 * sizeof(bf16) * ((ta ? STAGE_M_ELEMS : STAGE_K_ELEMS) + (tb ? STAGE_M_ELEMS : STAGE_K_ELEMS));
+#define GM(a, b)                                                                                          \
+  do {                                                                                                    \
+    static bool attr = false;                                                                             \
+    if (!attr) {                                                                                          \
+      hipFuncSetAttribute((const void*)gemm_mfma_bf16<a, b, TC>, hipFuncAttributeMaxDynamicSharedMemorySize, \
+                          (int)lds);                                                                      \
+      attr = true;                                                                                        \
+    }                                                                                                     \
+    gemm_mfma_bf16<a, b, TC><<<grid, 256, lds, s>>>((const bf16*)A, (const bf16*)B, (TC*)C, M, N, K, lda, ldb, \
+                                                    ldc, bs, ep);                                         \
+  } while (0)
+  if (ta == 0 && tb == 0) GM(0, 0);
+  else if (ta == 0 && tb == 1) GM(0, 1);
+  else if (ta == 1 && tb == 0) GM(1, 0);
+  else GM(1, 1);
+#undef GM
+  UVA_LAUNCH_CHECK();
+  return 0;
+}
+
+extern "C" int uva_gemm(int in_dtype, int out_dtype, int ta, int tb, const void* A, const void* B, void* C, int M,
+                        int N, int K, long long lda, long long ldb, long long ldc, int batch, int batch_inner,
+                        long long sAo, long long sAi, long long sBo, long long sBi, long long sCo, long long sCi,
+                        const float* bias, const void* residual, long long ldr, long long sRo, long long sRi,
+                        void* aux, int act, float alpha, float beta, float drop_p, unsigned long long drop_seed,
+                        int force_generic, hipStream_t stream) {
+  if (M <= 0 || N <= 0 || batch <= 0) return 0;
+  BatchStrides bs{sAo, sAi, sBo, sBi, sCo, sCi, batch_inner > 0 ? batch_inner : 1};
+  EpiParams ep;
+  ep.bias = bias;
+  ep.residual = residual;
+  ep.aux = aux;
+  ep.act = act;
+  ep.alpha = alpha;
+  ep.beta = beta;
+  ep.drop_thresh = drop_p > 0.f ? (uint32_t)fminf(drop_p * 4294967296.0f, 4294967295.0f) : 0u;
+  ep.drop_scale = drop_p > 0.f ? 1.0f / (1.0f - drop_p) : 1.0f;
+  ep.drop_seed = drop_seed;
+  ep.ldr = ldr;
+  ep.sRo = sRo;
+  ep.sRi = sRi;
+  if (K <= 0) return 0;
+  if (in_dtype == UVA_DT_BF16) {
+    // MFMA path needs 16-B chunks: K-contiguous dims and M/N-contiguous dims multiple of 8, aligned lds
+    bool ok = !force_generic && (K % 8 == 0) && (lda % 8 == 0) && (ldb % 8 == 0) && (!ta || M % 8 == 0) &&
+              (!tb || N % 8 == 0) && (((uintptr_t)A | (uintptr_t)B) % 16 == 0) && (sAo % 8 == 0) && (sAi % 8 == 0) &&
+              (sBo % 8 == 0) && (sBi % 8 == 0);
+    if (ok) {
+      if (out_dtype == UVA_DT_BF16) return launch_mfma<bf16>(ta, tb, A, B, C, M, N, K, lda, ldb, ldc, batch, bs, ep, stream);
+      return launch_mfma<float>(ta, tb, A, B, C, M, N, K, lda, ldb, ldc, batch, bs, ep, stream);
+    }
+    if (out_dtype == UVA_DT_BF16) return launch_generic<bf16, bf16>(ta, tb, A, B, C, M, N, K, lda, ldb, ldc, batch, bs, ep, stream);
+    return launch_generic<bf16, float>(ta, tb, A, B, C, M, N, K, lda, ldb, ldc, batch, bs, ep, stream);
+  }
+  if (out_dtype == UVA_DT_F32) return launch_generic<float, float>(ta, tb, A, B, C, M, N, K, lda, ldb, ldc, batch, bs, ep, stream);
+  return launch_generic<float, bf16>(ta, tb, A, B, C, M, N, K, lda, ldb, ldc, batch, bs, ep, stream);
+}

@@ -1,0 +1,416 @@
+// Row-wise kernels: LayerNorm / adaLN-modulated LayerNorm forward+backward
+// (timm Block norm1/norm2, z_proj_ln, encoder/decoder norms: mar_con_unified.py:198,215,252;
+//  DiffLoss ResBlock in_ln + modulate and FinalLayer norm_final: diffusion_loss.py:93-94,152,177),
+// and the row softmax of the materialised attention path.
+//
+// One wave per row, each lane owning D/64 elements in registers (VEC contiguous per
+// access when D % 256 == 0); statistics in fp32, two passes over registers.
+// HBM-bound: algorithmic bytes per row = D*(sizeof(in)+sizeof(out)) (+ modulation).
+#include "common.h"
+
+template <typename T>
+__device__ __forceinline__ void load_vec(const T* p, float* out, int n) {
+#pragma unroll
+  for (int i = 0; i < n; ++i) out[i] = to_f32(p[i]);
+}
+
+template <int VEC, typename T>
+__device__ __forceinline__ void ldv(const T* p, float (&o)[VEC]) {
+  if constexpr (VEC == 4 && sizeof(T) == 4) {
+    float4 v = *(const float4*)p;
+    o[0] = v.x; o[1] = v.y; o[2] = v.z; o[3] = v.w;
+  } else if constexpr (VEC == 4 && sizeof(T) == 2) {
+    bf16x4 v = *(const bf16x4*)p;
+    o[0] = (float)v[0]; o[1] = (float)v[1]; o[2] = (float)v[2]; o[3] = (float)v[3];
+  } else {
+#pragma unroll
+    for (int i = 0; i < VEC; ++i) o[i] = to_f32(p[i]);
+  }
+}
+
+template <int VEC, typename T>
+__device__ __forceinline__ void stv(T* p, const float (&o)[VEC]) {
+  if constexpr (VEC == 4 && sizeof(T) == 4) {
+    *(float4*)p = make_float4(o[0], o[1], o[2], o[3]);
+  } else if constexpr (VEC == 4 && sizeof(T) == 2) {
+    bf16x4 v = {(bf16)o[0], (bf16)o[1], (bf16)o[2], (bf16)o[3]};
+    *(bf16x4*)p = v;
+  } else {
+#pragma unroll
+    for (int i = 0; i < VEC; ++i) p[i] = from_f32<T>(o[i]);
+  }
+}
+
+// element index of slot (c, v) of lane
+template <int VEC>
+__device__ __forceinline__ int col_of(int c, int lane, int v) { return (c * 64 + lane) * VEC + v; }
+
+// ------------------------------------------------------------------------------------
+// forward: y = LN(x) * w + b                    (w, b fp32, nullable)
+//          y = LN(x) * (1 + scale) + shift      (scale/shift rows of TO, ld = ldm) if scale
+// ------------------------------------------------------------------------------------
+template <typename TI, typename TO, int VEC, int NC>
+__global__ __launch_bounds__(256) void ln_fwd(const TI* __restrict__ x, const float* __restrict__ w,
+                                              const float* __restrict__ b, const TO* __restrict__ scale,
+                                              const TO* __restrict__ shift, long long ldm, TO* __restrict__ y,
+                                              float* __restrict__ mean_out, float* __restrict__ rstd_out, int rows,
+                                              int D, float eps) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  const TI* xr = x + (long long)row * D;
+  float v[NC][VEC];
+  float s = 0.f;
+#pragma unroll
+  for (int c = 0; c < NC; ++c) {
+    int col = col_of<VEC>(c, lane, 0);
+    if (col < D) {
+      ldv<VEC>(xr + col, v[c]);
+    } else {
+#pragma unroll
+      for (int i = 0; i < VEC; ++i) v[c][i] = 0.f;
+    }
+#pragma unroll
+    for (int i = 0; i < VEC; ++i) s += v[c][i];
+  }
+  const float mean = wave_sum(s) / D;
+  float q = 0.f;
+#pragma unroll
+  for (int c = 0; c < NC; ++c)
+#pragma unroll
+    for (int i = 0; i < VEC; ++i) {
+      int col = col_of<VEC>(c, lane, i);
+      float d = (col < D) ? v[c][i] - mean : 0.f;
+      q += d * d;
+    }
+  const float var = wave_sum(q) / D;
+  const float rstd = 1.0f / sqrtf(var + eps);
+  if (lane == 0) {
+    mean_out[row] = mean;
+    rstd_out[row] = rstd;
+  }
+  TO* yr = y + (long long)row * D;
+#pragma unroll
+  for (int c = 0; c < NC; ++c) {
+    int col0 = col_of<VEC>(c, lane, 0);
+    if (col0 >= D) continue;
+    float o[VEC];
+    float sc[VEC], sh[VEC];
+    if (scale) {
+      ldv<VEC>(scale + (long long)row * ldm + col0, sc);
+      ldv<VEC>(shift + (long long)row * ldm + col0, sh);
+    }
+#pragma unroll
+    for (int i = 0; i < VEC; ++i) {
+      float h = (v[c][i] - mean) * rstd;
+      if (w) h = h * w[col0 + i];
+      if (b) h = h + b[col0 + i];
+      if (scale) h = h * (1.0f + sc[i]) + sh[i];
+      o[i] = h;
+    }
+    stv<VEC>(yr + col0, o);
+  }
+}
+
+// ------------------------------------------------------------------------------------
+// backward.  dy fp32.  g = dy*w (affine) or dy*(1+scale) (modulated)
+//   dx (+)= rstd * (g - mean(g) - xhat*mean(g*xhat))           fp32, accumulate if accum
+//   modulated: dscale = dy*xhat, dshift = dy  (TO, ld = ldm)
+//   affine: per-block partial sums dw_part[blk][D] = sum dy*xhat, db_part = sum dy
+// ------------------------------------------------------------------------------------
+template <typename TI, typename TO, int VEC, int NC>
+__global__ __launch_bounds__(256) void ln_bwd(const TI* __restrict__ x, const float* __restrict__ w,
+                                              const TO* __restrict__ scale, long long ldm,
+                                              const float* __restrict__ dy, const float* __restrict__ mean_in,
+                                              const float* __restrict__ rstd_in, float* __restrict__ dx, int accum,
+                                              TO* __restrict__ dscale, TO* __restrict__ dshift,
+                                              float* __restrict__ dw_part, float* __restrict__ db_part, int rows,
+                                              int D, int rows_per_block) {
+  __shared__ float red_w[4][1024];
+  __shared__ float red_b[4][1024];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  float pw[NC][VEC], pb[NC][VEC];
+#pragma unroll
+  for (int c = 0; c < NC; ++c)
+#pragma unroll
+    for (int i = 0; i < VEC; ++i) pw[c][i] = pb[c][i] = 0.f;
+  const int r0 = blockIdx.x * rows_per_block;
+  const int r1 = min(rows, r0 + rows_per_block);
+  for (int row = r0 + wid; row < r1; row += 4) {
+    const float mean = mean_in[row], rstd = rstd_in[row];
+    float xh[NC][VEC], g[NC][VEC];
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+      int col0 = col_of<VEC>(c, lane, 0);
+      if (col0 >= D) {
+#pragma unroll
+        for (int i = 0; i < VEC; ++i) xh[c][i] = g[c][i] = 0.f;
+        continue;
+      }
+      float xv[VEC], dv[VEC], sc[VEC];
+      ldv<VEC>(x + (long long)row * D + col0, xv);
+      ldv<VEC>(dy + (long long)row * D + col0, dv);
+      if (scale) ldv<VEC>(scale + (long long)row * ldm + col0, sc);
+      float ds[VEC], dsh[VEC];
+#pragma unroll
+      for (int i = 0; i < VEC; ++i) {
+        xh[c][i] = (xv[i] - mean) * rstd;
+        if (scale) {
+          g[c][i] = dv[i] * (1.0f + sc[i]);
+          ds[i] = dv[i] * xh[c][i];
+          dsh[i] = dv[i];
+        } else {
+          g[c][i] = w ? dv[i] * w[col0 + i] : dv[i];
+          pw[c][i] += dv[i] * xh[c][i];
+          pb[c][i] += dv[i];
+        }
+        s1 += g[c][i];
+        s2 += g[c][i] * xh[c][i];
+      }
+      if (scale) {
+        stv<VEC>(dscale + (long long)row * ldm + col0, ds);
+        stv<VEC>(dshift + (long long)row * ldm + col0, dsh);
+      }
+    }
+    const float m1 = wave_sum(s1) / D, m2 = wave_sum(s2) / D;
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+      int col0 = col_of<VEC>(c, lane, 0);
+      if (col0 >= D) continue;
+      float o[VEC];
+      float* dxr = dx + (long long)row * D + col0;
+      if (accum) ldv<VEC>(dxr, o);
+#pragma unroll
+      for (int i = 0; i < VEC; ++i) {
+        float d = rstd * (g[c][i] - m1 - xh[c][i] * m2);
+        o[i] = accum ? o[i] + d : d;
+      }
+      stv<VEC>(dxr, o);
+    }
+  }
+  if (dw_part) {
+#pragma unroll
+    for (int c = 0; c < NC; ++c)
+#pragma unroll
+      for (int i = 0; i < VEC; ++i) {
+        int col = col_of<VEC>(c, lane, i);
+        if (col < D) {
+          red_w[wid][col] = pw[c][i];
+          red_b[wid][col] = pb[c][i];
+        }
+      }
+    __syncthreads();
+    for (int col = threadIdx.x; col < D; col += 256) {
+      dw_part[(long long)blockIdx.x * D + col] = red_w[0][col] + red_w[1][col] + red_w[2][col] + red_w[3][col];
+      db_part[(long long)blockIdx.x * D + col] = red_b[0][col] + red_b[1][col] + red_b[2][col] + red_b[3][col];
+    }
+  }
+}
+
+// column sum: out[c] (+)= sum_r in[r][c]  (in: dtype dt, fp32 out).  Deterministic two-level.
+template <typename T>
+__global__ __launch_bounds__(256) void colsum_kernel(const T* __restrict__ in, long long ld, float* __restrict__ out,
+                                                     int rows, int cols, int accum) {
+  // block = 256 threads over 64 columns x 4 row-lanes
+  __shared__ float red[4][64];
+  const int cl = threadIdx.x & 63, rl = threadIdx.x >> 6;
+  const int col = blockIdx.x * 64 + cl;
+  float s = 0.f;
+  if (col < cols)
+    for (int r = rl; r < rows; r += 4) s += to_f32(in[(long long)r * ld + col]);
+  red[rl][cl] = s;
+  __syncthreads();
+  if (rl == 0 && col < cols) {
+    float t = red[0][cl] + red[1][cl] + red[2][cl] + red[3][cl];
+    out[col] = accum ? out[col] + t : t;
+  }
+}
+
+// row-partitioned column sum for tall inputs: part[blk][c] = sum over blk's rows
+template <typename T>
+__global__ __launch_bounds__(256) void colsum_part_kernel(const T* __restrict__ in, long long ld,
+                                                          float* __restrict__ part, int rows, int cols,
+                                                          int rows_per_block) {
+  __shared__ float red[4][64];
+  const int cl = threadIdx.x & 63, rl = threadIdx.x >> 6;
+  const int col = blockIdx.x * 64 + cl;
+  const int r0 = blockIdx.y * rows_per_block, r1 = min(rows, r0 + rows_per_block);
+  float s = 0.f;
+  if (col < cols)
+    for (int r = r0 + rl; r < r1; r += 4) s += to_f32(in[(long long)r * ld + col]);
+  red[rl][cl] = s;
+  __syncthreads();
+  if (rl == 0 && col < cols) part[(long long)blockIdx.y * cols + col] = red[0][cl] + red[1][cl] + red[2][cl] + red[3][cl];
+}
+
+// ------------------------------------------------------------------------------------
+// softmax over rows of length L (materialised attention, fp32 parity path and VAE attn)
+//   P = softmax(scale * S);  Pd = P * keep/(1-p) if dropout (else Pd may alias nothing)
+// ------------------------------------------------------------------------------------
+template <typename T>
+__global__ __launch_bounds__(256) void softmax_fwd_kernel(const T* __restrict__ S, T* __restrict__ P,
+                                                          T* __restrict__ Pd, long long rows, int L, float scale,
+                                                          uint32_t thresh, float dscale, uint64_t seed) {
+  const int lane = threadIdx.x & 63;
+  const long long row = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  const T* s = S + row * L;
+  float m = -INFINITY;
+  for (int j = lane; j < L; j += 64) m = fmaxf(m, to_f32(s[j]) * scale);
+  m = wave_max(m);
+  float sum = 0.f;
+  for (int j = lane; j < L; j += 64) sum += __expf(to_f32(s[j]) * scale - m);
+  sum = wave_sum(sum);
+  const float inv = 1.0f / sum;
+  for (int j = lane; j < L; j += 64) {
+    float p = __expf(to_f32(s[j]) * scale - m) * inv;
+    P[row * L + j] = from_f32<T>(p);
+    if (Pd) {
+      float pd = dropout_keep(seed, (uint64_t)(row * L + j), thresh) ? p * dscale : 0.f;
+      Pd[row * L + j] = from_f32<T>(pd);
+    }
+  }
+}
+
+// dS = scale * P * (dP' - sum_j P*dP'),  dP' = dPd * keep/(1-p)
+template <typename T>
+__global__ __launch_bounds__(256) void softmax_bwd_kernel(const T* __restrict__ P, const T* __restrict__ dPd,
+                                                          T* __restrict__ dS, long long rows, int L, float scale,
+                                                          uint32_t thresh, float dscale, uint64_t seed) {
+  const int lane = threadIdx.x & 63;
+  const long long row = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  float dot = 0.f;
+  for (int j = lane; j < L; j += 64) {
+    float dp = to_f32(dPd[row * L + j]);
+    if (thresh) dp = dropout_keep(seed, (uint64_t)(row * L + j), thresh) ? dp * dscale : 0.f;
+    dot += dp * to_f32(P[row * L + j]);
+  }
+  dot = wave_sum(dot);
+  for (int j = lane; j < L; j += 64) {
+    float dp = to_f32(dPd[row * L + j]);
+    if (thresh) dp = dropout_keep(seed, (uint64_t)(row * L + j), thresh) ? dp * dscale : 0.f;
+    dS[row * L + j] = from_f32<T>(scale * to_f32(P[row * L + j]) * (dp - dot));
+  }
+}
+
+// =====================================================================================
+// C ABI
+// =====================================================================================
+#define DISPATCH_LN(KERNEL, TI, TO, ...)                                                    \
+  do {                                                                                       \
+    if (D % 256 == 0 && D <= 1024) {                                                         \
+      KERNEL<TI, TO, 4, 4><<<grid, 256, 0, stream>>>(__VA_ARGS__);                           \
+    } else if (D <= 1024) {                                                                  \
+      KERNEL<TI, TO, 1, 16><<<grid, 256, 0, stream>>>(__VA_ARGS__);                          \
+    } else {                                                                                 \
+      return (int)hipErrorInvalidValue;                                                      \
+    }                                                                                        \
+  } while (0)
+
+extern "C" int uva_layernorm_fwd(int in_dtype, int out_dtype, const void* x, const float* w, const float* b,
+                                 const void* scale, const void* shift, long long ldm, void* y, float* mean,
+                                 float* rstd, int rows, int D, float eps, hipStream_t stream) {
+  if (rows <= 0) return 0;
+  dim3 grid((rows + 3) / 4);
+  if (in_dtype == UVA_DT_F32 && out_dtype == UVA_DT_F32)
+    DISPATCH_LN(ln_fwd, float, float, (const float*)x, w, b, (const float*)scale, (const float*)shift, ldm,
+                (float*)y, mean, rstd, rows, D, eps);
+  else if (in_dtype == UVA_DT_F32 && out_dtype == UVA_DT_BF16)
+    DISPATCH_LN(ln_fwd, float, bf16, (const float*)x, w, b, (const bf16*)scale, (const bf16*)shift, ldm, (bf16*)y,
+                mean, rstd, rows, D, eps);
+  else if (in_dtype == UVA_DT_BF16 && out_dtype == UVA_DT_BF16)
+    DISPATCH_LN(ln_fwd, bf16, bf16, (const bf16*)x, w, b, (const bf16*)scale, (const bf16*)shift, ldm, (bf16*)y,
+                mean, rstd, rows, D, eps);
+  else
+    return (int)hipErrorInvalidValue;
+  UVA_LAUNCH_CHECK();
+  return 0;
+}
+
+extern "C" int uva_layernorm_bwd(int in_dtype, int out_dtype, const void* x, const float* w, const void* scale,
+                                 long long ldm, const float* dy, const float* mean, const float* rstd, float* dx,
+                                 int accum, void* dscale, void* dshift, float* dw, float* db, int accum_wb,
+                                 float* workspace, int rows, int D, hipStream_t stream) {
+  if (rows <= 0) return 0;
+  // dw/db via per-block partials in `workspace` (nblk * D * 2 floats), then a column sum
+  const int rpb = 64;
+  const int nblk = (rows + rpb - 1) / rpb;
+  dim3 grid(nblk);
+  float* pw = dw ? workspace : nullptr;
+  float* pb = dw ? workspace + (long long)nblk * D : nullptr;
+  if (in_dtype == UVA_DT_F32 && out_dtype == UVA_DT_F32)
+    DISPATCH_LN(ln_bwd, float, float, (const float*)x, w, (const float*)scale, ldm, dy, mean, rstd, dx, accum,
+                (float*)dscale, (float*)dshift, pw, pb, rows, D, rpb);
+  else if (in_dtype == UVA_DT_F32 && out_dtype == UVA_DT_BF16)
+    DISPATCH_LN(ln_bwd, float, bf16, (const float*)x, w, (const bf16*)scale, ldm, dy, mean, rstd, dx, accum,
+                (bf16*)dscale, (bf16*)dshift, pw, pb, rows, D, rpb);
+  else if (in_dtype == UVA_DT_BF16 && out_dtype == UVA_DT_BF16)
+    DISPATCH_LN(ln_bwd, bf16, bf16, (const bf16*)x, w, (const bf16*)scale, ldm, dy, mean, rstd, dx, accum,
+                (bf16*)dscale, (bf16*)dshift, pw, pb, rows, D, rpb);
+  else
+    return (int)hipErrorInvalidValue;
+  UVA_LAUNCH_CHECK();
+  if (dw) {
+    dim3 g2((D + 63) / 64);
+    colsum_kernel<float><<<g2, 256, 0, stream>>>(pw, D, dw, nblk, D, accum_wb);
+    if (db) colsum_kernel<float><<<g2, 256, 0, stream>>>(pb, D, db, nblk, D, accum_wb);
+    UVA_LAUNCH_CHECK();
+  }
+  return 0;
+}
+
+extern "C" long long uva_layernorm_bwd_workspace(int rows, int D) {
+  const int rpb = 64;
+  return (long long)((rows + rpb - 1) / rpb) * D * 2;  // floats
+}
+
+// out[c] (+)= sum_r in[r*ld + c]; tall inputs go through a partial buffer (floats: ceil(rows/512)*cols)
+extern "C" int uva_colsum(int dtype, const void* in, long long ld, float* out, int rows, int cols, int accum,
+                          float* workspace, hipStream_t stream) {
+  if (rows <= 0 || cols <= 0) return 0;
+  const int rpb = 512;
+  int nb = (rows + rpb - 1) / rpb;
+  dim3 g1((cols + 63) / 64, nb);
+  if (nb > 1 && workspace) {
+    if (dtype == UVA_DT_BF16) colsum_part_kernel<bf16><<<g1, 256, 0, stream>>>((const bf16*)in, ld, workspace, rows, cols, rpb);
+    else colsum_part_kernel<float><<<g1, 256, 0, stream>>>((const float*)in, ld, workspace, rows, cols, rpb);
+    colsum_kernel<float><<<dim3((cols + 63) / 64), 256, 0, stream>>>(workspace, cols, out, nb, cols, accum);
+  } else {
+    if (dtype == UVA_DT_BF16) colsum_kernel<bf16><<<dim3((cols + 63) / 64), 256, 0, stream>>>((const bf16*)in, ld, out, rows, cols, accum);
+    else colsum_kernel<float><<<dim3((cols + 63) / 64), 256, 0, stream>>>((const float*)in, ld, out, rows, cols, accum);
+  }
+  UVA_LAUNCH_CHECK();
+  return 0;
+}
+
+extern "C" long long uva_colsum_workspace(int rows, int cols) { return (long long)((rows + 511) / 512) * cols; }
+
+extern "C" int uva_softmax_fwd(int dtype, const void* S, void* P, void* Pd, long long rows, int L, float scale,
+                               float drop_p, unsigned long long seed, hipStream_t stream) {
+  if (rows <= 0) return 0;
+  uint32_t th = drop_p > 0.f ? (uint32_t)fminf(drop_p * 4294967296.0f, 4294967295.0f) : 0u;
+  float ds = drop_p > 0.f ? 1.0f / (1.0f - drop_p) : 1.0f;
+  dim3 grid((unsigned)((rows + 3) / 4));
+  if (dtype == UVA_DT_BF16)
+    softmax_fwd_kernel<bf16><<<grid, 256, 0, stream>>>((const bf16*)S, (bf16*)P, th ? (bf16*)Pd : nullptr, rows, L, scale, th, ds, seed);
+  else
+    softmax_fwd_kernel<float><<<grid, 256, 0, stream>>>((const float*)S, (float*)P, th ? (float*)Pd : nullptr, rows, L, scale, th, ds, seed);
+  UVA_LAUNCH_CHECK();
+  return 0;
+}
+
+extern "C" int uva_softmax_bwd(int dtype, const void* P, const void* dPd, void* dS, long long rows, int L, float scale,
+                               float drop_p, unsigned long long seed, hipStream_t stream) {
+  if (rows <= 0) return 0;
+  uint32_t th = drop_p > 0.f ? (uint32_t)fminf(drop_p * 4294967296.0f, 4294967295.0f) : 0u;
+  float ds = drop_p > 0.f ? 1.0f / (1.0f - drop_p) : 1.0f;
+  dim3 grid((unsigned)((rows + 3) / 4));
+  if (dtype == UVA_DT_BF16)
+    softmax_bwd_kernel<bf16><<<grid, 256, 0, stream>>>((const bf16*)P, (const bf16*)dPd, (bf16*)dS, rows, L, scale, th, ds, seed);
+  else
+    softmax_bwd_kernel<float><<<grid, 256, 0, stream>>>((const float*)P, (const float*)dPd, (float*)dS, rows, L, scale, th, ds, seed);
+  UVA_LAUNCH_CHECK();
+  return 0;
+}

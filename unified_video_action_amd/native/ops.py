@@ -1,0 +1,196 @@
+"""Thin torch-tensor wrappers over the C ABI (device pointers, strides, current stream).
+Shape/dtype checks happen here, before launch (SURVEY §8b C-ABI conventions)."""
+import ctypes
+
+import torch
+
+from .lib import lib
+
+F32, BF16 = 0, 1
+ACT = {"none": 0, "gelu": 1, "silu": 2, "relu": 3}
+
+
+def dt(t):
+    if t.dtype == torch.bfloat16:
+        return BF16
+    if t.dtype == torch.float32:
+        return F32
+    raise TypeError(f"unsupported dtype {t.dtype}")
+
+
+def ptr(t):
+    return None if t is None else t.data_ptr()
+
+
+def stream():
+    return torch.cuda.current_stream().cuda_stream
+
+
+def _ld(t):
+    """leading dimension of a 2-D (row-major, unit inner stride) view."""
+    assert t.dim() == 2 and t.stride(1) == 1, (t.shape, t.stride())
+    return t.stride(0)
+
+
+def gemm(A, B, C, M, N, K, lda, ldb, ldc, ta=0, tb=0, batch=1, inner=1, sA=(0, 0), sB=(0, 0), sC=(0, 0),
+         bias=None, residual=None, ldr=0, sR=(0, 0), aux=None, act="none", alpha=1.0, beta=0.0,
+         drop_p=0.0, seed=0, force_generic=False):
+    assert A.dtype == B.dtype, (A.dtype, B.dtype)
+    if bias is not None:
+        assert bias.dtype == torch.float32 and bias.is_contiguous()
+    if residual is not None:
+        assert residual.dtype == C.dtype
+    if aux is not None:
+        assert aux.dtype == C.dtype
+    lib().call("uva_gemm", dt(A), dt(C), ta, tb, ptr(A), ptr(B), ptr(C), M, N, K, lda, ldb, ldc, batch, inner,
+               sA[0], sA[1], sB[0], sB[1], sC[0], sC[1], ptr(bias), ptr(residual), ldr, sR[0], sR[1], ptr(aux),
+               ACT[act] if isinstance(act, str) else act, float(alpha), float(beta), float(drop_p),
+               int(seed) & 0xFFFFFFFFFFFFFFFF, int(force_generic), stream())
+
+
+def linear(x, w, out, bias=None, act="none", aux=None, residual=None, drop_p=0.0, seed=0, beta=0.0):
+    """out[M,N] = epi(x[M,K] @ w[N,K]^T) -- nn.Linear forward."""
+    M, K = x.shape
+    N = w.shape[0]
+    assert w.shape[1] == K and out.shape == (M, N)
+    gemm(x, w, out, M, N, K, _ld(x), _ld(w), _ld(out), 0, 0, bias=bias, act=act, aux=aux,
+         residual=residual, ldr=_ld(residual) if residual is not None else 0, drop_p=drop_p, seed=seed,
+         beta=beta)
+
+
+def linear_dx(dy, w, dx, beta=0.0):
+    """dx[M,K] (+)= dy[M,N] @ w[N,K]."""
+    M, N = dy.shape
+    K = w.shape[1]
+    assert dx.shape == (M, K)
+    gemm(dy, w, dx, M, K, N, _ld(dy), _ld(w), _ld(dx), 0, 1, beta=beta)
+
+
+def linear_dw(dy, x, dw, beta=1.0):
+    """dw[N,K] (+)= dy[M,N]^T @ x[M,K]  (fp32 grad buffer, accumulate by default)."""
+    M, N = dy.shape
+    K = x.shape[1]
+    assert dw.shape == (N, K)
+    gemm(dy, x, dw, N, K, M, _ld(dy), _ld(x), _ld(dw), 1, 1, beta=beta)
+
+
+_WS = {}
+
+
+def workspace(n_floats, device):
+    key = (device, "ws")
+    t = _WS.get(key)
+    if t is None or t.numel() < n_floats:
+        t = torch.empty(max(int(n_floats), 1 << 20), dtype=torch.float32, device=device)
+        _WS[key] = t
+    return t
+
+
+def colsum(x, out, accum=True):
+    rows, cols = x.shape
+    ws = workspace(lib().query("uva_colsum_workspace", rows, cols), x.device)
+    lib().call("uva_colsum", dt(x), ptr(x), _ld(x), ptr(out), rows, cols, int(accum), ptr(ws), stream())
+
+
+def layernorm_fwd(x, w, b, y, mean, rstd, eps=1e-6, scale=None, shift=None, ldm=0):
+    rows, D = x.shape
+    assert x.is_contiguous() and y.is_contiguous()
+    lib().call("uva_layernorm_fwd", dt(x), dt(y), ptr(x), ptr(w), ptr(b), ptr(scale), ptr(shift), ldm, ptr(y),
+               ptr(mean), ptr(rstd), rows, D, float(eps), stream())
+
+
+def layernorm_bwd(x, w, dy, mean, rstd, dx, accum, dw=None, db=None, scale=None, ldm=0, dscale=None, dshift=None,
+                  out_dtype=None, accum_wb=True):
+    rows, D = x.shape
+    assert dy.dtype == torch.float32 and dx.dtype == torch.float32
+    odt = out_dtype if out_dtype is not None else (dt(scale) if scale is not None else dt(x))
+    ws = None
+    if dw is not None:
+        ws = workspace(lib().query("uva_layernorm_bwd_workspace", rows, D), x.device)
+    lib().call("uva_layernorm_bwd", dt(x), odt, ptr(x), ptr(w), ptr(scale), ldm, ptr(dy), ptr(mean), ptr(rstd),
+               ptr(dx), int(accum), ptr(dscale), ptr(dshift), ptr(dw), ptr(db), int(accum_wb), ptr(ws), rows, D,
+               stream())
+
+
+def softmax_fwd(S, P, Pd, L, scale, drop_p=0.0, seed=0):
+    rows = S.numel() // L
+    lib().call("uva_softmax_fwd", dt(S), ptr(S), ptr(P), ptr(Pd), rows, L, float(scale), float(drop_p),
+               int(seed) & 0xFFFFFFFFFFFFFFFF, stream())
+
+
+def softmax_bwd(P, dPd, dS, L, scale, drop_p=0.0, seed=0):
+    rows = P.numel() // L
+    lib().call("uva_softmax_bwd", dt(P), ptr(P), ptr(dPd), ptr(dS), rows, L, float(scale), float(drop_p),
+               int(seed) & 0xFFFFFFFFFFFFFFFF, stream())
+
+
+def cast(src, dst):
+    if src.dim() == 1 or (src.is_contiguous() and dst.is_contiguous()):
+        rows, cols = 1, src.numel()
+        lds = ldd = cols
+    else:
+        rows, cols = src.shape
+        lds, ldd = _ld(src), _ld(dst)
+    lib().call("uva_cast", dt(src), ptr(src), lds, dt(dst), ptr(dst), ldd, rows, cols, stream())
+
+
+def act_fwd(x, y, act):
+    lib().call("uva_act_fwd", dt(x), ptr(x), dt(y), ptr(y), x.numel(), ACT[act], stream())
+
+
+def act_bwd(pre, dy, dx, act, drop_p=0.0, seed=0, accum=False):
+    """dx (+)= dy * dropout_mask * act'(pre); 2-D views (pre contiguous)."""
+    rows, cols = dy.shape
+    lib().call("uva_act_bwd", dt(pre) if pre is not None else F32, ptr(pre), dt(dy), ptr(dy), _ld(dy), dt(dx),
+               ptr(dx), _ld(dx), rows, cols, ACT[act], float(drop_p), int(seed) & 0xFFFFFFFFFFFFFFFF, int(accum),
+               stream())
+
+
+def gate_bwd(dout, h, gate, dh, dgate):
+    rows, cols = dout.shape
+    lib().call("uva_gate_bwd", ptr(dout), dt(h), ptr(h), dt(gate), ptr(gate), _ld(gate), dt(dh), ptr(dh),
+               ptr(dgate), rows, cols, stream())
+
+
+def fill(t, v):
+    lib().call("uva_fill", ptr(t), t.numel(), float(v), stream())
+
+
+def _tables_arg(tables):
+    arr = (ctypes.c_void_p * 8)(*[t.data_ptr() for t in tables])
+    return arr
+
+
+def q_sample(x0, noise, t, tables, xt):
+    rows, C = x0.shape
+    arr = _tables_arg(tables)
+    lib().call("uva_q_sample", ptr(x0), ptr(noise), ptr(t), ctypes.cast(arr, ctypes.c_void_p), dt(xt), ptr(xt),
+               rows, C, stream())
+
+
+def timestep_features(t, freqs, out):
+    rows = t.numel()
+    lib().call("uva_timestep_features", ptr(t), ptr(freqs), dt(out), ptr(out), rows, freqs.numel(), stream())
+
+
+def diffusion_loss(x0, noise, t, out, tables, loss_row, dl):
+    rows, C = x0.shape
+    arr = _tables_arg(tables)
+    lib().call("uva_diffusion_loss", ptr(x0), ptr(noise), ptr(t), dt(out), ptr(out), _ld(out),
+               ctypes.cast(arr, ctypes.c_void_p), ptr(loss_row), ptr(dl), rows, C, stream())
+
+
+def weighted_mean(l, w, res):
+    lib().call("uva_weighted_mean", ptr(l), ptr(w), l.numel(), ptr(res), stream())
+
+
+def loss_grad(dl, w, wsum, g_up, dout):
+    rows, C2 = dl.shape
+    lib().call("uva_loss_grad", ptr(dl), ptr(w), ptr(wsum), ptr(g_up), dt(dout), ptr(dout), _ld(dout), rows, C2,
+               stream())
+
+
+def adamw_ema(p, g, m, v, ema, p_bf16, n_decay, lr, b1, b2, eps, wd, step, grad_scale, ema_decay):
+    lib().call("uva_adamw_ema", ptr(p), ptr(g), ptr(m), ptr(v), ptr(ema), ptr(p_bf16), p.numel(), int(n_decay),
+               float(lr), float(b1), float(b2), float(eps), float(wd), int(step), float(grad_scale),
+               float(ema_decay), stream())
