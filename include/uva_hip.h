@@ -43,7 +43,25 @@ int uva_gemm(int in_dtype, int out_dtype, int ta, int tb, const void* A, const v
              int K, long long lda, long long ldb, long long ldc, int batch, int batch_inner, long long sAo,
              long long sAi, long long sBo, long long sBi, long long sCo, long long sCi, const float* bias,
              const void* residual, long long ldr, long long sRo, long long sRi, void* aux, int act, float alpha,
-             float beta, float drop_p, unsigned long long drop_seed, int force_generic, hipStream_t stream);
+             float beta, float drop_p, unsigned long long drop_seed, int res_dtype, const void* gate,
+             long long ldg, int gate_dtype, int force_generic, float* workspace, long long ws_floats,
+             hipStream_t stream);
+/* res_dtype: dtype of `residual`; gate (dtype gate_dtype, ld ldg) multiplies the value after
+ * dropout and before the residual add (adaLN: x + gate * mlp(h), diffusion_loss.py:163-167). */
+/* workspace (fp32, ws_floats) enables deterministic split-K for few-tile / long-K products
+ * (the dW GEMMs, K = tokens); pass NULL/0 to disable. */
+
+/* ---- convolution as implicit GEMM over NHWC (bf16: MFMA, fp32: VALU) -----------------
+ * out[n,oh,ow,co] = bias[co] + residual + sum_{kh,kw,ci} act(in[n,ih,iw,ci]) w[co][kh][kw][ci]
+ * with ih = oh*stride + kh - pad_t (zero outside), act = GroupNorm-apply + SiLU when
+ * gn_scale/gn_shift ([Nimg][Ci] fp32) are given (SiLU only if gn_silu); `act` applies to the
+ * output before the residual add.  Ci % 8 == 0 for the MFMA path.
+ * Replaces nn.Conv2d (+ the preceding Normalize/nonlinearity) of the KL-VAE encoder
+ * (vae/vaekl.py:36-113,116-159,162-273,469) and DiffActLoss.conv (diffusion_action_loss.py:42-46). */
+int uva_conv2d(int dtype, const void* in, const void* w, void* out, const float* bias, const void* residual, int Nimg,
+               int Hin, int Win, int Ci, int Co, int ks, int stride, int pad_t, int pad_l, int Hout, int Wout,
+               const float* gn_scale, const float* gn_shift, int gn_silu, int act, int force_generic,
+               hipStream_t stream);
 
 /* ---- LayerNorm (affine or adaLN-modulated) --------------------------------------------
  * Replaces nn.LayerNorm(eps=1e-6) (mar_con_unified.py:198,215,252; timm norm1/norm2)
@@ -51,8 +69,10 @@ int uva_gemm(int in_dtype, int out_dtype, int ta, int tb, const void* A, const v
 int uva_layernorm_fwd(int in_dtype, int out_dtype, const void* x, const float* w, const float* b, const void* scale,
                       const void* shift, long long ldm, void* y, float* mean, float* rstd, int rows, int D, float eps,
                       hipStream_t stream);
-int uva_layernorm_bwd(int in_dtype, int out_dtype, const void* x, const float* w, const void* scale, long long ldm,
-                      const float* dy, const float* mean, const float* rstd, float* dx, int accum, void* dscale,
+int uva_layernorm_bwd(int in_dtype, int out_dtype, const void* x, const float* w, const float* b, const void* scale,
+                      long long ldm,
+                      const float* dy, const float* mean, const float* rstd, const float* dx_base, float* dx,
+                      int accum, void* dscale,
                       void* dshift, float* dw, float* db, int accum_wb, float* workspace, int rows, int D,
                       hipStream_t stream);
 long long uva_layernorm_bwd_workspace(int rows, int D); /* floats */
@@ -109,6 +129,23 @@ int uva_attn_fwd(const void* qkv, void* out, float* lse2, int B, int N, int H, f
                  unsigned long long seed, hipStream_t stream);
 int uva_attn_bwd(const void* qkv, const void* out, const void* dout, const float* lse2, float* Dvec, void* dqkv,
                  int B, int N, int H, float scale, float drop_p, unsigned long long seed, hipStream_t stream);
+
+/* ---- KL-VAE encoder plumbing (vae/vaekl.py, utils/data_utils.py) ---------------------
+ * uva_resize_select: obs image [B,T,3,Hin,Win] fp32 in [0,1] -> NHWC [B*nsel,256,256,Cpad]
+ *   frames sel[] (select_frames, data_utils.py:140-158), bilinear align_corners=False
+ *   (data_utils.py:72-81), x*255/127.5-1 (:210,226); images ordered future-half first,
+ *   then history-half (get_vae_latent encodes x then c, :405-424).
+ * uva_groupnorm_stats: GroupNorm(32, eps) of NHWC x -> scale/shift [Nimg][C] consumed by
+ *   uva_conv2d's GN+SiLU A-loader (vaekl.py:14-17).  workspace: uva_groupnorm_workspace floats.
+ * uva_posterior_sample: moments NHWC [Nimg,256,32] -> z tokens [Nimg,256,16] fp32,
+ *   eps NCHW [Nimg,16,16,16] (DiagonalGaussianDistribution.sample, vaekl.py:400-417, x0.2325). */
+int uva_resize_select(const float* img, int B, int T, int Hin, int Win, const int* sel, int nsel, int odt, void* out,
+                      int Cpad, hipStream_t stream);
+long long uva_groupnorm_workspace(int Nimg, int HW);
+int uva_groupnorm_stats(int dtype, const void* x, int Nimg, int HW, int C, const float* gamma, const float* beta,
+                        float eps, float* scale, float* shift, float* workspace, hipStream_t stream);
+int uva_posterior_sample(int mdt, const void* moments, const float* eps, float* z, int Nimg, float scale,
+                         hipStream_t stream);
 
 #ifdef __cplusplus
 }

@@ -1,0 +1,91 @@
+"""Fused bf16 attention vs a plain PyTorch fp32 reference on the same bf16 inputs
+(p = 0; tolerance 2e-2 of the output scale), and vs the materialised GEMM+softmax
+path with dropout on (same counter-hash mask; tolerance 3e-2)."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def rel_err(a, b):
+    a, b = a.double(), b.double()
+    return ((a - b).abs().max() / (b.abs().max() + 1e-12)).item()
+
+
+def ref_attention(qkv, B, N, H, drop_mask=None, p=0.0):
+    q, k, v = qkv.float().view(B, N, 3, H, 64).permute(2, 0, 3, 1, 4)
+    q, k, v = (t.clone().requires_grad_(True) for t in (q, k, v))
+    a = torch.softmax((q @ k.transpose(-1, -2)) * 0.125, dim=-1)
+    if drop_mask is not None:
+        a = a * drop_mask / (1 - p)
+    o = (a @ v).transpose(1, 2).reshape(B, N, H * 64)
+    return o, (q, k, v)
+
+
+@pytest.mark.parametrize("B,N,H", [(2, 1024, 12), (1, 1088, 12), (2, 256, 2)])
+def test_flash_fwd_bwd_vs_fp32(B, N, H):
+    from unified_video_action_amd.native import ops
+    torch.manual_seed(0)
+    qkv = (torch.randn(B, N, 3 * H * 64, device=DEV) * 1.0).to(torch.bfloat16)
+    out = torch.empty(B, N, H * 64, device=DEV, dtype=torch.bfloat16)
+    lse = torch.empty(B, H, N, device=DEV)
+    ops.attn_fwd(qkv, out, lse, B, N, H, 0.125)
+    ref, (q, k, v) = ref_attention(qkv, B, N, H)
+    assert rel_err(out.float(), ref) < 2e-2
+    dout = torch.randn(B, N, H * 64, device=DEV).to(torch.bfloat16)
+    ref.backward(dout.float())
+    dqkv = torch.empty_like(qkv)
+    dvec = torch.empty(B, H, N, device=DEV)
+    ops.attn_bwd(qkv, out, dout, lse, dvec, dqkv, B, N, H, 0.125)
+    d = dqkv.float().view(B, N, 3, H, 64)
+    for i, t in enumerate((q, k, v)):
+        assert rel_err(d[:, :, i].permute(0, 2, 1, 3), t.grad) < 3e-2, i
+
+
+def test_flash_rescale_branch_forced():
+    """Spike one key so the running max jumps mid-sweep (exercises the online rescale)."""
+    from unified_video_action_amd.native import ops
+    B, N, H = 1, 512, 2
+    qkv = torch.randn(B, N, 3, H, 64, device=DEV) * 0.5
+    qkv[0, 400, 1] = qkv[0, :, 0].mean(0) * 40  # key 400 aligned with the mean query
+    qkv = qkv.reshape(B, N, -1).to(torch.bfloat16)
+    out = torch.empty(B, N, H * 64, device=DEV, dtype=torch.bfloat16)
+    lse = torch.empty(B, H, N, device=DEV)
+    ops.attn_fwd(qkv, out, lse, B, N, H, 0.125)
+    ref, _ = ref_attention(qkv, B, N, H)
+    assert rel_err(out.float(), ref) < 2e-2
+
+
+def test_flash_dropout_matches_materialised_path():
+    from unified_video_action_amd.native import ops
+    torch.manual_seed(1)
+    B, N, H, p, seed = 1, 256, 2, 0.1, 777
+    qkv = torch.randn(B, N, 3 * H * 64, device=DEV).to(torch.bfloat16)
+    out = torch.empty(B, N, H * 64, device=DEV, dtype=torch.bfloat16)
+    lse = torch.empty(B, H, N, device=DEV)
+    ops.attn_fwd(qkv, out, lse, B, N, H, 0.125, drop_p=p, seed=seed)
+    # materialised: S = Q K^T (fp32), P = softmax, Pd = dropout(P) with the same hash
+    q = qkv.float().view(B, N, 3, H, 64)
+    ld = 3 * H * 64
+    qf = qkv.float()
+    S = torch.empty(B, H, N, N, device=DEV)
+    ops.gemm(qf[..., :H * 64], qf[..., H * 64:], S, N, N, 64, ld, ld, N, 0, 0, batch=B * H, inner=H,
+             sA=(N * ld, 64), sB=(N * ld, 64), sC=(H * N * N, N * N))
+    P = torch.empty_like(S)
+    Pd = torch.empty_like(S)
+    ops.softmax_fwd(S, P, Pd, N, 0.125, drop_p=p, seed=seed)
+    keep = (Pd != 0).float()
+    assert abs(keep.mean().item() - 0.9) < 0.01
+    ref = (Pd @ q[:, :, 2].permute(0, 2, 1, 3)).transpose(1, 2).reshape(B, N, H * 64)
+    assert rel_err(out.float(), ref) < 2e-2
+    # backward consistency against autograd of the masked reference
+    refo, (qq, kk, vv) = ref_attention(qkv, B, N, H, drop_mask=keep, p=p)
+    dout = torch.randn(B, N, H * 64, device=DEV).to(torch.bfloat16)
+    refo.backward(dout.float())
+    dqkv = torch.empty_like(qkv)
+    dvec = torch.empty(B, H, N, device=DEV)
+    ops.attn_bwd(qkv, out, dout, lse, dvec, dqkv, B, N, H, 0.125, drop_p=p, seed=seed)
+    d = dqkv.float().view(B, N, 3, H, 64)
+    for i, t in enumerate((qq, kk, vv)):
+        assert rel_err(d[:, :, i].permute(0, 2, 1, 3), t.grad) < 3e-2, i

@@ -1,0 +1,63 @@
+"""Kernel micro-benchmarks at the MAR training shapes (B=32, N=1024, D=768)."""
+import sys
+import torch
+sys.path.insert(0, ".")
+from unified_video_action_amd.native import ops
+
+
+def timeit(fn, iters=20):
+    for _ in range(3):
+        fn()
+    torch.cuda.synchronize()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(iters):
+        fn()
+    e.record()
+    torch.cuda.synchronize()
+    return s.elapsed_time(e) / iters
+
+
+def main():
+    dev = "cuda"
+    M = 32 * 1024
+    for (N, K) in ((2304, 768), (768, 768), (3072, 768), (768, 3072)):
+        x = torch.randn(M, K, device=dev).to(torch.bfloat16)
+        w = torch.randn(N, K, device=dev).to(torch.bfloat16)
+        y = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+        dy = torch.randn(M, N, device=dev).to(torch.bfloat16)
+        dx = torch.empty(M, K, device=dev)
+        dw = torch.zeros(N, K, device=dev)
+        fl = 2 * M * N * K
+        t1 = timeit(lambda: ops.linear(x, w, y))
+        t2 = timeit(lambda: ops.linear_dx(dy, w, dx))
+        t3 = timeit(lambda: ops.linear_dw(dy, x, dw))
+        tt = timeit(lambda: torch.matmul(x, w.t()))
+        print(f"gemm M={M} N={N} K={K}: fwd {fl/t1/1e9:.0f} TF  dx {fl/t2/1e9:.0f} TF  dw {fl/t3/1e9:.0f} TF"
+              f"   (torch/hipBLASLt fwd {fl/tt/1e9:.0f} TF)")
+    B, N, H = 32, 1024, 12
+    qkv = torch.randn(B, N, 3 * H * 64, device=dev).to(torch.bfloat16)
+    out = torch.empty(B, N, H * 64, device=dev, dtype=torch.bfloat16)
+    lse = torch.empty(B, H, N, device=dev)
+    dqkv = torch.empty_like(qkv)
+    dvec = torch.empty(B, H, N, device=dev)
+    fl = 4 * B * H * N * N * 64
+    for p in (0.0, 0.1):
+        t1 = timeit(lambda: ops.attn_fwd(qkv, out, lse, B, N, H, 0.125, p, 1))
+        t2 = timeit(lambda: ops.attn_bwd(qkv, out, out, lse, dvec, dqkv, B, N, H, 0.125, p, 1))
+        print(f"attn B={B} N={N} H={H} p={p}: fwd {t1:.3f} ms {fl/t1/1e9:.0f} TF, bwd {t2:.3f} ms "
+              f"{2.5*fl/t2/1e9:.0f} TF(alg)")
+    q = qkv.view(B, N, 3, H, 64).permute(2, 0, 3, 1, 4)
+    ts = timeit(lambda: torch.nn.functional.scaled_dot_product_attention(q[0], q[1], q[2]))
+    print(f"torch sdpa fwd {ts:.3f} ms {fl/ts/1e9:.0f} TF")
+    x = torch.randn(M, 768, device=dev)
+    yb = torch.empty(M, 768, device=dev, dtype=torch.bfloat16)
+    w = torch.ones(768, device=dev)
+    mean = torch.empty(M, device=dev)
+    rstd = torch.empty(M, device=dev)
+    t = timeit(lambda: ops.layernorm_fwd(x, w, w, yb, mean, rstd))
+    print(f"layernorm fwd f32->bf16 [{M},768]: {t*1e3:.1f} us, {M*768*6/t/1e6:.0f} GB/s")
+
+
+if __name__ == "__main__":
+    main()

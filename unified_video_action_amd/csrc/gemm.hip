@@ -28,11 +28,27 @@ struct EpiParams {
   uint64_t drop_seed;
   long long ldr;
   long long sRo, sRi;     // residual batch strides
+  const void* gate;       // adaLN gate (row-major, ld = ldg, dtype gate_dt) or null
+  long long ldg;
+  int gate_dt, res_dt;    // runtime dtypes of gate / residual (UVA_DT_*)
 };
 
 struct BatchStrides {
   long long sAo, sAi, sBo, sBi, sCo, sCi;
   int binner;
+};
+
+// implicit-GEMM convolution view of operand A (ta == 2): A[m][k] with
+//   m = (n, oh, ow) over the NHWC output,  k = (kh, kw, ci)
+//   A[m][k] = act(in[n][oh*stride+kh-pad_t][ow*stride+kw-pad_l][ci])   (0 outside the image)
+// act = GroupNorm-apply + SiLU (per-(n, ci) scale/shift, fp32) when gn_scale != null.
+// Replaces torch.nn.Conv2d of vae/vaekl.py:73-91,122-133,188,238,469 and the
+// GroupNorm+swish that precedes them (vaekl.py:9-17,94-104,270-271).
+struct ConvParams {
+  int Hin, Win, Ci, Hout, Wout, ks, stride, pad_t, pad_l;
+  const float* gn_scale;
+  const float* gn_shift;
+  int gn_silu;
 };
 
 template <typename TC>
@@ -44,7 +60,14 @@ __device__ __forceinline__ void epi_store(TC* C, long long ldc, long long coff, 
   if (ep.aux) ((TC*)ep.aux)[ci] = from_f32<TC>(v);
   v = apply_act(ep.act, v);
   if (ep.drop_thresh) v = dropout_keep(ep.drop_seed, (uint64_t)didx, ep.drop_thresh) ? v * ep.drop_scale : 0.f;
-  if (ep.residual) v += to_f32(((const TC*)ep.residual)[roff + (long long)row * ep.ldr + col]);
+  if (ep.gate) {
+    long long gi = (long long)row * ep.ldg + col;
+    v *= ep.gate_dt == UVA_DT_BF16 ? (float)((const bf16*)ep.gate)[gi] : ((const float*)ep.gate)[gi];
+  }
+  if (ep.residual) {
+    long long ri = roff + (long long)row * ep.ldr + col;
+    v += ep.res_dt == UVA_DT_BF16 ? (float)((const bf16*)ep.residual)[ri] : ((const float*)ep.residual)[ri];
+  }
   if (ep.beta != 0.f) v += ep.beta * to_f32(C[ci]);
   C[ci] = from_f32<TC>(v);
 }
@@ -52,10 +75,26 @@ __device__ __forceinline__ void epi_store(TC* C, long long ldc, long long coff, 
 // =====================================================================================
 // generic VALU kernel: 64x64 tile, BK=16, 256 threads x (4x4) outputs
 // =====================================================================================
+template <typename TI>
+__device__ __forceinline__ float conv_gather(const TI* __restrict__ in, const ConvParams& cp, int m, int k) {
+  const int hw = cp.Hout * cp.Wout;
+  const int n = m / hw, r = m % hw, oh = r / cp.Wout, ow = r % cp.Wout;
+  const int tap = k / cp.Ci, ci = k % cp.Ci;
+  const int ih = oh * cp.stride + tap / cp.ks - cp.pad_t, iw = ow * cp.stride + tap % cp.ks - cp.pad_l;
+  if (ih < 0 || ih >= cp.Hin || iw < 0 || iw >= cp.Win) return 0.f;
+  float v = to_f32(in[(((long long)n * cp.Hin + ih) * cp.Win + iw) * cp.Ci + ci]);
+  if (cp.gn_scale) {
+    v = v * cp.gn_scale[(long long)n * cp.Ci + ci] + cp.gn_shift[(long long)n * cp.Ci + ci];
+    if (cp.gn_silu) v = silu(v);
+  }
+  return v;
+}
+
 template <typename TI, typename TC, int TA, int TB>
 __global__ __launch_bounds__(256) void gemm_generic(const TI* __restrict__ A, const TI* __restrict__ B,
                                                     TC* __restrict__ C, int M, int N, int K, long long lda,
-                                                    long long ldb, long long ldc, BatchStrides bs, EpiParams ep) {
+                                                    long long ldb, long long ldc, BatchStrides bs, EpiParams ep,
+                                                    ConvParams cp) {
   __shared__ float As[16][64 + 4];
   __shared__ float Bs[16][64 + 4];
   const int z = blockIdx.z, zo = z / bs.binner, zi = z % bs.binner;
@@ -71,10 +110,13 @@ __global__ __launch_bounds__(256) void gemm_generic(const TI* __restrict__ A, co
     for (int i = 0; i < 4; ++i) {
       int e = t + i * 256;  // 0..1023 over a 64x16 tile
       int mm, kk;
-      if (TA == 0) { mm = e >> 4; kk = e & 15; } else { kk = e >> 6; mm = e & 63; }
+      if (TA != 1) { mm = e >> 4; kk = e & 15; } else { kk = e >> 6; mm = e & 63; }
       int gm = m0 + mm, gk = k0 + kk;
       float v = 0.f;
-      if (gm < M && gk < K) v = to_f32(TA == 0 ? A[(long long)gm * lda + gk] : A[(long long)gk * lda + gm]);
+      if (gm < M && gk < K) {
+        if (TA == 2) v = conv_gather(A, cp, gm, gk);
+        else v = to_f32(TA == 0 ? A[(long long)gm * lda + gk] : A[(long long)gk * lda + gm]);
+      }
       As[kk][mm] = v;
       int nn;
       if (TB == 0) { nn = e >> 4; kk = e & 15; } else { kk = e >> 6; nn = e & 63; }
@@ -120,22 +162,67 @@ __global__ __launch_bounds__(256) void gemm_generic(const TI* __restrict__ A, co
 
 template <int T>
 struct OperandImage {
-  static constexpr int elems = (T == 0) ? STAGE_K_ELEMS : STAGE_M_ELEMS;
+  static constexpr int elems = (T == 1) ? STAGE_M_ELEMS : STAGE_K_ELEMS;
 };
+
+// per-thread decode of the 4 output rows a conv A-tile chunk belongs to (fixed over k)
+struct ConvRows {
+  int n[4], ih0[4], iw0[4];
+  bool ok[4];
+};
+
+__device__ __forceinline__ void conv_rows_init(const ConvParams& cp, int row0, int M, ConvRows& cr) {
+  const int t = threadIdx.x, hw = cp.Hout * cp.Wout;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    int m = row0 + ((t + i * 256) >> 3);
+    cr.ok[i] = m < M;
+    int mm = cr.ok[i] ? m : 0;
+    int n = mm / hw, r = mm % hw;
+    cr.n[i] = n;
+    cr.ih0[i] = (r / cp.Wout) * cp.stride - cp.pad_t;
+    cr.iw0[i] = (r % cp.Wout) * cp.stride - cp.pad_l;
+  }
+}
 
 // global -> registers for one 128x64 operand tile (4 chunks of 8 bf16 per thread)
 template <int T>
 __device__ __forceinline__ void tile_load(const bf16* __restrict__ P, long long ld, int row0, int nrows, int k0, int K,
-                                          bf16x8 (&r)[4]) {
+                                          bf16x8 (&r)[4], const ConvParams& cp, const ConvRows& cr) {
   const int t = threadIdx.x;
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     int id = t + i * 256;
+    if (T == 2) {
+      const int k = k0 + (id & 7) * 8;
+      bf16x8 v = (bf16x8){};
+      if (cr.ok[i] && k < K) {
+        const int tap = k / cp.Ci, ci = k - tap * cp.Ci;
+        const int ih = cr.ih0[i] + tap / cp.ks, iw = cr.iw0[i] + tap % cp.ks;
+        if (ih >= 0 && ih < cp.Hin && iw >= 0 && iw < cp.Win) {
+          v = *(const bf16x8*)(P + (((long long)cr.n[i] * cp.Hin + ih) * cp.Win + iw) * cp.Ci + ci);
+          if (cp.gn_scale) {
+            const float* sc = cp.gn_scale + (long long)cr.n[i] * cp.Ci + ci;
+            const float* sh = cp.gn_shift + (long long)cr.n[i] * cp.Ci + ci;
+            float4 s0 = *(const float4*)sc, s1 = *(const float4*)(sc + 4);
+            float4 h0 = *(const float4*)sh, h1 = *(const float4*)(sh + 4);
+            float ss[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
+            float hh[8] = {h0.x, h0.y, h0.z, h0.w, h1.x, h1.y, h1.z, h1.w};
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+              float u = (float)v[j] * ss[j] + hh[j];
+              v[j] = (bf16)(cp.gn_silu ? silu(u) : u);
+            }
+          }
+        }
+      }
+      r[i] = v;
+      continue;
+    }
     int row, k;
     if (T == 0) { row = id >> 3; k = (id & 7) * 8; } else { k = id >> 4; row = (id & 15) * 8; }
     int gr = row0 + row, gk = k0 + k;
-    bool ok = (T == 0) ? (gr < nrows && gk < K) : (gr < nrows && gk < K);
-    if (ok) {
+    if (gr < nrows && gk < K) {
       const bf16* src = (T == 0) ? P + (long long)gr * ld + gk : P + (long long)gk * ld + gr;
       r[i] = *(const bf16x8*)src;
     } else {
@@ -150,7 +237,7 @@ __device__ __forceinline__ void tile_store(bf16* lds, const bf16x8 (&r)[4]) {
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     int id = t + i * 256;
-    if (T == 0) {
+    if (T != 1) {
       int row = id >> 3, c = id & 7;
       *(bf16x8*)(lds + row * LDK_ROW + ((c ^ (row & 7)) * 8)) = r[i];
     } else {
@@ -164,7 +251,7 @@ __device__ __forceinline__ void tile_store(bf16* lds, const bf16x8 (&r)[4]) {
 template <int T>
 __device__ __forceinline__ bf16x8 frag_load(const bf16* lds, int row0, int ks) {
   const int l = threadIdx.x & 63;
-  if (T == 0) {
+  if (T != 1) {
     int row = row0 + (l & 15);
     int c = ks * 4 + (l >> 4);
     return *(const bf16x8*)(lds + row * LDK_ROW + ((c ^ (row & 7)) * 8));
@@ -187,11 +274,14 @@ __device__ __forceinline__ int xcd_remap(int bid, int nblk) {
   return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + bid / 8;
 }
 
+// splits > 1: blockIdx.y = K-slice; raw fp32 partials go to `part` (+ slice * M * N),
+// the epilogue runs in splitk_reduce.
 template <int TA, int TB, typename TC>
 __global__ __launch_bounds__(256, 2) void gemm_mfma_bf16(const bf16* __restrict__ A, const bf16* __restrict__ B,
                                                          TC* __restrict__ C, int M, int N, int K, long long lda,
                                                          long long ldb, long long ldc, BatchStrides bs,
-                                                         EpiParams ep) {
+                                                         EpiParams ep, ConvParams cp, float* __restrict__ part,
+                                                         int k_per_split) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   bf16* sA = (bf16*)smem;
   bf16* sB = sA + 2 * OperandImage<TA>::elems;
@@ -211,6 +301,11 @@ __global__ __launch_bounds__(256, 2) void gemm_mfma_bf16(const bf16* __restrict_
   int bm = first_m + (pid % (GROUP * tn)) % gsz;
   int bn = (pid % (GROUP * tn)) / gsz;
   const int m0 = bm * MB_M, n0 = bn * MB_N;
+  const int kbeg = blockIdx.y * k_per_split;
+  const int kend = min(K, kbeg + k_per_split);
+
+  ConvRows cr;
+  if (TA == 2) conv_rows_init(cp, m0, M, cr);
 
   const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int wm = wid >> 1, wn = wid & 1;
@@ -221,9 +316,9 @@ __global__ __launch_bounds__(256, 2) void gemm_mfma_bf16(const bf16* __restrict_
     for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
 
   bf16x8 ra[4], rb[4];
-  const int nk = (K + MB_K - 1) / MB_K;
-  tile_load<TA>(A, lda, m0, M, 0, K, ra);
-  tile_load<TB>(B, ldb, n0, N, 0, K, rb);
+  const int nk = (kend - kbeg + MB_K - 1) / MB_K;
+  tile_load<TA>(A, lda, m0, M, kbeg, kend, ra, cp, cr);
+  tile_load<TB>(B, ldb, n0, N, kbeg, kend, rb, cp, cr);
   tile_store<TA>(sA, ra);
   tile_store<TB>(sB, rb);
   __syncthreads();
@@ -231,8 +326,8 @@ __global__ __launch_bounds__(256, 2) void gemm_mfma_bf16(const bf16* __restrict_
   for (int kt = 0; kt < nk; ++kt) {
     const bool more = kt + 1 < nk;
     if (more) {
-      tile_load<TA>(A, lda, m0, M, (kt + 1) * MB_K, K, ra);
-      tile_load<TB>(B, ldb, n0, N, (kt + 1) * MB_K, K, rb);
+      tile_load<TA>(A, lda, m0, M, kbeg + (kt + 1) * MB_K, kend, ra, cp, cr);
+      tile_load<TB>(B, ldb, n0, N, kbeg + (kt + 1) * MB_K, kend, rb, cp, cr);
     }
     const bf16* cA = sA + cur * OperandImage<TA>::elems;
     const bf16* cB = sB + cur * OperandImage<TB>::elems;
@@ -256,6 +351,7 @@ __global__ __launch_bounds__(256, 2) void gemm_mfma_bf16(const bf16* __restrict_
     cur ^= 1;
   }
   // epilogue: acc[i][j] lane -> (row (lane>>4)*4 + r, col lane&15)
+  float* pslab = part ? part + (long long)blockIdx.y * M * N : nullptr;
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -264,25 +360,42 @@ __global__ __launch_bounds__(256, 2) void gemm_mfma_bf16(const bf16* __restrict_
       for (int r = 0; r < 4; ++r) {
         int row = m0 + wm * 64 + i * 16 + (lane >> 4) * 4 + r;
         int col = n0 + wn * 64 + j * 16 + (lane & 15);
-        if (row < M && col < N)
-          epi_store<TC>(C, ldc, coff, ep, roff, row, col, N, (long long)z * M * N + (long long)row * N + col,
-                        acc[i][j][r]);
+        if (row < M && col < N) {
+          if (pslab) pslab[(long long)row * N + col] = acc[i][j][r];
+          else
+            epi_store<TC>(C, ldc, coff, ep, roff, row, col, N, (long long)z * M * N + (long long)row * N + col,
+                          acc[i][j][r]);
+        }
       }
 }
 
+template <typename TC>
+__global__ __launch_bounds__(256) void splitk_reduce(const float* __restrict__ part, int splits, TC* __restrict__ C,
+                                                     int M, int N, long long ldc, EpiParams ep) {
+  const long long n = (long long)M * N;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
+    float s = 0.f;
+    for (int k = 0; k < splits; ++k) s += part[k * n + i];
+    int row = (int)(i / N), col = (int)(i % N);
+    epi_store<TC>(C, ldc, 0, ep, 0, row, col, N, i, s);
+  }
+}
+
 // =====================================================================================
-// host launcher
+// host launchers
 // =====================================================================================
 template <typename TI, typename TC>
 static int launch_generic(int ta, int tb, const void* A, const void* B, void* C, int M, int N, int K, long long lda,
                           long long ldb, long long ldc, int batch, const BatchStrides& bs, const EpiParams& ep,
-                          hipStream_t s) {
+                          const ConvParams& cp, hipStream_t s) {
   dim3 grid((N + 63) / 64, (M + 63) / 64, batch);
-#define GG(a, b) gemm_generic<TI, TC, a, b><<<grid, 256, 0, s>>>((const TI*)A, (const TI*)B, (TC*)C, M, N, K, lda, ldb, ldc, bs, ep)
-  if (ta == 0 && tb == 0) GG(0, 0);
+#define GG(a, b) gemm_generic<TI, TC, a, b><<<grid, 256, 0, s>>>((const TI*)A, (const TI*)B, (TC*)C, M, N, K, lda, ldb, ldc, bs, ep, cp)
+  if (ta == 2 && tb == 0) GG(2, 0);
+  else if (ta == 0 && tb == 0) GG(0, 0);
   else if (ta == 0 && tb == 1) GG(0, 1);
   else if (ta == 1 && tb == 0) GG(1, 0);
-  else GG(1, 1);
+  else if (ta == 1 && tb == 1) GG(1, 1);
+  else return (int)hipErrorInvalidValue;
 #undef GG
   UVA_LAUNCH_CHECK();
   return 0;
@@ -291,10 +404,25 @@ static int launch_generic(int ta, int tb, const void* A, const void* B, void* C,
 template <typename TC>
 static int launch_mfma(int ta, int tb, const void* A, const void* B, void* C, int M, int N, int K, long long lda,
                        long long ldb, long long ldc, int batch, const BatchStrides& bs, const EpiParams& ep,
-                       hipStream_t s) {
+                       const ConvParams& cp, float* ws, long long ws_floats, hipStream_t s) {
   const int nblk = ((M + MB_M - 1) / MB_M) * ((N + MB_N - 1) / MB_N);
-  dim3 grid(nblk, 1, batch);
-  size_t lds = 2 * sizeof(bf16) * ((ta ? STAGE_M_ELEMS : STAGE_K_ELEMS) + (tb ? STAGE_M_ELEMS : STAGE_K_ELEMS));
+  // split-K when the output tiling cannot fill the chip (dW GEMMs: few tiles, K = tokens)
+  int splits = 1;
+  if (batch == 1 && ws && nblk < 256 && K >= 4 * MB_K) {
+    splits = (512 + nblk - 1) / nblk;
+    int kmax = K / (2 * MB_K);
+    if (splits > kmax) splits = kmax;
+    if (splits > 16) splits = 16;
+    while (splits > 1 && (long long)splits * M * N > ws_floats) --splits;
+  }
+  int kps = K;
+  if (splits > 1) {
+    kps = ((K + splits - 1) / splits + MB_K - 1) / MB_K * MB_K;
+    splits = (K + kps - 1) / kps;
+  }
+  float* part = splits > 1 ? ws : nullptr;
+  dim3 grid(nblk, splits, batch);
+  size_t lds = 2 * sizeof(bf16) * ((ta == 1 ? STAGE_M_ELEMS : STAGE_K_ELEMS) + (tb == 1 ? STAGE_M_ELEMS : STAGE_K_ELEMS));
 #define GM(a, b)                                                                                          \
   do {                                                                                                    \
     static bool attr = false;                                                                             \
@@ -304,26 +432,29 @@ static int launch_mfma(int ta, int tb, const void* A, const void* B, void* C, in
       attr = true;                                                                                        \
     }                                                                                                     \
     gemm_mfma_bf16<a, b, TC><<<grid, 256, lds, s>>>((const bf16*)A, (const bf16*)B, (TC*)C, M, N, K, lda, ldb, \
-                                                    ldc, bs, ep);                                         \
+                                                    ldc, bs, ep, cp, part, kps);                          \
   } while (0)
-  if (ta == 0 && tb == 0) GM(0, 0);
+  if (ta == 2 && tb == 0) GM(2, 0);
+  else if (ta == 0 && tb == 0) GM(0, 0);
   else if (ta == 0 && tb == 1) GM(0, 1);
   else if (ta == 1 && tb == 0) GM(1, 0);
-  else GM(1, 1);
+  else if (ta == 1 && tb == 1) GM(1, 1);
+  else return (int)hipErrorInvalidValue;
 #undef GM
   UVA_LAUNCH_CHECK();
+  if (part) {
+    long long n = (long long)M * N;
+    long long blocks = (n + 255) / 256;
+    if (blocks > 4096) blocks = 4096;
+    splitk_reduce<TC><<<dim3((unsigned)blocks), 256, 0, s>>>(part, splits, (TC*)C, M, N, ldc, ep);
+    UVA_LAUNCH_CHECK();
+  }
   return 0;
 }
 
-extern "C" int uva_gemm(int in_dtype, int out_dtype, int ta, int tb, const void* A, const void* B, void* C, int M,
-                        int N, int K, long long lda, long long ldb, long long ldc, int batch, int batch_inner,
-                        long long sAo, long long sAi, long long sBo, long long sBi, long long sCo, long long sCi,
-                        const float* bias, const void* residual, long long ldr, long long sRo, long long sRi,
-                        void* aux, int act, float alpha, float beta, float drop_p, unsigned long long drop_seed,
-                        int force_generic, hipStream_t stream) {
-  if (M <= 0 || N <= 0 || batch <= 0) return 0;
-  BatchStrides bs{sAo, sAi, sBo, sBi, sCo, sCi, batch_inner > 0 ? batch_inner : 1};
-  EpiParams ep;
+static EpiParams make_epi(const float* bias, const void* residual, long long ldr, long long sRo, long long sRi,
+                          void* aux, int act, float alpha, float beta, float drop_p, unsigned long long drop_seed) {
+  EpiParams ep{};
   ep.bias = bias;
   ep.residual = residual;
   ep.aux = aux;
@@ -336,19 +467,64 @@ extern "C" int uva_gemm(int in_dtype, int out_dtype, int ta, int tb, const void*
   ep.ldr = ldr;
   ep.sRo = sRo;
   ep.sRi = sRi;
-  if (K <= 0) return 0;
+  return ep;
+}
+
+static int gemm_dispatch(int in_dtype, int out_dtype, int ta, int tb, const void* A, const void* B, void* C, int M,
+                         int N, int K, long long lda, long long ldb, long long ldc, int batch, const BatchStrides& bs,
+                         const EpiParams& ep, const ConvParams& cp, int force_generic, float* ws, long long ws_floats,
+                         hipStream_t stream) {
   if (in_dtype == UVA_DT_BF16) {
     // MFMA path needs 16-B chunks: K-contiguous dims and M/N-contiguous dims multiple of 8, aligned lds
-    bool ok = !force_generic && (K % 8 == 0) && (lda % 8 == 0) && (ldb % 8 == 0) && (!ta || M % 8 == 0) &&
-              (!tb || N % 8 == 0) && (((uintptr_t)A | (uintptr_t)B) % 16 == 0) && (sAo % 8 == 0) && (sAi % 8 == 0) &&
-              (sBo % 8 == 0) && (sBi % 8 == 0);
+    bool ok = !force_generic && (K % 8 == 0) && (((uintptr_t)A | (uintptr_t)B) % 16 == 0) &&
+              (bs.sAo % 8 == 0) && (bs.sAi % 8 == 0) && (bs.sBo % 8 == 0) && (bs.sBi % 8 == 0) && (ldb % 8 == 0) &&
+              (!tb || N % 8 == 0);
+    if (ta == 2) ok = ok && (cp.Ci % 8 == 0);
+    else ok = ok && (lda % 8 == 0) && (!ta || M % 8 == 0);
     if (ok) {
-      if (out_dtype == UVA_DT_BF16) return launch_mfma<bf16>(ta, tb, A, B, C, M, N, K, lda, ldb, ldc, batch, bs, ep, stream);
-      return launch_mfma<float>(ta, tb, A, B, C, M, N, K, lda, ldb, ldc, batch, bs, ep, stream);
+      if (out_dtype == UVA_DT_BF16)
+        return launch_mfma<bf16>(ta, tb, A, B, C, M, N, K, lda, ldb, ldc, batch, bs, ep, cp, ws, ws_floats, stream);
+      return launch_mfma<float>(ta, tb, A, B, C, M, N, K, lda, ldb, ldc, batch, bs, ep, cp, ws, ws_floats, stream);
     }
-    if (out_dtype == UVA_DT_BF16) return launch_generic<bf16, bf16>(ta, tb, A, B, C, M, N, K, lda, ldb, ldc, batch, bs, ep, stream);
-    return launch_generic<bf16, float>(ta, tb, A, B, C, M, N, K, lda, ldb, ldc, batch, bs, ep, stream);
+    if (out_dtype == UVA_DT_BF16)
+      return launch_generic<bf16, bf16>(ta, tb, A, B, C, M, N, K, lda, ldb, ldc, batch, bs, ep, cp, stream);
+    return launch_generic<bf16, float>(ta, tb, A, B, C, M, N, K, lda, ldb, ldc, batch, bs, ep, cp, stream);
   }
-  if (out_dtype == UVA_DT_F32) return launch_generic<float, float>(ta, tb, A, B, C, M, N, K, lda, ldb, ldc, batch, bs, ep, stream);
-  return launch_generic<float, bf16>(ta, tb, A, B, C, M, N, K, lda, ldb, ldc, batch, bs, ep, stream);
+  if (out_dtype == UVA_DT_F32)
+    return launch_generic<float, float>(ta, tb, A, B, C, M, N, K, lda, ldb, ldc, batch, bs, ep, cp, stream);
+  return launch_generic<float, bf16>(ta, tb, A, B, C, M, N, K, lda, ldb, ldc, batch, bs, ep, cp, stream);
+}
+
+extern "C" int uva_gemm(int in_dtype, int out_dtype, int ta, int tb, const void* A, const void* B, void* C, int M,
+                        int N, int K, long long lda, long long ldb, long long ldc, int batch, int batch_inner,
+                        long long sAo, long long sAi, long long sBo, long long sBi, long long sCo, long long sCi,
+                        const float* bias, const void* residual, long long ldr, long long sRo, long long sRi,
+                        void* aux, int act, float alpha, float beta, float drop_p, unsigned long long drop_seed,
+                        int res_dtype, const void* gate, long long ldg, int gate_dtype, int force_generic,
+                        float* workspace, long long ws_floats, hipStream_t stream) {
+  if (M <= 0 || N <= 0 || batch <= 0 || K <= 0) return 0;
+  if (ta == 2) return (int)hipErrorInvalidValue;  // conv view only through uva_conv2d
+  BatchStrides bs{sAo, sAi, sBo, sBi, sCo, sCi, batch_inner > 0 ? batch_inner : 1};
+  EpiParams ep = make_epi(bias, residual, ldr, sRo, sRi, aux, act, alpha, beta, drop_p, drop_seed);
+  ep.res_dt = res_dtype;
+  ep.gate = gate;
+  ep.ldg = ldg;
+  ep.gate_dt = gate_dtype;
+  ConvParams cp{};
+  return gemm_dispatch(in_dtype, out_dtype, ta, tb, A, B, C, M, N, K, lda, ldb, ldc, batch, bs, ep, cp, force_generic,
+                       workspace, ws_floats, stream);
+}
+
+extern "C" int uva_conv2d(int dtype, const void* in, const void* w, void* out, const float* bias, const void* residual,
+                          int Nimg, int Hin, int Win, int Ci, int Co, int ks, int stride, int pad_t, int pad_l,
+                          int Hout, int Wout, const float* gn_scale, const float* gn_shift, int gn_silu, int act,
+                          int force_generic, hipStream_t stream) {
+  const int M = Nimg * Hout * Wout, K = ks * ks * Ci;
+  if (M <= 0) return 0;
+  BatchStrides bs{0, 0, 0, 0, 0, 0, 1};
+  EpiParams ep = make_epi(bias, residual, Co, 0, 0, nullptr, act, 1.0f, 0.0f, 0.0f, 0);
+  ep.res_dt = dtype;
+  ConvParams cp{Hin, Win, Ci, Hout, Wout, ks, stride, pad_t, pad_l, gn_scale, gn_shift, gn_silu};
+  return gemm_dispatch(dtype, dtype, 2, 0, in, w, out, M, Co, K, 0, K, Co, 1, bs, ep, cp, force_generic, nullptr, 0,
+                       stream);
 }

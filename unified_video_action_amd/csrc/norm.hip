@@ -120,9 +120,10 @@ __global__ __launch_bounds__(256) void ln_fwd(const TI* __restrict__ x, const fl
 // ------------------------------------------------------------------------------------
 template <typename TI, typename TO, int VEC, int NC>
 __global__ __launch_bounds__(256) void ln_bwd(const TI* __restrict__ x, const float* __restrict__ w,
-                                              const TO* __restrict__ scale, long long ldm,
+                                              const float* __restrict__ b, const TO* __restrict__ scale, long long ldm,
                                               const float* __restrict__ dy, const float* __restrict__ mean_in,
-                                              const float* __restrict__ rstd_in, float* __restrict__ dx, int accum,
+                                              const float* __restrict__ rstd_in, const float* dx_base,
+                                              float* dx, int accum,
                                               TO* __restrict__ dscale, TO* __restrict__ dshift,
                                               float* __restrict__ dw_part, float* __restrict__ db_part, int rows,
                                               int D, int rows_per_block) {
@@ -156,14 +157,20 @@ __global__ __launch_bounds__(256) void ln_bwd(const TI* __restrict__ x, const fl
 #pragma unroll
       for (int i = 0; i < VEC; ++i) {
         xh[c][i] = (xv[i] - mean) * rstd;
+        // y_aff = xhat*w + b ; h = y_aff*(1+scale) + shift (modulated) or h = y_aff
+        float da = dv[i];
         if (scale) {
-          g[c][i] = dv[i] * (1.0f + sc[i]);
-          ds[i] = dv[i] * xh[c][i];
+          float ya = w ? xh[c][i] * w[col0 + i] + (b ? b[col0 + i] : 0.f) : xh[c][i];
+          da = dv[i] * (1.0f + sc[i]);
+          ds[i] = dv[i] * ya;
           dsh[i] = dv[i];
+        }
+        if (w) {
+          pw[c][i] += da * xh[c][i];
+          pb[c][i] += da;
+          g[c][i] = da * w[col0 + i];
         } else {
-          g[c][i] = w ? dv[i] * w[col0 + i] : dv[i];
-          pw[c][i] += dv[i] * xh[c][i];
-          pb[c][i] += dv[i];
+          g[c][i] = da;
         }
         s1 += g[c][i];
         s2 += g[c][i] * xh[c][i];
@@ -180,11 +187,13 @@ __global__ __launch_bounds__(256) void ln_bwd(const TI* __restrict__ x, const fl
       if (col0 >= D) continue;
       float o[VEC];
       float* dxr = dx + (long long)row * D + col0;
-      if (accum) ldv<VEC>(dxr, o);
+      const bool add = accum || dx_base;
+      if (dx_base) ldv<VEC>(dx_base + (long long)row * D + col0, o);
+      else if (accum) ldv<VEC>(dxr, o);
 #pragma unroll
       for (int i = 0; i < VEC; ++i) {
         float d = rstd * (g[c][i] - m1 - xh[c][i] * m2);
-        o[i] = accum ? o[i] + d : d;
+        o[i] = add ? o[i] + d : d;
       }
       stv<VEC>(dxr, o);
     }
@@ -329,9 +338,10 @@ extern "C" int uva_layernorm_fwd(int in_dtype, int out_dtype, const void* x, con
   return 0;
 }
 
-extern "C" int uva_layernorm_bwd(int in_dtype, int out_dtype, const void* x, const float* w, const void* scale,
-                                 long long ldm, const float* dy, const float* mean, const float* rstd, float* dx,
-                                 int accum, void* dscale, void* dshift, float* dw, float* db, int accum_wb,
+extern "C" int uva_layernorm_bwd(int in_dtype, int out_dtype, const void* x, const float* w, const float* b,
+                                 const void* scale,
+                                 long long ldm, const float* dy, const float* mean, const float* rstd,
+                                 const float* dx_base, float* dx, int accum, void* dscale, void* dshift, float* dw, float* db, int accum_wb,
                                  float* workspace, int rows, int D, hipStream_t stream) {
   if (rows <= 0) return 0;
   // dw/db via per-block partials in `workspace` (nblk * D * 2 floats), then a column sum
@@ -341,13 +351,13 @@ extern "C" int uva_layernorm_bwd(int in_dtype, int out_dtype, const void* x, con
   float* pw = dw ? workspace : nullptr;
   float* pb = dw ? workspace + (long long)nblk * D : nullptr;
   if (in_dtype == UVA_DT_F32 && out_dtype == UVA_DT_F32)
-    DISPATCH_LN(ln_bwd, float, float, (const float*)x, w, (const float*)scale, ldm, dy, mean, rstd, dx, accum,
+    DISPATCH_LN(ln_bwd, float, float, (const float*)x, w, b, (const float*)scale, ldm, dy, mean, rstd, dx_base, dx, accum,
                 (float*)dscale, (float*)dshift, pw, pb, rows, D, rpb);
   else if (in_dtype == UVA_DT_F32 && out_dtype == UVA_DT_BF16)
-    DISPATCH_LN(ln_bwd, float, bf16, (const float*)x, w, (const bf16*)scale, ldm, dy, mean, rstd, dx, accum,
+    DISPATCH_LN(ln_bwd, float, bf16, (const float*)x, w, b, (const bf16*)scale, ldm, dy, mean, rstd, dx_base, dx, accum,
                 (bf16*)dscale, (bf16*)dshift, pw, pb, rows, D, rpb);
   else if (in_dtype == UVA_DT_BF16 && out_dtype == UVA_DT_BF16)
-    DISPATCH_LN(ln_bwd, bf16, bf16, (const bf16*)x, w, (const bf16*)scale, ldm, dy, mean, rstd, dx, accum,
+    DISPATCH_LN(ln_bwd, bf16, bf16, (const bf16*)x, w, b, (const bf16*)scale, ldm, dy, mean, rstd, dx_base, dx, accum,
                 (bf16*)dscale, (bf16*)dshift, pw, pb, rows, D, rpb);
   else
     return (int)hipErrorInvalidValue;

@@ -1,0 +1,169 @@
+// KL-VAE encoder plumbing around the implicit-GEMM convolutions (gemm.hip uva_conv2d):
+//   frame select + bilinear resize + pixel normalisation  (data_utils.py:19-83,140-158,206-226)
+//   GroupNorm(32, eps 1e-6) statistics -> per-(image, channel) scale/shift consumed by the
+//     next convolution's A-loader (vaekl.py:14-17)
+//   posterior sample  z = (mean + exp(0.5*clamp(logvar,-30,20)) * eps) * 0.2325
+//     (vaekl.py:400-417, data_utils.py:391-399), written directly as MAR tokens.
+#include "common.h"
+
+// obs image [B, T, 3, Hin, Win] fp32 in [0,1] -> NHWC [B*nsel, 256, 256, Cpad] (dtype odt)
+// image order: first every sample's future frames (sel[half..]), then the history frames
+// (get_vae_latent encodes x = future first, then c = history: data_utils.py:405-424).
+__global__ void resize_select_kernel(const float* __restrict__ img, int B, int T, int Hin, int Win,
+                                     const int* __restrict__ sel, int nsel, void* out, int odt, int Cpad) {
+  const int HO = 256, WO = 256;
+  const long long total = (long long)B * nsel * HO * WO;
+  const float sh = (float)Hin / HO, sw = (float)Win / WO;
+  const int half = nsel / 2;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long long)gridDim.x * blockDim.x) {
+    const int ox = i % WO;
+    const int oy = (i / WO) % HO;
+    const long long img_id = i / (HO * WO);  // output image index
+    const int part = img_id / ((long long)B * half);  // 0: future, 1: history
+    const int rem = img_id % ((long long)B * half);
+    const int b = rem / half, f = rem % half;
+    const int frame = sel[(part == 0 ? half : 0) + f];
+    float sy = sh * (oy + 0.5f) - 0.5f;
+    float sx = sw * (ox + 0.5f) - 0.5f;
+    sy = sy < 0.f ? 0.f : sy;
+    sx = sx < 0.f ? 0.f : sx;
+    int y0 = (int)sy, x0 = (int)sx;
+    int y1 = y0 + (y0 < Hin - 1 ? 1 : 0), x1 = x0 + (x0 < Win - 1 ? 1 : 0);
+    float ly = sy - y0, lx = sx - x0;
+    float hy = 1.f - ly, hx = 1.f - lx;
+    const float* base = img + ((long long)b * T + frame) * 3 * Hin * Win;
+    for (int c = 0; c < Cpad; ++c) {
+      float v = 0.f;
+      if (c < 3) {
+        const float* p = base + (long long)c * Hin * Win;
+        float r = hy * (hx * p[y0 * Win + x0] + lx * p[y0 * Win + x1]) + ly * (hx * p[y1 * Win + x0] + lx * p[y1 * Win + x1]);
+        v = (r * 255.0f) / 127.5f - 1.0f;
+      }
+      long long o = i * Cpad + c;
+      if (odt == UVA_DT_BF16) ((bf16*)out)[o] = (bf16)v;
+      else ((float*)out)[o] = v;
+    }
+  }
+}
+
+// GroupNorm partial sums: grid (Nimg, chunks).  x NHWC [Nimg, HW, C].
+// part[n][chunk][g][0..1] = (sum, sumsq) of the chunk's pixels for group g (32 groups)
+template <typename T>
+__global__ __launch_bounds__(256) void gn_partial_kernel(const T* __restrict__ x, int HW, int C, int pix_per_chunk,
+                                                         float* __restrict__ part) {
+  __shared__ float red[2][512];
+  const int n = blockIdx.x, chunk = blockIdx.y, nch = gridDim.y;
+  const int p0 = chunk * pix_per_chunk, p1 = min(HW, p0 + pix_per_chunk);
+  // each thread: fixed channel c, pixels strided by (256 / C) lanes
+  for (int i = threadIdx.x; i < 2 * C; i += 256) red[i / C][i % C] = 0.f;
+  __syncthreads();
+  const int tpc = 256 / C >= 1 ? 256 / C : 1;
+  for (int c0 = 0; c0 < C; c0 += 256) {
+    const int c = c0 + (threadIdx.x % min(C, 256));
+    const int pl = threadIdx.x / min(C, 256);
+    float s = 0.f, q = 0.f;
+    if (c < C)
+      for (int p = p0 + pl; p < p1; p += tpc) {
+        float v = to_f32(x[((long long)n * HW + p) * C + c]);
+        s += v;
+        q += v * v;
+      }
+    if (c < C) {
+      atomicAdd(&red[0][c], s);
+      atomicAdd(&red[1][c], q);
+    }
+  }
+  __syncthreads();
+  const int gs = C / 32;
+  if (threadIdx.x < 32) {
+    float s = 0.f, q = 0.f;
+    for (int j = 0; j < gs; ++j) {
+      s += red[0][threadIdx.x * gs + j];
+      q += red[1][threadIdx.x * gs + j];
+    }
+    float* o = part + (((long long)n * nch + chunk) * 32 + threadIdx.x) * 2;
+    o[0] = s;
+    o[1] = q;
+  }
+}
+
+// finalize: per (n, c) scale = gamma*rstd, shift = beta - mean*scale
+__global__ void gn_finalize_kernel(const float* __restrict__ part, int nch, int HW, int C, const float* __restrict__ gamma,
+                                   const float* __restrict__ beta, float eps, float* __restrict__ scale,
+                                   float* __restrict__ shift, int Nimg) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (long long)Nimg * C) return;
+  const int n = i / C, c = i % C, gs = C / 32, g = c / gs;
+  double s = 0.0, q = 0.0;
+  for (int k = 0; k < nch; ++k) {
+    const float* o = part + (((long long)n * nch + k) * 32 + g) * 2;
+    s += o[0];
+    q += o[1];
+  }
+  const double cnt = (double)HW * gs;
+  const double mean = s / cnt;
+  double var = q / cnt - mean * mean;
+  if (var < 0) var = 0;
+  const float rstd = (float)(1.0 / sqrt(var + (double)eps));
+  const float sc = gamma[c] * rstd;
+  scale[i] = sc;
+  shift[i] = beta[c] - (float)mean * sc;
+}
+
+// moments NHWC [Nimg, 256, 32] -> tokens [Nimg, 256, 16] (fp32); eps given NCHW [Nimg,16,16,16]
+__global__ void posterior_kernel(const void* __restrict__ mom, int mdt, const float* __restrict__ eps,
+                                 float* __restrict__ z, int Nimg, float scale) {
+  const long long total = (long long)Nimg * 256 * 16;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long long)gridDim.x * blockDim.x) {
+    const int c = i % 16;
+    const long long pix = i / 16;
+    const int s = pix % 256;
+    const long long n = pix / 256;
+    float mean = mdt == UVA_DT_BF16 ? (float)((const bf16*)mom)[pix * 32 + c] : ((const float*)mom)[pix * 32 + c];
+    float lv = mdt == UVA_DT_BF16 ? (float)((const bf16*)mom)[pix * 32 + 16 + c] : ((const float*)mom)[pix * 32 + 16 + c];
+    lv = fminf(fmaxf(lv, -30.0f), 20.0f);
+    const float e = eps[(n * 16 + c) * 256 + s];
+    z[i] = (mean + expf(0.5f * lv) * e) * scale;
+  }
+}
+
+static inline dim3 gridn(long long n) {
+  long long b = (n + 255) / 256;
+  if (b > 16384) b = 16384;
+  return dim3((unsigned)(b < 1 ? 1 : b));
+}
+
+extern "C" int uva_resize_select(const float* img, int B, int T, int Hin, int Win, const int* sel, int nsel, int odt,
+                                 void* out, int Cpad, hipStream_t s) {
+  resize_select_kernel<<<gridn((long long)B * nsel * 256 * 256), 256, 0, s>>>(img, B, T, Hin, Win, sel, nsel, out, odt,
+                                                                              Cpad);
+  UVA_LAUNCH_CHECK();
+  return 0;
+}
+
+extern "C" long long uva_groupnorm_workspace(int Nimg, int HW) {
+  int nch = (HW + 1023) / 1024;
+  return (long long)Nimg * nch * 32 * 2;
+}
+
+extern "C" int uva_groupnorm_stats(int dtype, const void* x, int Nimg, int HW, int C, const float* gamma,
+                                   const float* beta, float eps, float* scale, float* shift, float* workspace,
+                                   hipStream_t s) {
+  if (C % 32 != 0 || C > 512) return (int)hipErrorInvalidValue;
+  const int ppc = 1024;
+  const int nch = (HW + ppc - 1) / ppc;
+  dim3 g1(Nimg, nch);
+  if (dtype == UVA_DT_BF16) gn_partial_kernel<bf16><<<g1, 256, 0, s>>>((const bf16*)x, HW, C, ppc, workspace);
+  else gn_partial_kernel<float><<<g1, 256, 0, s>>>((const float*)x, HW, C, ppc, workspace);
+  gn_finalize_kernel<<<gridn((long long)Nimg * C), 256, 0, s>>>(workspace, nch, HW, C, gamma, beta, eps, scale, shift,
+                                                                 Nimg);
+  UVA_LAUNCH_CHECK();
+  return 0;
+}
+
+extern "C" int uva_posterior_sample(int mdt, const void* moments, const float* eps, float* z, int Nimg, float scale,
+                                    hipStream_t s) {
+  posterior_kernel<<<gridn((long long)Nimg * 4096), 256, 0, s>>>(moments, mdt, eps, z, Nimg, scale);
+  UVA_LAUNCH_CHECK();
+  return 0;
+}

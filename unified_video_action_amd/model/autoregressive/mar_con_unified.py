@@ -1,0 +1,319 @@
+"""MAR video+action transformer on the HIP path (reference:
+model/autoregressive/mar_con_unified.py:28-943; size presets :1162-1234).
+
+Same constructor surface and parameter names (timm Block names norm1/attn.qkv/attn.proj/
+norm2/mlp.fc1/mlp.fc2) as the reference, so `model.policy.autoregressive_model_params.*`
+configs and checkpoints carry over.  Training forward only (the sampler is §8f "next").
+
+Token layout: latents arrive either in the reference layout [B, T, C, H, W] or already
+patchified as tokens [B, T, 256, C] (the VAE path writes tokens directly); token index
+t*256 + h*16 + w, channels last.  Every random draw can be injected through `rng`
+(orders, mask_rate, text_drop_u, randint/randn_like queues) for bit-exact token indexing
+against the reference; otherwise they are drawn like the reference (numpy shuffle,
+scipy truncnorm, torch RNG).
+"""
+from functools import partial
+
+import numpy as np
+import scipy.stats as stats
+import torch
+import torch.nn as nn
+
+from ...runtime import cdt
+from .diffusion_action_loss import DiffActLoss
+from .diffusion_loss import DiffLoss
+from .functional import F32, block_forward, layer_norm, linear
+
+
+class Attention(nn.Module):
+    def __init__(self, dim, num_heads, qkv_bias=True):
+        super().__init__()
+        assert dim % num_heads == 0
+        self.num_heads = num_heads
+        self.qkv = nn.Linear(dim, 3 * dim, bias=qkv_bias)
+        self.proj = nn.Linear(dim, dim)
+
+
+class Mlp(nn.Module):
+    def __init__(self, dim, hidden):
+        super().__init__()
+        self.fc1 = nn.Linear(dim, hidden)
+        self.fc2 = nn.Linear(hidden, dim)
+
+
+class Block(nn.Module):
+    """timm 0.9.7 Block (pre-LN); forward = functional.BlockFn (one fused autograd node)."""
+
+    def __init__(self, dim, num_heads, mlp_ratio=4.0, qkv_bias=True, norm_layer=nn.LayerNorm, proj_drop=0.0,
+                 attn_drop=0.0):
+        super().__init__()
+        self.norm1 = norm_layer(dim)
+        self.attn = Attention(dim, num_heads, qkv_bias)
+        self.norm2 = norm_layer(dim)
+        self.mlp = Mlp(dim, int(dim * mlp_ratio))
+        self.attn_drop = attn_drop
+        self.proj_drop = proj_drop
+
+    def forward(self, x):
+        B, N, _ = x.shape
+        pa = self.attn_drop if self.training else 0.0
+        pp = self.proj_drop if self.training else 0.0
+        return block_forward(self, x, B, N, pa, pp)
+
+
+class MAR(nn.Module):
+    def __init__(self, img_size=256, vae_stride=16, patch_size=1, encoder_embed_dim=1024, encoder_depth=16,
+                 encoder_num_heads=16, decoder_embed_dim=1024, decoder_depth=16, decoder_num_heads=16,
+                 mlp_ratio=4.0, norm_layer=nn.LayerNorm, vae_embed_dim=16, mask_ratio_min=0.7, label_drop_prob=0.1,
+                 attn_dropout=0.1, proj_dropout=0.1, diffloss_d=3, diffloss_w=1024, diffloss_act_d=3,
+                 diffloss_act_w=1024, num_sampling_steps="100", diffusion_batch_mul=4, grad_checkpointing=False,
+                 predict_video=True, act_diff_training_steps=1000, act_diff_testing_steps="100",
+                 action_model_params={}, **kwargs):
+        super().__init__()
+        self.task_name = kwargs["task_name"]
+        self.different_history_freq = kwargs.get("different_history_freq") or False
+        self.use_history_action = kwargs.get("use_history_action") or False
+        self.use_proprioception = kwargs.get("use_proprioception") or False
+        self.predict_wrist_img = kwargs.get("predict_wrist_img") or False
+        self.predict_proprioception = kwargs.get("predict_proprioception") or False
+        if self.use_history_action or self.predict_wrist_img:
+            raise NotImplementedError("history-action / wrist-image variants are outside the accelerated path")
+        self.n_frames = 4
+        self.seq_h = self.seq_w = img_size // vae_stride // patch_size
+        self.seq_len = self.seq_h * self.seq_w
+        self.token_embed_dim = vae_embed_dim * patch_size ** 2
+        self.vae_embed_dim = vae_embed_dim
+        self.label_drop_prob = label_drop_prob
+        self.attn_dropout, self.proj_dropout = attn_dropout, proj_dropout
+        self.mask_ratio_generator = stats.truncnorm((mask_ratio_min - 1.0) / 0.25, 0, loc=1.0, scale=0.25)
+        D, Dd = encoder_embed_dim, decoder_embed_dim
+        self.z_proj_cond = nn.Linear(self.token_embed_dim, D)
+        self.z_proj = nn.Linear(self.token_embed_dim, D)
+        self.predict_action = action_model_params["predict_action"]
+        act_dim = kwargs["shape_meta"]["action"]["shape"][0]
+        self.action_proj_cond = nn.Linear(act_dim, D)
+        self.buffer_size_action = 64
+        self.fake_latent_x = nn.Parameter(torch.zeros(1, D))
+        self.fake_action_latent = nn.Parameter(torch.zeros(1, D))
+        n_streams = 3
+        if self.use_proprioception:
+            if self.task_name != "umi":
+                raise NotImplementedError("proprioception is accelerated for the UMI path only")
+            self.buffer_size_properception = 64 * 4 if self.different_history_freq else 64
+            self.proprioception_proj_cond = nn.Linear(16, D)
+            self.proprioception_image_proj_cond = nn.Linear(self.token_embed_dim, D)
+            n_streams += 1
+        self.language_emb_model = kwargs.get("language_emb_model")
+        self.clip = self.language_emb_model == "clip"
+        if self.clip:
+            self.fake_latent = nn.Parameter(torch.zeros(1, D))
+            self.text_proj_cond = nn.Linear(512, D)
+            self.buffer_size_text = 64
+            self.text_pos_embed = nn.Parameter(torch.zeros(1, self.buffer_size_text, D))
+        self.proj_cond_x_layer = nn.Linear(n_streams * D, D)
+        self.temporal_pos_embed = nn.Parameter(torch.zeros(1, self.n_frames, D))
+        self.spatial_pos_embed = nn.Parameter(torch.zeros(1, self.seq_len, D))
+        self.z_proj_ln = nn.LayerNorm(D, eps=1e-6)
+        blk = partial(Block, mlp_ratio=mlp_ratio, qkv_bias=True, norm_layer=norm_layer, proj_drop=proj_dropout,
+                      attn_drop=attn_dropout)
+        self.encoder_blocks = nn.ModuleList([blk(D, encoder_num_heads) for _ in range(encoder_depth)])
+        self.encoder_norm = norm_layer(D)
+        self.decoder_embed = nn.Linear(D, Dd)
+        self.decoder_temporal_pos_embed = nn.Parameter(torch.zeros(1, self.n_frames, Dd))
+        self.decoder_spatial_pos_embed = nn.Parameter(torch.zeros(1, self.seq_len, Dd))
+        if self.clip:
+            self.decoder_text_pos_embed = nn.Parameter(torch.zeros(1, self.buffer_size_text, Dd))
+        self.decoder_blocks = nn.ModuleList([blk(Dd, decoder_num_heads) for _ in range(decoder_depth)])
+        self.decoder_norm = norm_layer(Dd)
+        self.diffusion_temporal_embed = nn.Parameter(torch.zeros(1, self.n_frames, Dd))
+        self.diffusion_spatial_embed = nn.Parameter(torch.zeros(1, self.seq_len, Dd))
+        self.initialize_weights()
+        self.predict_video = predict_video
+        if predict_video:
+            self.diffloss = DiffLoss(self.token_embed_dim, Dd, diffloss_d, diffloss_w, num_sampling_steps,
+                                     grad_checkpointing, n_frames=self.n_frames)
+        if self.predict_action:
+            self.diffactloss = DiffActLoss(act_dim, Dd, diffloss_act_d, diffloss_act_w, num_sampling_steps,
+                                           grad_checkpointing, n_frames=self.n_frames,
+                                           act_model_type=action_model_params.get("act_model_type", "conv_fc"),
+                                           act_diff_training_steps=act_diff_training_steps)
+        if self.predict_proprioception:
+            if self.task_name != "umi":
+                raise NotImplementedError
+            self.diffproploss = DiffActLoss(6, Dd, diffloss_act_d, diffloss_act_w, num_sampling_steps,
+                                            grad_checkpointing, n_frames=self.n_frames,
+                                            act_diff_training_steps=act_diff_training_steps)
+
+    # ---- init (mar_con_unified.py:349-391) ----------------------------------------------
+    def initialize_weights(self):
+        for p in (self.fake_latent_x, self.fake_action_latent, self.temporal_pos_embed, self.spatial_pos_embed,
+                  self.decoder_temporal_pos_embed, self.decoder_spatial_pos_embed, self.diffusion_temporal_embed,
+                  self.diffusion_spatial_embed):
+            nn.init.normal_(p, std=0.02)
+        if self.clip:
+            for p in (self.fake_latent, self.text_pos_embed, self.decoder_text_pos_embed):
+                nn.init.normal_(p, std=0.02)
+        for m in self.modules():
+            if isinstance(m, nn.Linear):
+                nn.init.xavier_uniform_(m.weight)
+                if m.bias is not None:
+                    nn.init.zeros_(m.bias)
+            elif isinstance(m, nn.LayerNorm) and m.weight is not None:
+                nn.init.ones_(m.weight)
+                nn.init.zeros_(m.bias)
+
+    # ---- token bookkeeping (bit-exact index semantics of :393-443) ------------------------
+    @staticmethod
+    def to_tokens(z):
+        """[B,T,C,H,W] -> [B,T,H*W,C]  or pass-through [B,T,S,C]."""
+        if z.dim() == 5:
+            B, T, C, H, W = z.shape
+            return z.permute(0, 1, 3, 4, 2).reshape(B, T, H * W, C)
+        return z
+
+    def sample_orders(self, bsz):
+        orders = []
+        for _ in range(bsz):
+            order = np.arange(self.seq_len)
+            np.random.shuffle(order)
+            orders.append(order)
+        return np.stack(orders)
+
+    def token_mask(self, orders, mask_rate, device):
+        """[B, T*S] float mask: 1 for the first ceil(S*rate) tokens of each order, every frame."""
+        B = orders.shape[0]
+        n = int(np.ceil(self.seq_len * mask_rate))
+        sm = np.zeros((B, self.seq_len), np.float32)
+        np.put_along_axis(sm, np.asarray(orders)[:, :n], 1.0, axis=1)
+        m = np.repeat(sm[:, None, :], self.n_frames, axis=1).reshape(B, -1)
+        return torch.from_numpy(m).to(device)
+
+    def _pos(self, temporal, spatial):
+        return (temporal[:, :, None, :] + spatial[:, None, :, :]).reshape(1, -1, temporal.shape[-1])
+
+    # ---- encoder (:445-659) -------------------------------------------------------------
+    def forward_mae_encoder(self, x, mask, cond, text_latents, nactions, task_mode, prop, text_drop_u):
+        B, T, S, _ = x.shape
+        D = self.fake_latent_x.shape[1]
+        c = cdt()
+        fake = self.fake_latent_x.to(c)
+        if task_mode == "policy_model":
+            cond_e = linear(cond, self.z_proj_cond, out_dtype=c).reshape(B, T * S, D)
+            x_e = fake.expand(B, T * S, D)
+        elif task_mode == "inverse_model":
+            x_e = linear(x, self.z_proj, out_dtype=c).reshape(B, T * S, D)
+            cond_e = fake.expand(B, T * S, D)
+        else:
+            cond_e = linear(cond, self.z_proj_cond, out_dtype=c).reshape(B, T * S, D)
+            x_e = linear(x, self.z_proj, out_dtype=c).reshape(B, T * S, D)
+            x_e = torch.where(mask[..., None] == 1, fake.expand(B, T * S, D), x_e)
+        if task_mode == "dynamic_model":
+            act = linear(nactions, self.action_proj_cond, out_dtype=c)
+        else:
+            act = self.fake_action_latent.to(c)[None].expand(B, 16, D)
+        streams = [x_e, cond_e, act.repeat_interleave(self.buffer_size_action, dim=1)]
+        if self.use_proprioception:
+            ps = torch.cat([prop["robot0_eef_pos"], prop["robot0_eef_rot_axis_angle"], prop["robot0_gripper_width"],
+                            prop["robot0_eef_rot_axis_angle_wrt_start"]], dim=-1).float()
+            pe = linear(ps, self.proprioception_proj_cond, out_dtype=c)
+            streams.append(pe.repeat_interleave(self.buffer_size_properception, dim=1))
+        h = linear(torch.cat(streams, dim=-1), self.proj_cond_x_layer, out_dtype=F32)
+        h = h + self._pos(self.temporal_pos_embed, self.spatial_pos_embed)
+        if self.clip:
+            txt = text_latents[:, None, :].expand(B, self.buffer_size_text, D)
+            if self.training:
+                drop = (text_drop_u < self.label_drop_prob).to(F32).to(h.device)[:, None, None]
+                txt = drop * self.fake_latent[:, None, :] + (1 - drop) * txt
+            h = torch.cat([txt + self.text_pos_embed, h], dim=1)
+        h = layer_norm(h, self.z_proj_ln, out_dtype=F32)
+        for blk in self.encoder_blocks:
+            h = blk(h)
+        return layer_norm(h, self.encoder_norm, out_dtype=c)
+
+    # ---- decoder (:661-726) -------------------------------------------------------------
+    def forward_mae_decoder(self, x):
+        h = linear(x, self.decoder_embed, out_dtype=F32)
+        pos = self._pos(self.decoder_temporal_pos_embed, self.decoder_spatial_pos_embed)
+        if self.clip:
+            pos = torch.cat([self.decoder_text_pos_embed, pos], dim=1)
+        h = h + pos
+        for blk in self.decoder_blocks:
+            h = blk(h)
+        h = layer_norm(h, self.decoder_norm, out_dtype=F32)
+        if self.clip:
+            h = h[:, self.buffer_size_text:]
+        return h + self._pos(self.diffusion_temporal_embed, self.diffusion_spatial_embed)
+
+    # ---- losses (:728-787) --------------------------------------------------------------
+    def forward_loss(self, z, target, mask, nactions, task_mode, prop, draws):
+        zero = torch.zeros((), device=z.device)
+        video_loss = act_loss = zero
+
+        def nxt():
+            t = draws["randint"].pop(0) if draws["randint"] else None
+            nz = draws["randn_like"].pop(0) if draws["randn_like"] else None
+            return t, nz
+
+        if task_mode in ("video_model", "dynamic_model", "full_dynamic_model"):
+            t, nz = nxt()
+            video_loss = self.diffloss(target, z, mask, t=t, noise=nz)
+        if task_mode in ("policy_model", "inverse_model", "full_dynamic_model"):
+            t, nz = nxt()
+            act_loss = self.diffactloss(nactions, z, task_mode, t=t, noise=nz)
+        if task_mode == "full_dynamic_model":
+            loss = video_loss + act_loss
+        elif task_mode in ("video_model", "dynamic_model"):
+            loss = video_loss
+        else:
+            loss = act_loss
+        if self.predict_proprioception:
+            t, nz = nxt()
+            loss = loss + self.diffproploss(prop["robot0_eef_rot_axis_angle_wrt_start_pred"], z, t=t, noise=nz)
+        return loss, video_loss, act_loss
+
+    def forward(self, imgs, cond, history_nactions=None, nactions=None, text_latents=None, task_mode=None,
+                proprioception_input={}, rng=None):
+        dev = cond.device
+        x = self.to_tokens(imgs).to(F32)
+        cnd = self.to_tokens(cond).to(F32)
+        B = x.shape[0]
+        if text_latents is not None and self.clip:
+            text_latents = linear(text_latents.to(dev).float(), self.text_proj_cond, out_dtype=F32)
+        gt = x.reshape(B, -1, x.shape[-1])
+        rng = rng or {}
+        orders = rng["orders"] if "orders" in rng else self.sample_orders(B)
+        rate = rng["mask_rate"] if "mask_rate" in rng else self.mask_ratio_generator.rvs(1)[0]
+        mask = self.token_mask(orders, rate, dev)
+        tdu = rng.get("text_drop_u")
+        tdu = torch.as_tensor(tdu) if tdu is not None else torch.rand(B)
+        draws = {"randint": [torch.as_tensor(a).to(dev) for a in rng.get("randint", [])],
+                 "randn_like": [torch.as_tensor(a).to(dev) for a in rng.get("randn_like", [])]}
+        h = self.forward_mae_encoder(x, mask, cnd, text_latents, nactions, task_mode, proprioception_input, tdu)
+        z = self.forward_mae_decoder(h)
+        return self.forward_loss(z, gt, mask, nactions, task_mode, proprioception_input, draws)
+
+
+def _mar(D, depth, heads, **kwargs):
+    return MAR(encoder_embed_dim=D, encoder_depth=depth, encoder_num_heads=heads, decoder_embed_dim=D,
+               decoder_depth=depth, decoder_num_heads=heads, mlp_ratio=4,
+               norm_layer=partial(nn.LayerNorm, eps=1e-6), **kwargs)
+
+
+def mar_tiny(**kw):
+    return _mar(768, 3, 6, **kw)
+
+
+def mar_small(**kw):
+    return _mar(768, 6, 6, **kw)
+
+
+def mar_base(**kw):
+    return _mar(768, 12, 12, **kw)
+
+
+def mar_large(**kw):
+    return _mar(1024, 16, 16, **kw)
+
+
+def mar_huge(**kw):
+    return _mar(1280, 20, 16, **kw)

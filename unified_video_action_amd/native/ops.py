@@ -34,28 +34,32 @@ def _ld(t):
 
 def gemm(A, B, C, M, N, K, lda, ldb, ldc, ta=0, tb=0, batch=1, inner=1, sA=(0, 0), sB=(0, 0), sC=(0, 0),
          bias=None, residual=None, ldr=0, sR=(0, 0), aux=None, act="none", alpha=1.0, beta=0.0,
-         drop_p=0.0, seed=0, force_generic=False):
+         drop_p=0.0, seed=0, force_generic=False, splitk=True, gate=None, ldg=0):
     assert A.dtype == B.dtype, (A.dtype, B.dtype)
+    ws = workspace(SPLITK_WS_FLOATS, A.device) if (splitk and batch == 1) else None
     if bias is not None:
         assert bias.dtype == torch.float32 and bias.is_contiguous()
-    if residual is not None:
-        assert residual.dtype == C.dtype
     if aux is not None:
         assert aux.dtype == C.dtype
     lib().call("uva_gemm", dt(A), dt(C), ta, tb, ptr(A), ptr(B), ptr(C), M, N, K, lda, ldb, ldc, batch, inner,
                sA[0], sA[1], sB[0], sB[1], sC[0], sC[1], ptr(bias), ptr(residual), ldr, sR[0], sR[1], ptr(aux),
                ACT[act] if isinstance(act, str) else act, float(alpha), float(beta), float(drop_p),
-               int(seed) & 0xFFFFFFFFFFFFFFFF, int(force_generic), stream())
+               int(seed) & 0xFFFFFFFFFFFFFFFF, dt(residual) if residual is not None else 0, ptr(gate), ldg,
+               dt(gate) if gate is not None else 0, int(force_generic), ptr(ws),
+               ws.numel() if ws is not None else 0, stream())
 
 
-def linear(x, w, out, bias=None, act="none", aux=None, residual=None, drop_p=0.0, seed=0, beta=0.0):
+SPLITK_WS_FLOATS = 1 << 25  # 128 MB fp32 partial slabs
+
+
+def linear(x, w, out, bias=None, act="none", aux=None, residual=None, drop_p=0.0, seed=0, beta=0.0, gate=None):
     """out[M,N] = epi(x[M,K] @ w[N,K]^T) -- nn.Linear forward."""
     M, K = x.shape
     N = w.shape[0]
     assert w.shape[1] == K and out.shape == (M, N)
     gemm(x, w, out, M, N, K, _ld(x), _ld(w), _ld(out), 0, 0, bias=bias, act=act, aux=aux,
          residual=residual, ldr=_ld(residual) if residual is not None else 0, drop_p=drop_p, seed=seed,
-         beta=beta)
+         beta=beta, gate=gate, ldg=_ld(gate) if gate is not None else 0)
 
 
 def linear_dx(dy, w, dx, beta=0.0):
@@ -100,15 +104,17 @@ def layernorm_fwd(x, w, b, y, mean, rstd, eps=1e-6, scale=None, shift=None, ldm=
 
 
 def layernorm_bwd(x, w, dy, mean, rstd, dx, accum, dw=None, db=None, scale=None, ldm=0, dscale=None, dshift=None,
-                  out_dtype=None, accum_wb=True):
+                  out_dtype=None, accum_wb=True, dx_base=None, b=None):
+    """dx (= dx_base +) LN backward.  With `scale` (adaLN modulation) the affine (w, b) output is
+    modulated: h = (xhat*w + b)*(1+scale) + shift; b is needed for d(scale)."""
     rows, D = x.shape
     assert dy.dtype == torch.float32 and dx.dtype == torch.float32
     odt = out_dtype if out_dtype is not None else (dt(scale) if scale is not None else dt(x))
     ws = None
     if dw is not None:
         ws = workspace(lib().query("uva_layernorm_bwd_workspace", rows, D), x.device)
-    lib().call("uva_layernorm_bwd", dt(x), odt, ptr(x), ptr(w), ptr(scale), ldm, ptr(dy), ptr(mean), ptr(rstd),
-               ptr(dx), int(accum), ptr(dscale), ptr(dshift), ptr(dw), ptr(db), int(accum_wb), ptr(ws), rows, D,
+    lib().call("uva_layernorm_bwd", dt(x), odt, ptr(x), ptr(w), ptr(b), ptr(scale), ldm, ptr(dy), ptr(mean), ptr(rstd),
+               ptr(dx_base), ptr(dx), int(accum), ptr(dscale), ptr(dshift), ptr(dw), ptr(db), int(accum_wb), ptr(ws), rows, D,
                stream())
 
 
@@ -194,3 +200,44 @@ def adamw_ema(p, g, m, v, ema, p_bf16, n_decay, lr, b1, b2, eps, wd, step, grad_
     lib().call("uva_adamw_ema", ptr(p), ptr(g), ptr(m), ptr(v), ptr(ema), ptr(p_bf16), p.numel(), int(n_decay),
                float(lr), float(b1), float(b2), float(eps), float(wd), int(step), float(grad_scale),
                float(ema_decay), stream())
+
+
+def attn_fwd(qkv, out, lse2, B, N, H, scale, drop_p=0.0, seed=0):
+    assert qkv.dtype == torch.bfloat16 and qkv.is_contiguous() and out.is_contiguous()
+    assert N % 64 == 0 and qkv.shape[-1] == 3 * H * 64
+    lib().call("uva_attn_fwd", ptr(qkv), ptr(out), ptr(lse2), B, N, H, float(scale), float(drop_p),
+               int(seed) & 0xFFFFFFFFFFFFFFFF, stream())
+
+
+def attn_bwd(qkv, out, dout, lse2, dvec, dqkv, B, N, H, scale, drop_p=0.0, seed=0):
+    assert dout.dtype == torch.bfloat16 and dout.is_contiguous() and dqkv.is_contiguous()
+    lib().call("uva_attn_bwd", ptr(qkv), ptr(out), ptr(dout), ptr(lse2), ptr(dvec), ptr(dqkv), B, N, H,
+               float(scale), float(drop_p), int(seed) & 0xFFFFFFFFFFFFFFFF, stream())
+
+
+def conv2d(x, w, out, Nimg, Hin, Win, Ci, Co, ks, stride, pad_t, pad_l, Hout, Wout, bias=None, residual=None,
+           gn_scale=None, gn_shift=None, gn_silu=True, act="none", force_generic=False):
+    """NHWC implicit-GEMM conv; w stored [Co][ks][ks][Ci]."""
+    assert x.dtype == w.dtype == out.dtype
+    assert w.numel() == Co * ks * ks * Ci and out.numel() == Nimg * Hout * Wout * Co
+    if residual is not None:
+        assert residual.dtype == out.dtype and residual.numel() == out.numel()
+    lib().call("uva_conv2d", dt(x), ptr(x), ptr(w), ptr(out), ptr(bias), ptr(residual), Nimg, Hin, Win, Ci, Co, ks,
+               stride, pad_t, pad_l, Hout, Wout, ptr(gn_scale), ptr(gn_shift), int(gn_silu), ACT[act],
+               int(force_generic), stream())
+
+
+def groupnorm_stats(x, Nimg, HW, C, gamma, beta, scale, shift, eps=1e-6):
+    ws = workspace(lib().query("uva_groupnorm_workspace", Nimg, HW), x.device)
+    lib().call("uva_groupnorm_stats", dt(x), ptr(x), Nimg, HW, C, ptr(gamma), ptr(beta), float(eps), ptr(scale),
+               ptr(shift), ptr(ws), stream())
+
+
+def resize_select(img, sel, out, Cpad):
+    B, T, C, H, W = img.shape
+    assert C == 3 and img.dtype == torch.float32 and img.is_contiguous()
+    lib().call("uva_resize_select", ptr(img), B, T, H, W, ptr(sel), sel.numel(), dt(out), ptr(out), Cpad, stream())
+
+
+def posterior_sample(moments, eps, z, Nimg, scale=0.2325):
+    lib().call("uva_posterior_sample", dt(moments), ptr(moments), ptr(eps), ptr(z), Nimg, float(scale), stream())
