@@ -134,10 +134,20 @@ class Block(nn.Module):
         self.attn = _Attn(dim, heads)
         self.norm2 = nn.LayerNorm(dim, eps=LN_EPS)
         self.mlp = _Mlp(dim, int(dim * mlp_ratio))
+        self.p_drop = 0.0  # attn_dropout = proj_dropout (uva.yaml:31-32); 0 for parity runs
 
     def forward(self, x):
-        x = x + self.attn(self.norm1(x))
-        return x + self.mlp(self.norm2(x))
+        p = self.p_drop if self.training else 0.0
+        x = x + F.dropout(self.attn(self.norm1(x), p), p, self.training)
+        h = F.dropout(F.gelu(self.mlp.fc1(self.norm2(x))), p, self.training)
+        return x + F.dropout(self.mlp.fc2(h), p, self.training)
+
+
+def set_dropout(model, p):
+    """configure the 4 timm Block dropouts (only for CPU-baseline timing; parity uses 0)."""
+    for m in model.modules():
+        if isinstance(m, Block):
+            m.p_drop = p
 
 
 # --------------------------------------------------------------------------------------

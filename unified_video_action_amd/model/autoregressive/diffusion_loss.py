@@ -110,7 +110,7 @@ class SimpleMLPAdaLN(nn.Module):
         for blk in self.res_blocks:
             params += blk.trunk_params()
         params += self.final_layer.trunk_params()
-        return AdaLNTrunkFn.apply(x0, y, len(self.res_blocks), *params)
+        return AdaLNTrunkFn.apply(x0, y, len(self.res_blocks), getattr(self, "_uva_bucket_hook", None), *params)
 
 
 class DiffusionLossFn(torch.autograd.Function):

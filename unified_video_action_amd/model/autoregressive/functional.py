@@ -207,7 +207,7 @@ class BlockFn(torch.autograd.Function):
     x: [B*N, D] fp32 residual stream."""
 
     @staticmethod
-    def forward(ctx, x, shape, p_attn, p_proj, n1w, n1b, qkvw, qkvb, projw, projb, n2w, n2b, fc1w, fc1b,
+    def forward(ctx, x, shape, p_attn, p_proj, hook, n1w, n1b, qkvw, qkvb, projw, projb, n2w, n2b, fc1w, fc1b,
                 fc2w, fc2b):
         B, N, H = shape
         M, D = x.shape
@@ -248,6 +248,7 @@ class BlockFn(torch.autograd.Function):
         ctx.save_for_backward(x, h1, m1, r1, qkv, o, lse, P, Pd, x1, h2, m2, r2, pre1, a,
                               n1w, n1b, qkvw, qkvb, projw, projb, n2w, n2b, fc1w, fc1b, fc2w, fc2b)
         ctx.cfg = (B, N, H, p_attn, p_proj, seeds, flash)
+        ctx.hook = hook
         return x2
 
     @staticmethod
@@ -305,7 +306,9 @@ class BlockFn(torch.autograd.Function):
         gx = torch.empty(M, D, dtype=F32, device=dev)
         ops.layernorm_bwd(x, n1w.detach(), dh1, m1, r1, gx, accum=False, dw=grad_buf(n1w), db=grad_buf(n1b),
                           dx_base=g1)
-        return (gx,) + (None,) * 15
+        if ctx.hook is not None:
+            ctx.hook()  # every grad of this block is enqueued: launch its DP bucket all-reduce
+        return (gx,) + (None,) * 16
 
 
 def block_forward(blk, x, B, N, p_attn, p_proj):
@@ -313,7 +316,7 @@ def block_forward(blk, x, B, N, p_attn, p_proj):
     D = x.shape[-1]
     a, m = blk.attn, blk.mlp
     y = BlockFn.apply(x.reshape(B * N, D).contiguous(), (B, N, a.num_heads), p_attn, p_proj,
-                      blk.norm1.weight, blk.norm1.bias, a.qkv.weight, a.qkv.bias, a.proj.weight, a.proj.bias,
+                      getattr(blk, "_uva_bucket_hook", None), blk.norm1.weight, blk.norm1.bias, a.qkv.weight, a.qkv.bias, a.proj.weight, a.proj.bias,
                       blk.norm2.weight, blk.norm2.bias, m.fc1.weight, m.fc1.bias, m.fc2.weight, m.fc2.bias)
     return y.reshape(B, N, D)
 
@@ -325,7 +328,7 @@ class AdaLNTrunkFn(torch.autograd.Function):
     final: LN(x)*(1+scale)+shift -> linear.   x0, y: [R, W] fp32 -> out [R, 2C] fp32."""
 
     @staticmethod
-    def forward(ctx, x0, y, depth, *params):
+    def forward(ctx, x0, y, depth, hook, *params):
         R, W = x0.shape
         dev = x0.device
         c = cdt()
@@ -361,6 +364,7 @@ class AdaLNTrunkFn(torch.autograd.Function):
         saved += [x, fmod, hf, meanf, rstdf]
         ctx.save_for_backward(y, sy, *saved, *params)
         ctx.depth = depth
+        ctx.hook = hook
         return out
 
     @staticmethod
@@ -413,7 +417,9 @@ class AdaLNTrunkFn(torch.autograd.Function):
             dx = dxn
         dy = torch.empty(R, W, dtype=F32, device=dev)
         ops.act_bwd(y, dsy, dy, "silu")
-        return (dx, dy, None) + (None,) * len(params)
+        if ctx.hook is not None:
+            ctx.hook()
+        return (dx, dy, None, None) + (None,) * len(params)
 
 
 def _ln_mod_fwd(x, lnw, lnb, mod, W, h, mean, rstd):

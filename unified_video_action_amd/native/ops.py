@@ -26,6 +26,28 @@ def stream():
     return torch.cuda.current_stream().cuda_stream
 
 
+# ---- live kernel tracing (bench.py roofline): HIP events around selected launches ----------
+TRACE = None  # dict tag -> list[(start_event, end_event, flops)] when enabled
+
+
+class _traced:
+    __slots__ = ("tag", "flops", "ev")
+
+    def __init__(self, tag, flops):
+        self.tag, self.flops = tag, flops
+
+    def __enter__(self):
+        if TRACE is not None:
+            self.ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+            self.ev[0].record()
+        return self
+
+    def __exit__(self, *a):
+        if TRACE is not None:
+            self.ev[1].record()
+            TRACE.setdefault(self.tag, []).append((self.ev[0], self.ev[1], self.flops))
+
+
 def _ld(t):
     """leading dimension of a 2-D (row-major, unit inner stride) view."""
     assert t.dim() == 2 and t.stride(1) == 1, (t.shape, t.stride())
@@ -41,12 +63,14 @@ def gemm(A, B, C, M, N, K, lda, ldb, ldc, ta=0, tb=0, batch=1, inner=1, sA=(0, 0
         assert bias.dtype == torch.float32 and bias.is_contiguous()
     if aux is not None:
         assert aux.dtype == C.dtype
-    lib().call("uva_gemm", dt(A), dt(C), ta, tb, ptr(A), ptr(B), ptr(C), M, N, K, lda, ldb, ldc, batch, inner,
-               sA[0], sA[1], sB[0], sB[1], sC[0], sC[1], ptr(bias), ptr(residual), ldr, sR[0], sR[1], ptr(aux),
-               ACT[act] if isinstance(act, str) else act, float(alpha), float(beta), float(drop_p),
-               int(seed) & 0xFFFFFFFFFFFFFFFF, dt(residual) if residual is not None else 0, ptr(gate), ldg,
-               dt(gate) if gate is not None else 0, int(force_generic), ptr(ws),
-               ws.numel() if ws is not None else 0, stream())
+    with _traced(f"gemm[{'NT'[ta]}{'NT'[tb]}] {'bf16' if dt(A) else 'f32'} M{M} N{N} K{K} b{batch}",
+                 2.0 * M * N * K * batch):
+        lib().call("uva_gemm", dt(A), dt(C), ta, tb, ptr(A), ptr(B), ptr(C), M, N, K, lda, ldb, ldc, batch, inner,
+                   sA[0], sA[1], sB[0], sB[1], sC[0], sC[1], ptr(bias), ptr(residual), ldr, sR[0], sR[1], ptr(aux),
+                   ACT[act] if isinstance(act, str) else act, float(alpha), float(beta), float(drop_p),
+                   int(seed) & 0xFFFFFFFFFFFFFFFF, dt(residual) if residual is not None else 0, ptr(gate), ldg,
+                   dt(gate) if gate is not None else 0, int(force_generic), ptr(ws),
+                   ws.numel() if ws is not None else 0, stream())
 
 
 SPLITK_WS_FLOATS = 1 << 25  # 128 MB fp32 partial slabs
@@ -205,12 +229,22 @@ def adamw_ema(p, g, m, v, ema, p_bf16, n_decay, lr, b1, b2, eps, wd, step, grad_
 def attn_fwd(qkv, out, lse2, B, N, H, scale, drop_p=0.0, seed=0):
     assert qkv.dtype == torch.bfloat16 and qkv.is_contiguous() and out.is_contiguous()
     assert N % 64 == 0 and qkv.shape[-1] == 3 * H * 64
+    with _traced(f"attn_fwd B{B} N{N} H{H}", 4.0 * B * H * N * N * 64):
+        _attn_fwd_call(qkv, out, lse2, B, N, H, scale, drop_p, seed)
+
+
+def _attn_fwd_call(qkv, out, lse2, B, N, H, scale, drop_p, seed):
     lib().call("uva_attn_fwd", ptr(qkv), ptr(out), ptr(lse2), B, N, H, float(scale), float(drop_p),
                int(seed) & 0xFFFFFFFFFFFFFFFF, stream())
 
 
 def attn_bwd(qkv, out, dout, lse2, dvec, dqkv, B, N, H, scale, drop_p=0.0, seed=0):
     assert dout.dtype == torch.bfloat16 and dout.is_contiguous() and dqkv.is_contiguous()
+    with _traced(f"attn_bwd B{B} N{N} H{H}", 8.0 * B * H * N * N * 64):
+        _attn_bwd_call(qkv, out, dout, lse2, dvec, dqkv, B, N, H, scale, drop_p, seed)
+
+
+def _attn_bwd_call(qkv, out, dout, lse2, dvec, dqkv, B, N, H, scale, drop_p, seed):
     lib().call("uva_attn_bwd", ptr(qkv), ptr(out), ptr(dout), ptr(lse2), ptr(dvec), ptr(dqkv), B, N, H,
                float(scale), float(drop_p), int(seed) & 0xFFFFFFFFFFFFFFFF, stream())
 
@@ -222,6 +256,14 @@ def conv2d(x, w, out, Nimg, Hin, Win, Ci, Co, ks, stride, pad_t, pad_l, Hout, Wo
     assert w.numel() == Co * ks * ks * Ci and out.numel() == Nimg * Hout * Wout * Co
     if residual is not None:
         assert residual.dtype == out.dtype and residual.numel() == out.numel()
+    with _traced(f"conv{ks}x{ks}/s{stride} {'bf16' if dt(x) else 'f32'} {Hin}x{Win} Ci{Ci} Co{Co} n{Nimg}",
+                 2.0 * Nimg * Hout * Wout * Co * ks * ks * Ci):
+        _conv_call(x, w, out, Nimg, Hin, Win, Ci, Co, ks, stride, pad_t, pad_l, Hout, Wout, bias, residual, gn_scale,
+                   gn_shift, gn_silu, act, force_generic)
+
+
+def _conv_call(x, w, out, Nimg, Hin, Win, Ci, Co, ks, stride, pad_t, pad_l, Hout, Wout, bias, residual, gn_scale,
+               gn_shift, gn_silu, act, force_generic):
     lib().call("uva_conv2d", dt(x), ptr(x), ptr(w), ptr(out), ptr(bias), ptr(residual), Nimg, Hin, Win, Ci, Co, ks,
                stride, pad_t, pad_l, Hout, Wout, ptr(gn_scale), ptr(gn_shift), int(gn_silu), ACT[act],
                int(force_generic), stream())

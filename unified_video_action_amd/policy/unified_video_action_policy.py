@@ -1,0 +1,172 @@
+"""Drop-in policy for `model.policy._target_` (reference:
+policy/unified_video_action_policy.py:33-428).
+
+Same constructor kwargs (vae_model_params, autoregressive_model_params, action_model_params,
+shape_meta, n_action_steps, shift_action, language_emb_model, task_name, task_modes,
+**kwargs incl. normalizer_type, selected_training_mode, use_proprioception, ...) and the
+same training surface: forward(batch) -> (loss, (video_loss, action_loss)),
+compute_loss, get_optimizer(weight_decay, learning_rate, betas), set_normalizer,
+add_weight_decay.  The step runs on libuva_hip.so end to end (frame select+resize,
+VAE encoder, MAR, diffusion heads, backward); inference (`predict_action`) is the §8f
+"next" row and raises.
+
+Differences that do not change results: frames are selected before the bilinear resize
+(per-frame op), and the "loss += 0*p.sum()" DDP workaround (policy:421-423) is replaced
+by the zero-initialised flat gradient buffer that the DP reducer all-reduces whole.
+"""
+import random
+
+import numpy as np
+import torch
+import torch.nn as nn
+
+from ..model.autoregressive import mar_con_unified as mar
+from ..model.common.normalizer import LinearNormalizer
+from ..utils.data_utils import (get_trajectory, image_key, select_frame_indices, umi_proprioception,
+                                vae_images)
+from ..vae.vaekl import AutoencoderKL
+
+ALL_TASK_MODES = ["video_model", "dynamic_model", "policy_model", "inverse_model", "full_dynamic_model"]
+
+
+def _get(cfg, key, default=None):
+    if cfg is None:
+        return default
+    if isinstance(cfg, dict):
+        return cfg.get(key, default)
+    return getattr(cfg, key, default)
+
+
+def _plain(cfg):
+    if isinstance(cfg, dict):
+        return {k: _plain(v) for k, v in cfg.items()}
+    if hasattr(cfg, "items"):
+        return {k: _plain(v) for k, v in cfg.items()}
+    return cfg
+
+
+class UnifiedVideoActionPolicy(nn.Module):
+    def __init__(self, vae_model_params, autoregressive_model_params, action_model_params, shape_meta,
+                 n_action_steps, shift_action=True, language_emb_model=None, task_name=None, task_modes=[],
+                 **kwargs):
+        super().__init__()
+        self.task_name = task_name or ""
+        self.task_modes = list(task_modes or [])
+        self.autoregressive_model_params = autoregressive_model_params
+        self.n_action_steps = n_action_steps
+        self.shift_action = shift_action
+        self.language_emb_model = language_emb_model
+        shape_meta = _plain(shape_meta)
+        self.action_dim = shape_meta["action"]["shape"][0]
+        self.kwargs = kwargs
+        self.normalizer_type = kwargs.get("normalizer_type", "all")
+        self.selected_training_mode = kwargs.get("selected_training_mode")
+        self.use_history_action = kwargs.get("use_history_action") or False
+        self.use_proprioception = kwargs.get("use_proprioception") or False
+        self.different_history_freq = kwargs.get("different_history_freq") or False
+
+        self.vae_model = AutoencoderKL(**_plain(vae_model_params))
+        self.vae_model.eval()
+        for p in self.vae_model.parameters():
+            p.requires_grad = False
+
+        ap = autoregressive_model_params
+        self.model = getattr(mar, _get(ap, "model_size", "mar_base"))(
+            img_size=_get(ap, "img_size", 256), vae_stride=_get(ap, "vae_stride", 16),
+            patch_size=_get(ap, "patch_size", 1), vae_embed_dim=_get(ap, "vae_embed_dim", 16),
+            mask_ratio_min=_get(ap, "mask_ratio_min", 0.7), label_drop_prob=_get(ap, "label_drop_prob", 0.1),
+            attn_dropout=_get(ap, "attn_dropout", 0.1), proj_dropout=_get(ap, "proj_dropout", 0.1),
+            diffloss_d=_get(ap, "diffloss_d", 6), diffloss_w=_get(ap, "diffloss_w", 1024),
+            diffloss_act_d=_get(ap, "diffloss_act_d", 6), diffloss_act_w=_get(ap, "diffloss_act_w", 1024),
+            num_sampling_steps=_get(ap, "num_sampling_steps", "100"),
+            diffusion_batch_mul=_get(ap, "diffusion_batch_mul", 1),
+            grad_checkpointing=_get(ap, "grad_checkpointing", False), predict_video=_get(ap, "predict_video", True),
+            act_diff_training_steps=_get(ap, "act_diff_training_steps", 1000),
+            act_diff_testing_steps=_get(ap, "act_diff_testing_steps", "100"),
+            action_model_params=_plain(action_model_params), use_history_action=self.use_history_action,
+            action_mask_ratio=kwargs.get("action_mask_ratio", 0.5), use_proprioception=self.use_proprioception,
+            predict_wrist_img=kwargs.get("predict_wrist_img") or False,
+            different_history_freq=self.different_history_freq,
+            predict_proprioception=kwargs.get("predict_proprioception") or False, task_name=self.task_name,
+            language_emb_model=language_emb_model, shape_meta=shape_meta)
+        self.normalizer = LinearNormalizer()
+        if self.selected_training_mode is None:
+            if len(self.task_modes) == 0:
+                self.task_modes = list(ALL_TASK_MODES)
+        elif self.selected_training_mode == "policy_model_full_dynamics_model":
+            self.task_modes = ["policy_model", "full_dynamic_model"]
+        else:
+            self.task_modes = [self.selected_training_mode]
+
+    @property
+    def device(self):
+        return next(self.model.parameters()).device
+
+    # ---- training surface ------------------------------------------------------------------
+    def set_normalizer(self, normalizer):
+        self.normalizer.load_state_dict(normalizer.state_dict())
+
+    def add_weight_decay(self, model, weight_decay=1e-5, skip_list=()):
+        decay, no_decay = [], []
+        for name, p in model.named_parameters():
+            if not p.requires_grad:
+                continue
+            (no_decay if (p.ndim == 1 or name.endswith(".bias") or name in skip_list) else decay).append(p)
+        return [{"params": no_decay, "weight_decay": 0.0}, {"params": decay, "weight_decay": weight_decay}]
+
+    def get_optimizer(self, weight_decay, learning_rate, betas):
+        from ..workspace.optim import FusedAdamWEMA
+        return FusedAdamWEMA(self.model, lr=learning_rate, betas=tuple(betas), weight_decay=weight_decay)
+
+    def _normalize(self, key, x):
+        if self.normalizer_type == "all" and key in self.normalizer:
+            return self.normalizer[key].normalize(x)
+        return x
+
+    def compute_loss(self, batch, rng=None):
+        """batch: {"obs": {<image key>: [B,T,3,H,W] in [0,1] (any H), low-dim keys...},
+        "action": [B,T,Da], optional "language_latents": [B,512]}.  `rng` injects the step's
+        random draws (cases.py semantics) for parity runs."""
+        rng = rng or {}
+        obs = batch["obs"]
+        img = obs.get("image", obs.get(image_key(self.task_name)))
+        B, T = img.shape[:2]
+        dev = img.device
+        text_latents = None
+        if self.language_emb_model == "clip":
+            if "language_latents" not in batch:
+                raise NotImplementedError("CLIP text encoding needs network weights; pass language_latents")
+            text_latents = batch["language_latents"]
+        nactions = self._normalize("action", batch["action"].float())
+        indices, prop = None, {}
+        if "umi" in self.task_name:
+            sel = np.arange(T)
+            if "img_indices" in obs:
+                indices = obs["img_indices"].int().squeeze(2)
+            T = T * 4  # 8 loaded frames stand for a 32-step horizon (data_utils.py:215-219)
+            if self.use_proprioception:
+                prop = umi_proprioception(obs, indices, self.different_history_freq)
+        else:
+            sel = select_frame_indices(T, different_history_freq=self.different_history_freq,
+                                       rng_choice=rng.get("history_combination"))
+        x = vae_images(img, sel, self.vae_model.CIN_PAD)
+        n_half = B * (len(sel) // 2)
+        eps = rng.get("vae_eps_x")
+        if eps is not None:
+            eps = torch.cat([torch.as_tensor(rng["vae_eps_x"]), torch.as_tensor(rng["vae_eps_c"])]).to(dev)
+        else:
+            eps = torch.randn(2 * n_half, self.vae_model.embed_dim, 16, 16, device=dev)
+        tokens = self.vae_model.encode_tokens(x, eps)
+        z = tokens[:n_half].reshape(B, -1, 256, tokens.shape[-1])
+        c = tokens[n_half:].reshape(B, -1, 256, tokens.shape[-1])
+        _, trajectory = get_trajectory(nactions, T, self.shift_action, self.use_history_action)
+        mode = rng.get("task_mode") or random.choice(self.task_modes)
+        loss, video_loss, act_loss = self.model(z, c, None, trajectory, text_latents, task_mode=mode,
+                                                proprioception_input=prop, rng=rng)
+        return loss, (video_loss, act_loss)
+
+    def forward(self, batch, **kwargs):
+        return self.compute_loss(batch, **kwargs)
+
+    def predict_action(self, obs_dict, language_goal=None):
+        raise NotImplementedError("inference sampler (MAR.sample_tokens + DiffActLoss.sample) is SURVEY §8f next")

@@ -1,0 +1,212 @@
+"""Frozen KL-VAE encoder on the HIP path (reference: unified_video_action/vae/vaekl.py).
+
+Parameters keep the reference module tree (encoder.conv_in, encoder.down.{i}.block.{j}.
+{norm1,conv1,norm2,conv2,nin_shortcut}, encoder.down.{i}.attn.{j}.{norm,q,k,v,proj_out},
+encoder.down.{i}.downsample.conv, encoder.mid.*, encoder.norm_out, encoder.conv_out,
+quant_conv) so reference checkpoints (kl16.ckpt "model" dict) load unchanged.  The decoder
+is used only by the epoch-end FVD eval and is out of scope.
+
+Forward runs entirely in NHWC on libuva_hip.so:
+  * every conv = implicit-GEMM MFMA kernel, the preceding GroupNorm+SiLU folded into its
+    A-loader (per-(image, channel) scale/shift from uva_groupnorm_stats), residual adds in
+    its epilogue;
+  * AttnBlock = fused qkv 1x1 conv (GN prologue, no SiLU) -> batched QK^T GEMM -> row
+    softmax -> PV GEMM -> proj_out 1x1 conv + residual;
+  * quant_conv 1x1, then the posterior sample kernel writes MAR tokens directly.
+"""
+import os
+
+import torch
+import torch.nn as nn
+
+from ..native import ops
+from ..runtime import cdt
+
+F32 = torch.float32
+
+
+def _gn(c):
+    return nn.GroupNorm(32, c, eps=1e-6, affine=True)
+
+
+class ResnetBlock(nn.Module):
+    def __init__(self, in_channels, out_channels):
+        super().__init__()
+        self.in_channels, self.out_channels = in_channels, out_channels
+        self.norm1 = _gn(in_channels)
+        self.conv1 = nn.Conv2d(in_channels, out_channels, 3, 1, 1)
+        self.norm2 = _gn(out_channels)
+        self.conv2 = nn.Conv2d(out_channels, out_channels, 3, 1, 1)
+        if in_channels != out_channels:
+            self.nin_shortcut = nn.Conv2d(in_channels, out_channels, 1)
+
+
+class AttnBlock(nn.Module):
+    def __init__(self, c):
+        super().__init__()
+        self.norm = _gn(c)
+        self.q = nn.Conv2d(c, c, 1)
+        self.k = nn.Conv2d(c, c, 1)
+        self.v = nn.Conv2d(c, c, 1)
+        self.proj_out = nn.Conv2d(c, c, 1)
+
+
+class Downsample(nn.Module):
+    def __init__(self, c):
+        super().__init__()
+        self.conv = nn.Conv2d(c, c, 3, 2, 0)
+
+
+class Encoder(nn.Module):
+    def __init__(self, ch=128, ch_mult=(1, 1, 2, 2, 4), num_res_blocks=2, attn_resolutions=(16,), in_channels=3,
+                 resolution=256, z_channels=16, double_z=True, **ignore):
+        super().__init__()
+        self.ch = ch
+        self.num_resolutions = len(ch_mult)
+        self.num_res_blocks = num_res_blocks
+        self.conv_in = nn.Conv2d(in_channels, ch, 3, 1, 1)
+        in_mult = (1,) + tuple(ch_mult)
+        res = resolution
+        self.down = nn.ModuleList()
+        for lvl in range(self.num_resolutions):
+            d = nn.Module()
+            d.block, d.attn = nn.ModuleList(), nn.ModuleList()
+            cin = ch * in_mult[lvl]
+            for _ in range(num_res_blocks):
+                d.block.append(ResnetBlock(cin, ch * ch_mult[lvl]))
+                cin = ch * ch_mult[lvl]
+                if res in attn_resolutions:
+                    d.attn.append(AttnBlock(cin))
+            if lvl != self.num_resolutions - 1:
+                d.downsample = Downsample(cin)
+                res //= 2
+            self.down.append(d)
+        self.mid = nn.Module()
+        self.mid.block_1 = ResnetBlock(cin, cin)
+        self.mid.attn_1 = AttnBlock(cin)
+        self.mid.block_2 = ResnetBlock(cin, cin)
+        self.norm_out = _gn(cin)
+        self.conv_out = nn.Conv2d(cin, 2 * z_channels if double_z else z_channels, 3, 1, 1)
+
+
+class _Prepared:
+    """compute-dtype NHWC copies of the frozen weights ([Co][kh][kw][Ci])."""
+
+    def __init__(self, vae, dtype, device, cin_pad):
+        self.w, self.b = {}, {}
+        for name, m in vae.named_modules():
+            if isinstance(m, nn.Conv2d):
+                w = m.weight.detach().to(device)
+                if name.endswith("conv_in") and w.shape[1] < cin_pad:
+                    w = torch.nn.functional.pad(w, (0, 0, 0, 0, 0, cin_pad - w.shape[1]))
+                self.w[name] = w.permute(0, 2, 3, 1).contiguous().to(dtype)
+                self.b[name] = m.bias.detach().to(device, F32).contiguous()
+        for name, m in vae.named_modules():
+            if isinstance(m, AttnBlock):
+                self.w[name + ".qkv"] = torch.cat([self.w[name + ".q"], self.w[name + ".k"], self.w[name + ".v"]])
+                self.b[name + ".qkv"] = torch.cat([self.b[name + ".q"], self.b[name + ".k"], self.b[name + ".v"]])
+
+
+class AutoencoderKL(nn.Module):
+    CIN_PAD = 8  # RGB padded to 8 channels so every conv has 16-B channel chunks
+
+    def __init__(self, autoencoder_path=None, ddconfig=None, use_variational=True, output_dir=None, **kwargs):
+        super().__init__()
+        get = (lambda k, d: getattr(ddconfig, k, d) if not isinstance(ddconfig, dict) else ddconfig.get(k, d))
+        embed_dim = get("vae_embed_dim", 16)
+        ch_mult = tuple(get("ch_mult", (1, 1, 2, 2, 4)))
+        self.encoder = Encoder(ch_mult=ch_mult, z_channels=embed_dim)
+        self.use_variational = use_variational
+        self.quant_conv = nn.Conv2d(2 * embed_dim, (2 if use_variational else 1) * embed_dim, 1)
+        self.embed_dim = embed_dim
+        self._prep = None
+        if autoencoder_path is not None and os.path.exists(autoencoder_path):
+            self.init_from_ckpt(autoencoder_path)
+
+    def init_from_ckpt(self, path):
+        sd = torch.load(path, map_location="cpu", weights_only=True)
+        sd = sd.get("model", sd)
+        self.load_state_dict(sd, strict=False)
+        self._prep = None
+
+    def _prepared(self, device):
+        key = (cdt(), str(device))
+        if self._prep is None or self._prep[0] != key:
+            self._prep = (key, _Prepared(self, cdt(), device, self.CIN_PAD))
+        return self._prep[1]
+
+    # ---- HIP forward pieces --------------------------------------------------------------
+    def _gn(self, x, norm, n, hw, c):
+        sc = torch.empty(n, c, dtype=F32, device=x.device)
+        sh = torch.empty(n, c, dtype=F32, device=x.device)
+        ops.groupnorm_stats(x, n, hw, c, norm.weight.detach(), norm.bias.detach(), sc, sh, eps=norm.eps)
+        return sc, sh
+
+    def _conv(self, P, name, x, n, H, W, stride=1, gn=None, gn_silu=True, residual=None):
+        w = P.w[name]
+        Co, ks, Ci = w.shape[0], w.shape[1], w.shape[3]
+        if ks == 3 and stride == 1:
+            pad, Ho, Wo = 1, H, W
+        elif ks == 3:
+            pad, Ho, Wo = 0, H // 2, W // 2  # F.pad(0,1,0,1) then stride-2 conv (vaekl.py:47-50)
+        else:
+            pad, Ho, Wo = 0, H, W
+        out = torch.empty(n, Ho, Wo, Co, dtype=x.dtype, device=x.device)
+        ops.conv2d(x, w, out, n, H, W, Ci, Co, ks, stride, pad, pad, Ho, Wo, bias=P.b[name], residual=residual,
+                   gn_scale=None if gn is None else gn[0], gn_shift=None if gn is None else gn[1], gn_silu=gn_silu)
+        return out, Ho, Wo
+
+    def _resblock(self, P, name, blk, x, n, H, W):
+        c_in, c_out = blk.in_channels, blk.out_channels
+        g1 = self._gn(x, blk.norm1, n, H * W, c_in)
+        h, _, _ = self._conv(P, name + ".conv1", x, n, H, W, gn=g1)
+        g2 = self._gn(h, blk.norm2, n, H * W, c_out)
+        xs = self._conv(P, name + ".nin_shortcut", x, n, H, W)[0] if c_in != c_out else x
+        return self._conv(P, name + ".conv2", h, n, H, W, gn=g2, residual=xs)[0]
+
+    def _attn(self, P, name, blk, x, n, H, W):
+        C = x.shape[-1]
+        L = H * W
+        g = self._gn(x, blk.norm, n, L, C)
+        qkv, _, _ = self._conv(P, name + ".qkv", x, n, H, W, gn=g, gn_silu=False)  # [n, H, W, 3C]
+        q = qkv.reshape(n * L, 3 * C)
+        S = torch.empty(n, L, L, dtype=x.dtype, device=x.device)
+        ops.gemm(q, q[:, C:], S, L, L, C, 3 * C, 3 * C, L, 0, 0, batch=n, sA=(L * 3 * C, 0), sB=(L * 3 * C, 0),
+                 sC=(L * L, 0))
+        Pm = torch.empty_like(S)
+        ops.softmax_fwd(S, Pm, None, L, float(C) ** -0.5)
+        O = torch.empty(n * L, C, dtype=x.dtype, device=x.device)
+        ops.gemm(Pm, q[:, 2 * C:], O, L, C, L, L, 3 * C, C, 0, 1, batch=n, sA=(L * L, 0), sB=(L * 3 * C, 0),
+                 sC=(L * C, 0))
+        return self._conv(P, name + ".proj_out", O.reshape(n, H, W, C), n, H, W, residual=x)[0]
+
+    @torch.no_grad()
+    def moments_nhwc(self, x):
+        """x: NHWC [n, 256, 256, CIN_PAD] in the compute dtype -> moments NHWC [n, 16, 16, 2*embed]."""
+        P = self._prepared(x.device)
+        e = self.encoder
+        n, H, W, _ = x.shape
+        h, H, W = self._conv(P, "encoder.conv_in", x, n, H, W)
+        for lvl, d in enumerate(e.down):
+            for j, blk in enumerate(d.block):
+                h = self._resblock(P, f"encoder.down.{lvl}.block.{j}", blk, h, n, H, W)
+                if len(d.attn):
+                    h = self._attn(P, f"encoder.down.{lvl}.attn.{j}", d.attn[j], h, n, H, W)
+            if hasattr(d, "downsample"):
+                h, H, W = self._conv(P, f"encoder.down.{lvl}.downsample.conv", h, n, H, W, stride=2)
+        h = self._resblock(P, "encoder.mid.block_1", e.mid.block_1, h, n, H, W)
+        h = self._attn(P, "encoder.mid.attn_1", e.mid.attn_1, h, n, H, W)
+        h = self._resblock(P, "encoder.mid.block_2", e.mid.block_2, h, n, H, W)
+        g = self._gn(h, e.norm_out, n, H * W, h.shape[-1])
+        h, H, W = self._conv(P, "encoder.conv_out", h, n, H, W, gn=g)
+        return self._conv(P, "quant_conv", h, n, H, W)[0]
+
+    @torch.no_grad()
+    def encode_tokens(self, x, eps, scale=0.2325):
+        """NHWC images -> latent tokens [n, 256, embed] fp32 = (mean + std*eps)*scale
+        (DiagonalGaussianDistribution.sample + data_utils.py:396).  eps: NCHW [n, embed, 16, 16]."""
+        mom = self.moments_nhwc(x)
+        n = x.shape[0]
+        z = torch.empty(n, 256, self.embed_dim, dtype=F32, device=x.device)
+        ops.posterior_sample(mom, eps.contiguous().float(), z, n, scale)
+        return z
