@@ -1,0 +1,14 @@
+#!/bin/bash
+# GPU-box profiling recipe (run via gpurun from the repo root).
+set -o pipefail
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+export TMPDIR=/tmp
+OUT=$R/gpurun_out/prof
+mkdir -p $OUT
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/ktrace -o run -- \
+    python3 $R/bench.py --steps 3 --warmup 1 --no-cpu-baseline > $OUT/bench_ktrace.json 2> $OUT/bench_ktrace.err || exit $?
+timeout -k 10 400 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/pmc_fetch -o run -- \
+    python3 $R/bench.py --steps 1 --warmup 1 --no-cpu-baseline --no-trace > $OUT/bench_pmc1.json 2> $OUT/bench_pmc1.err || exit $?
+timeout -k 10 400 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/pmc_write -o run -- \
+    python3 $R/bench.py --steps 1 --warmup 1 --no-cpu-baseline --no-trace > $OUT/bench_pmc2.json 2> $OUT/bench_pmc2.err || exit $?
+echo profile-done
