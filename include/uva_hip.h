@@ -60,8 +60,11 @@ int uva_gemm(int in_dtype, int out_dtype, int ta, int tb, const void* A, const v
  * (vae/vaekl.py:36-113,116-159,162-273,469) and DiffActLoss.conv (diffusion_action_loss.py:42-46). */
 int uva_conv2d(int dtype, const void* in, const void* w, void* out, const float* bias, const void* residual, int Nimg,
                int Hin, int Win, int Ci, int Co, int ks, int stride, int pad_t, int pad_l, int Hout, int Wout,
-               const float* gn_scale, const float* gn_shift, int gn_silu, int act, int force_generic,
-               hipStream_t stream);
+               const float* gn_scale, const float* gn_shift, int gn_silu, int act, float* gn_part,
+               int force_generic, hipStream_t stream);
+/* gn_part (bf16 MFMA path): the epilogue also writes per-(128-row tile, group) (sum, sumsq) of
+ * the stored output for the NEXT GroupNorm(32) -> uva_groupnorm_finalize_tiles.  Needs
+ * (Hout*Wout) % 128 == 0, Co % 32 == 0; buffer [M/128][32][2] floats. */
 
 /* ---- LayerNorm (affine or adaLN-modulated) --------------------------------------------
  * Replaces nn.LayerNorm(eps=1e-6) (mar_con_unified.py:198,215,252; timm norm1/norm2)
@@ -144,6 +147,11 @@ int uva_resize_select(const float* img, int B, int T, int Hin, int Win, const in
 long long uva_groupnorm_workspace(int Nimg, int HW);
 int uva_groupnorm_stats(int dtype, const void* x, int Nimg, int HW, int C, const float* gamma, const float* beta,
                         float eps, float* scale, float* shift, float* workspace, hipStream_t stream);
+int uva_groupnorm_finalize_tiles(const float* part, int Nimg, int HW, int C, int tile_rows, const float* gamma,
+                                 const float* beta, float eps, float* scale, float* shift, hipStream_t stream);
+/* y = [SiLU](x*scale + shift) over NHWC bf16 (GroupNorm apply, once per element) */
+int uva_groupnorm_apply(const void* x, const float* scale, const float* shift, void* y, int Nimg, int HW, int C,
+                        int do_silu, hipStream_t stream);
 int uva_posterior_sample(int mdt, const void* moments, const float* eps, float* z, int Nimg, float scale,
                          hipStream_t stream);
 

@@ -59,5 +59,20 @@ def main():
     print(f"layernorm fwd f32->bf16 [{M},768]: {t*1e3:.1f} us, {M*768*6/t/1e6:.0f} GB/s")
 
 
-if __name__ == "__main__":
+if __name__ == "__main__" and len(sys.argv) == 1:
     main()
+
+
+def conv_bench():
+    dev = "cuda"
+    for (n, H, Ci, Co) in ((256, 256, 128, 128), (256, 128, 128, 128), (256, 64, 256, 256), (256, 16, 512, 512)):
+        x = torch.randn(n, H, H, Ci, device=dev).to(torch.bfloat16)
+        w = (torch.randn(Co, 3, 3, Ci, device=dev) * 0.05).to(torch.bfloat16)
+        out = torch.empty(n, H, H, Co, device=dev, dtype=torch.bfloat16)
+        fl = 2 * n * H * H * Co * 9 * Ci
+        t = timeit(lambda: ops.conv2d(x, w, out, n, H, H, Ci, Co, 3, 1, 1, 1, H, H), iters=5)
+        print(f"conv3x3 n{n} {H}x{H} Ci{Ci} Co{Co}: {t:.2f} ms {fl/t/1e9:.0f} TF")
+
+
+if __name__ == "__main__" and len(sys.argv) > 1 and sys.argv[1] == "conv":
+    conv_bench()

@@ -127,6 +127,52 @@ __global__ void posterior_kernel(const void* __restrict__ mom, int mdt, const fl
   }
 }
 
+// finalize fused (conv-epilogue) GroupNorm partials: part[tile][32][2], tiles_per_img tiles per image
+__global__ void gn_finalize_tiles_kernel(const float* __restrict__ part, int tiles_per_img, long long cnt_per_group,
+                                         int C, const float* __restrict__ gamma, const float* __restrict__ beta,
+                                         float eps, float* __restrict__ scale, float* __restrict__ shift, int Nimg) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (long long)Nimg * C) return;
+  const int n = i / C, c = i % C, gs = C / 32, g = c / gs;
+  double s = 0.0, q = 0.0;
+  const float* p = part + ((long long)n * tiles_per_img * 32 + g) * 2;
+  for (int t = 0; t < tiles_per_img; ++t) {
+    s += p[(long long)t * 64];
+    q += p[(long long)t * 64 + 1];
+  }
+  const double mean = s / cnt_per_group;
+  double var = q / cnt_per_group - mean * mean;
+  if (var < 0) var = 0;
+  const float rstd = (float)(1.0 / sqrt(var + (double)eps));
+  const float sc = gamma[c] * rstd;
+  scale[i] = sc;
+  shift[i] = beta[c] - (float)mean * sc;
+}
+
+// y = act(x * scale[n][c] + shift[n][c]), NHWC bf16, 8 channels per thread
+__global__ void gn_apply_kernel(const bf16* __restrict__ x, const float* __restrict__ scale,
+                                const float* __restrict__ shift, bf16* __restrict__ y, long long n8, int HW, int C,
+                                int do_silu) {
+  const int c8 = C / 8;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n8; i += (long long)gridDim.x * blockDim.x) {
+    const int c = (int)(i % c8) * 8;
+    const long long n = (i / c8) / HW;
+    const float* sc = scale + n * C + c;
+    const float* sh = shift + n * C + c;
+    float4 s0 = *(const float4*)sc, s1 = *(const float4*)(sc + 4);
+    float4 h0 = *(const float4*)sh, h1 = *(const float4*)(sh + 4);
+    float ss[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
+    float hh[8] = {h0.x, h0.y, h0.z, h0.w, h1.x, h1.y, h1.z, h1.w};
+    bf16x8 v = ((const bf16x8*)x)[i];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      float u = (float)v[j] * ss[j] + hh[j];
+      v[j] = (bf16)(do_silu ? silu(u) : u);
+    }
+    ((bf16x8*)y)[i] = v;
+  }
+}
+
 static inline dim3 gridn(long long n) {
   long long b = (n + 255) / 256;
   if (b > 16384) b = 16384;
@@ -164,6 +210,25 @@ extern "C" int uva_groupnorm_stats(int dtype, const void* x, int Nimg, int HW, i
 extern "C" int uva_posterior_sample(int mdt, const void* moments, const float* eps, float* z, int Nimg, float scale,
                                     hipStream_t s) {
   posterior_kernel<<<gridn((long long)Nimg * 4096), 256, 0, s>>>(moments, mdt, eps, z, Nimg, scale);
+  UVA_LAUNCH_CHECK();
+  return 0;
+}
+
+extern "C" int uva_groupnorm_finalize_tiles(const float* part, int Nimg, int HW, int C, int tile_rows,
+                                            const float* gamma, const float* beta, float eps, float* scale,
+                                            float* shift, hipStream_t s) {
+  if (HW % tile_rows != 0 || C % 32 != 0) return (int)hipErrorInvalidValue;
+  gn_finalize_tiles_kernel<<<gridn((long long)Nimg * C), 256, 0, s>>>(part, HW / tile_rows, (long long)HW * (C / 32), C,
+                                                                       gamma, beta, eps, scale, shift, Nimg);
+  UVA_LAUNCH_CHECK();
+  return 0;
+}
+
+extern "C" int uva_groupnorm_apply(const void* x, const float* scale, const float* shift, void* y, int Nimg, int HW,
+                                   int C, int do_silu, hipStream_t s) {
+  if (C % 8 != 0) return (int)hipErrorInvalidValue;
+  long long n8 = (long long)Nimg * HW * C / 8;
+  gn_apply_kernel<<<gridn(n8), 256, 0, s>>>((const bf16*)x, scale, shift, (bf16*)y, n8, HW, C, do_silu);
   UVA_LAUNCH_CHECK();
   return 0;
 }

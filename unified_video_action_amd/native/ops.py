@@ -250,7 +250,7 @@ def _attn_bwd_call(qkv, out, dout, lse2, dvec, dqkv, B, N, H, scale, drop_p, see
 
 
 def conv2d(x, w, out, Nimg, Hin, Win, Ci, Co, ks, stride, pad_t, pad_l, Hout, Wout, bias=None, residual=None,
-           gn_scale=None, gn_shift=None, gn_silu=True, act="none", force_generic=False):
+           gn_scale=None, gn_shift=None, gn_silu=True, act="none", force_generic=False, gn_part=None):
     """NHWC implicit-GEMM conv; w stored [Co][ks][ks][Ci]."""
     assert x.dtype == w.dtype == out.dtype
     assert w.numel() == Co * ks * ks * Ci and out.numel() == Nimg * Hout * Wout * Co
@@ -259,14 +259,23 @@ def conv2d(x, w, out, Nimg, Hin, Win, Ci, Co, ks, stride, pad_t, pad_l, Hout, Wo
     with _traced(f"conv{ks}x{ks}/s{stride} {'bf16' if dt(x) else 'f32'} {Hin}x{Win} Ci{Ci} Co{Co} n{Nimg}",
                  2.0 * Nimg * Hout * Wout * Co * ks * ks * Ci):
         _conv_call(x, w, out, Nimg, Hin, Win, Ci, Co, ks, stride, pad_t, pad_l, Hout, Wout, bias, residual, gn_scale,
-                   gn_shift, gn_silu, act, force_generic)
+                   gn_shift, gn_silu, act, force_generic, gn_part)
 
 
 def _conv_call(x, w, out, Nimg, Hin, Win, Ci, Co, ks, stride, pad_t, pad_l, Hout, Wout, bias, residual, gn_scale,
-               gn_shift, gn_silu, act, force_generic):
+               gn_shift, gn_silu, act, force_generic, gn_part):
     lib().call("uva_conv2d", dt(x), ptr(x), ptr(w), ptr(out), ptr(bias), ptr(residual), Nimg, Hin, Win, Ci, Co, ks,
-               stride, pad_t, pad_l, Hout, Wout, ptr(gn_scale), ptr(gn_shift), int(gn_silu), ACT[act],
+               stride, pad_t, pad_l, Hout, Wout, ptr(gn_scale), ptr(gn_shift), int(gn_silu), ACT[act], ptr(gn_part),
                int(force_generic), stream())
+
+
+def groupnorm_finalize_tiles(part, Nimg, HW, C, gamma, beta, scale, shift, eps=1e-6, tile_rows=128):
+    lib().call("uva_groupnorm_finalize_tiles", ptr(part), Nimg, HW, C, tile_rows, ptr(gamma), ptr(beta), float(eps),
+               ptr(scale), ptr(shift), stream())
+
+
+def groupnorm_apply(x, scale, shift, y, Nimg, HW, C, silu=True):
+    lib().call("uva_groupnorm_apply", ptr(x), ptr(scale), ptr(shift), ptr(y), Nimg, HW, C, int(silu), stream())
 
 
 def groupnorm_stats(x, Nimg, HW, C, gamma, beta, scale, shift, eps=1e-6):

@@ -7,9 +7,11 @@ quant_conv) so reference checkpoints (kl16.ckpt "model" dict) load unchanged.  T
 is used only by the epoch-end FVD eval and is out of scope.
 
 Forward runs entirely in NHWC on libuva_hip.so:
-  * every conv = implicit-GEMM MFMA kernel, the preceding GroupNorm+SiLU folded into its
-    A-loader (per-(image, channel) scale/shift from uva_groupnorm_stats), residual adds in
-    its epilogue;
+  * every conv = implicit-GEMM MFMA kernel with the residual add in its epilogue; the
+    epilogue also emits deterministic per-tile GroupNorm partial sums of its output, so the
+    next GroupNorm needs no statistics pass: finalize (tiny) + one vectorised GN-apply+SiLU
+    pass (once per element, not once per 3x3 tap); fp32 parity path: separate stats pass and
+    GN+SiLU in the conv A-loader;
   * AttnBlock = fused qkv 1x1 conv (GN prologue, no SiLU) -> batched QK^T GEMM -> row
     softmax -> PV GEMM -> proj_out 1x1 conv + residual;
   * quant_conv 1x1, then the posterior sample kernel writes MAR tokens directly.
@@ -136,13 +138,32 @@ class AutoencoderKL(nn.Module):
         return self._prep[1]
 
     # ---- HIP forward pieces --------------------------------------------------------------
-    def _gn(self, x, norm, n, hw, c):
+    # A GroupNorm'd tensor travels as (tensor, stats) where stats are the fused per-tile partial
+    # sums written by the producing conv's epilogue (bf16 MFMA path) or None (computed by a
+    # separate pass: fp32 parity path).
+    def _fused(self):
+        return cdt() == torch.bfloat16
+
+    def _gn(self, x, stats, norm, n, hw, c):
         sc = torch.empty(n, c, dtype=F32, device=x.device)
         sh = torch.empty(n, c, dtype=F32, device=x.device)
-        ops.groupnorm_stats(x, n, hw, c, norm.weight.detach(), norm.bias.detach(), sc, sh, eps=norm.eps)
+        if stats is not None:
+            ops.groupnorm_finalize_tiles(stats, n, hw, c, norm.weight.detach(), norm.bias.detach(), sc, sh,
+                                         eps=norm.eps)
+        else:
+            ops.groupnorm_stats(x, n, hw, c, norm.weight.detach(), norm.bias.detach(), sc, sh, eps=norm.eps)
         return sc, sh
 
-    def _conv(self, P, name, x, n, H, W, stride=1, gn=None, gn_silu=True, residual=None):
+    def _norm_act(self, x, stats, norm, n, hw, c, silu=True):
+        """GN(+SiLU) applied ONCE per element (fused path) -> (input for the next conv, prologue or None)."""
+        g = self._gn(x, stats, norm, n, hw, c)
+        if not self._fused():
+            return x, g  # fp32 path: apply inside the conv A-loader
+        y = torch.empty_like(x)
+        ops.groupnorm_apply(x, g[0], g[1], y, n, hw, c, silu)
+        return y, None
+
+    def _conv(self, P, name, x, n, H, W, stride=1, gn=None, gn_silu=True, residual=None, stats=False):
         w = P.w[name]
         Co, ks, Ci = w.shape[0], w.shape[1], w.shape[3]
         if ks == 3 and stride == 1:
@@ -152,23 +173,28 @@ class AutoencoderKL(nn.Module):
         else:
             pad, Ho, Wo = 0, H, W
         out = torch.empty(n, Ho, Wo, Co, dtype=x.dtype, device=x.device)
+        part = None
+        if stats and self._fused() and (Ho * Wo) % 128 == 0 and Co % 32 == 0:
+            part = torch.empty(n * Ho * Wo // 128, 32, 2, dtype=F32, device=x.device)
         ops.conv2d(x, w, out, n, H, W, Ci, Co, ks, stride, pad, pad, Ho, Wo, bias=P.b[name], residual=residual,
-                   gn_scale=None if gn is None else gn[0], gn_shift=None if gn is None else gn[1], gn_silu=gn_silu)
-        return out, Ho, Wo
+                   gn_scale=None if gn is None else gn[0], gn_shift=None if gn is None else gn[1], gn_silu=gn_silu,
+                   gn_part=part)
+        return out, Ho, Wo, part
 
-    def _resblock(self, P, name, blk, x, n, H, W):
+    def _resblock(self, P, name, blk, x, xs_stats, n, H, W):
         c_in, c_out = blk.in_channels, blk.out_channels
-        g1 = self._gn(x, blk.norm1, n, H * W, c_in)
-        h, _, _ = self._conv(P, name + ".conv1", x, n, H, W, gn=g1)
-        g2 = self._gn(h, blk.norm2, n, H * W, c_out)
+        a, g1 = self._norm_act(x, xs_stats, blk.norm1, n, H * W, c_in)
+        h, _, _, hs = self._conv(P, name + ".conv1", a, n, H, W, gn=g1, stats=True)
+        a2, g2 = self._norm_act(h, hs, blk.norm2, n, H * W, c_out)
         xs = self._conv(P, name + ".nin_shortcut", x, n, H, W)[0] if c_in != c_out else x
-        return self._conv(P, name + ".conv2", h, n, H, W, gn=g2, residual=xs)[0]
+        out, _, _, os_ = self._conv(P, name + ".conv2", a2, n, H, W, gn=g2, residual=xs, stats=True)
+        return out, os_
 
-    def _attn(self, P, name, blk, x, n, H, W):
+    def _attn(self, P, name, blk, x, xs_stats, n, H, W):
         C = x.shape[-1]
         L = H * W
-        g = self._gn(x, blk.norm, n, L, C)
-        qkv, _, _ = self._conv(P, name + ".qkv", x, n, H, W, gn=g, gn_silu=False)  # [n, H, W, 3C]
+        g = self._gn(x, xs_stats, blk.norm, n, L, C)
+        qkv = self._conv(P, name + ".qkv", x, n, H, W, gn=g, gn_silu=False)[0]  # [n, H, W, 3C]; 1x1: prologue once
         q = qkv.reshape(n * L, 3 * C)
         S = torch.empty(n, L, L, dtype=x.dtype, device=x.device)
         ops.gemm(q, q[:, C:], S, L, L, C, 3 * C, 3 * C, L, 0, 0, batch=n, sA=(L * 3 * C, 0), sB=(L * 3 * C, 0),
@@ -178,7 +204,8 @@ class AutoencoderKL(nn.Module):
         O = torch.empty(n * L, C, dtype=x.dtype, device=x.device)
         ops.gemm(Pm, q[:, 2 * C:], O, L, C, L, L, 3 * C, C, 0, 1, batch=n, sA=(L * L, 0), sB=(L * 3 * C, 0),
                  sC=(L * C, 0))
-        return self._conv(P, name + ".proj_out", O.reshape(n, H, W, C), n, H, W, residual=x)[0]
+        out, _, _, os_ = self._conv(P, name + ".proj_out", O.reshape(n, H, W, C), n, H, W, residual=x, stats=True)
+        return out, os_
 
     @torch.no_grad()
     def moments_nhwc(self, x):
@@ -186,19 +213,19 @@ class AutoencoderKL(nn.Module):
         P = self._prepared(x.device)
         e = self.encoder
         n, H, W, _ = x.shape
-        h, H, W = self._conv(P, "encoder.conv_in", x, n, H, W)
+        h, H, W, hs = self._conv(P, "encoder.conv_in", x, n, H, W, stats=True)
         for lvl, d in enumerate(e.down):
             for j, blk in enumerate(d.block):
-                h = self._resblock(P, f"encoder.down.{lvl}.block.{j}", blk, h, n, H, W)
+                h, hs = self._resblock(P, f"encoder.down.{lvl}.block.{j}", blk, h, hs, n, H, W)
                 if len(d.attn):
-                    h = self._attn(P, f"encoder.down.{lvl}.attn.{j}", d.attn[j], h, n, H, W)
+                    h, hs = self._attn(P, f"encoder.down.{lvl}.attn.{j}", d.attn[j], h, hs, n, H, W)
             if hasattr(d, "downsample"):
-                h, H, W = self._conv(P, f"encoder.down.{lvl}.downsample.conv", h, n, H, W, stride=2)
-        h = self._resblock(P, "encoder.mid.block_1", e.mid.block_1, h, n, H, W)
-        h = self._attn(P, "encoder.mid.attn_1", e.mid.attn_1, h, n, H, W)
-        h = self._resblock(P, "encoder.mid.block_2", e.mid.block_2, h, n, H, W)
-        g = self._gn(h, e.norm_out, n, H * W, h.shape[-1])
-        h, H, W = self._conv(P, "encoder.conv_out", h, n, H, W, gn=g)
+                h, H, W, hs = self._conv(P, f"encoder.down.{lvl}.downsample.conv", h, n, H, W, stride=2, stats=True)
+        h, hs = self._resblock(P, "encoder.mid.block_1", e.mid.block_1, h, hs, n, H, W)
+        h, hs = self._attn(P, "encoder.mid.attn_1", e.mid.attn_1, h, hs, n, H, W)
+        h, hs = self._resblock(P, "encoder.mid.block_2", e.mid.block_2, h, hs, n, H, W)
+        a, g = self._norm_act(h, hs, e.norm_out, n, H * W, h.shape[-1])
+        h, H, W, _ = self._conv(P, "encoder.conv_out", a, n, H, W, gn=g)
         return self._conv(P, "quant_conv", h, n, H, W)[0]
 
     @torch.no_grad()
