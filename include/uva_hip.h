@@ -58,6 +58,14 @@ int uva_gemm(int in_dtype, int out_dtype, int ta, int tb, const void* A, const v
  * output before the residual add.  Ci % 8 == 0 for the MFMA path.
  * Replaces nn.Conv2d (+ the preceding Normalize/nonlinearity) of the KL-VAE encoder
  * (vae/vaekl.py:36-113,116-159,162-273,469) and DiffActLoss.conv (diffusion_action_loss.py:42-46). */
+/* Which kernel a bf16 GEMM of this shape runs on (test / tuning introspection; no device work):
+ * kernel | BN << 4 | splits << 16; kernel 0 = VALU, 1 = MFMA register-staged 128x128,
+ * 2 = MFMA LDS-DMA 128x128, 3 = MFMA 8-phase 256-row (BN 128/256), splits = split-K slices. */
+/* Diagnostic: per-wave s_memtime segment sums of the last stamped 8-phase GEMM (UVA_8PH_VAR odd):
+ * [16 blocks][8 waves][read+issue, barrier-1, mfma issue, barrier-2, loop total]. */
+int uva_debug_gemm8_stamps(unsigned long long* host);
+long long uva_gemm_plan(int in_dtype, int ta, int tb, int M, int N, int K, int batch, int gn_prologue,
+                        long long ws_floats);
 int uva_conv2d(int dtype, const void* in, const void* w, void* out, const float* bias, const void* residual, int Nimg,
                int Hin, int Win, int Ci, int Co, int ks, int stride, int pad_t, int pad_l, int Hout, int Wout,
                const float* gn_scale, const float* gn_shift, int gn_silu, int act, float* gn_part,

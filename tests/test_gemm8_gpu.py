@@ -1,0 +1,134 @@
+"""8-phase 256-row MFMA GEMM (csrc/gemm.hip gemm_8ph) at shapes the dispatcher routes to it
+(asserted through the uva_gemm_plan query): all four operand layouts, ragged M/N edges and
+K tails, both output dtypes, split-K dW, the fused Linear epilogues (bias, GELU + aux,
+dropout, adaLN gate, residual, beta-accumulate) and the conv epilogue that also emits the
+next GroupNorm's per-tile statistics.  Reference: torch fp32 of the SAME bf16-rounded inputs;
+tolerance 5e-3 relative to the output scale for a bf16 input GEMM with fp32 accumulation
+(1e-2 for bf16 outputs: one extra rounding)."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+
+
+def rel_err(a, b):
+    a, b = a.double(), b.double()
+    return ((a - b).abs().max() / (b.abs().max() + 1e-12)).item()
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _seed():
+    from unified_video_action_amd.native import ops  # noqa: F401 -- fails loudly without the .so
+    torch.manual_seed(0)
+
+
+def _stored(op, t_flag):
+    return op.t().contiguous() if t_flag else op.contiguous()
+
+
+CASES = [(5376, 3072, 328, 256), (5000, 3000, 136, 256), (6144, 2048, 200, 256)]
+
+
+@pytest.mark.parametrize("odt", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("ta,tb", [(0, 0), (0, 1), (1, 0), (1, 1)])
+@pytest.mark.parametrize("M,N,K,bn", CASES)
+def test_gemm8_layouts(odt, ta, tb, M, N, K, bn):
+    from unified_video_action_amd.native import ops
+    assert ops.gemm_plan(M, N, K, ta, tb) == (3, bn, 1)
+    a = torch.randn(M, K, device=DEV).to(torch.bfloat16)
+    b = torch.randn(N, K, device=DEV).to(torch.bfloat16)
+    A, B = _stored(a, ta), _stored(b, tb)
+    C = torch.full((M, N), float("nan"), device=DEV, dtype=odt)
+    ops.gemm(A, B, C, M, N, K, A.stride(0), B.stride(0), C.stride(0), ta, tb)
+    ref = a.float() @ b.float().t()
+    assert torch.isfinite(C).all()
+    assert rel_err(C.float(), ref) < (5e-3 if odt == torch.float32 else 1e-2)
+
+
+@pytest.mark.parametrize("M,N,K,splits", [(768, 768, 16384, 26), (2304, 768, 8192, 9)])
+def test_gemm8_splitk_dw_accumulate(M, N, K, splits):
+    """dW = dY^T X accumulated into an fp32 grad (ta = tb = 1, K = tokens)."""
+    from unified_video_action_amd.native import ops
+    assert ops.gemm_plan(M, N, K, 1, 1) == (3, 256, splits)
+    dy = torch.randn(K, M, device=DEV).to(torch.bfloat16)
+    x = torch.randn(K, N, device=DEV).to(torch.bfloat16)
+    g = torch.randn(M, N, device=DEV)
+    g0 = g.clone()
+    ops.linear_dw(dy, x, g)
+    ref = g0.double() + dy.double().t() @ x.double()
+    assert rel_err(g, ref) < 1e-4  # exact bf16 products, fp32 partial sums over 8-16k terms
+
+
+def test_gemm8_epilogues():
+    from unified_video_action_amd.native import ops
+    M, N, K = 5376, 3072, 256
+    assert ops.gemm_plan(M, N, K) == (3, 256, 1)
+    x = torch.randn(M, K, device=DEV).to(torch.bfloat16)
+    w = (torch.randn(N, K, device=DEV) * 0.1).to(torch.bfloat16)
+    bias = torch.randn(N, device=DEV)
+    pre = x.float() @ w.float().t() + bias
+    # bias + GELU + pre-activation aux, bf16 out
+    out = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+    aux = torch.empty_like(out)
+    ops.linear(x, w, out, bias=bias, act="gelu", aux=aux)
+    assert rel_err(aux.float(), pre) < 1e-2
+    assert rel_err(out.float(), F.gelu(pre)) < 1e-2
+    # dropout: same keep pattern as the elementwise backward mask
+    outd = torch.empty(M, N, device=DEV)
+    ops.linear(x, w, outd, bias=bias, drop_p=0.1, seed=77)
+    kept = outd != 0
+    assert abs(kept.float().mean().item() - 0.9) < 0.005
+    assert rel_err(outd[kept], pre[kept] / 0.9) < 5e-3
+    dg = torch.empty(M, N, device=DEV)
+    ops.act_bwd(None, torch.ones(M, N, device=DEV), dg, "none", drop_p=0.1, seed=77)
+    assert torch.equal(dg != 0, kept)
+    # adaLN gate (bf16, strided) + fp32 residual, fp32 out
+    gate_full = torch.randn(M, 3 * N, device=DEV).to(torch.bfloat16)
+    gate = gate_full[:, 2 * N:]
+    res = torch.randn(M, N, device=DEV)
+    outg = torch.empty(M, N, device=DEV)
+    ops.linear(x, w, outg, bias=bias, gate=gate, residual=res)
+    assert rel_err(outg, res + gate.float() * pre) < 5e-3
+    # bf16 residual, beta accumulate into bf16 C
+    c = torch.randn(M, N, device=DEV).to(torch.bfloat16)
+    c0 = c.float()
+    resb = torch.randn(M, N, device=DEV).to(torch.bfloat16)
+    ops.gemm(x, w, c, M, N, K, K, K, N, 0, 0, residual=resb, ldr=N, beta=1.0)
+    assert rel_err(c.float(), c0 + resb.float() + x.float() @ w.float().t()) < 1e-2
+
+
+@pytest.mark.parametrize("residual", [False, True])
+def test_conv8_with_groupnorm_stats(residual):
+    """3x3 conv (NHWC implicit GEMM) + bias (+residual) through the 8-phase kernel, and the per-128-row
+    GroupNorm(32) partial sums of its stored output -> finalize == GroupNorm of the output."""
+    from unified_video_action_amd.native import ops
+    n, H, W, Ci, Co = 16, 64, 64, 128, 256
+    M = n * H * W
+    assert ops.gemm_plan(M, Co, 9 * Ci, 2, 0, splitk=False) == (3, 256, 1)
+    x = torch.randn(n, H, W, Ci, device=DEV).to(torch.bfloat16)
+    w = (torch.randn(Co, 3, 3, Ci, device=DEV) * 0.05).to(torch.bfloat16)
+    bias = torch.randn(Co, device=DEV) * 0.1
+    res = torch.randn(n, H, W, Co, device=DEV).to(torch.bfloat16) if residual else None
+    out = torch.empty(n, H, W, Co, device=DEV, dtype=torch.bfloat16)
+    part = torch.empty(M // 128, 32, 2, device=DEV)
+    ops.conv2d(x, w, out, n, H, W, Ci, Co, 3, 1, 1, 1, H, W, bias=bias, residual=res, gn_part=part)
+    ref = F.conv2d(x.float().permute(0, 3, 1, 2), w.float().permute(0, 3, 1, 2), bias, padding=1).permute(0, 2, 3, 1)
+    if residual:
+        ref = ref + res.float()
+    assert rel_err(out.float(), ref) < 1e-2
+    gamma = torch.randn(Co, device=DEV)
+    beta = torch.randn(Co, device=DEV)
+    sc = torch.empty(n, Co, device=DEV)
+    sh = torch.empty(n, Co, device=DEV)
+    ops.groupnorm_finalize_tiles(part, n, H * W, Co, gamma, beta, sc, sh, eps=1e-6)
+    o = out.double().reshape(n, H * W, 32, Co // 32)
+    mean = o.mean(dim=(1, 3))
+    var = o.var(dim=(1, 3), unbiased=False)
+    rstd = (var + 1e-6).rsqrt()
+    sc_ref = gamma.double()[None] * rstd.repeat_interleave(Co // 32, dim=1)
+    sh_ref = beta.double()[None] - mean.repeat_interleave(Co // 32, dim=1) * sc_ref
+    assert rel_err(sc, sc_ref) < 1e-4
+    assert rel_err(sh, sh_ref) < 1e-4

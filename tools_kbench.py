@@ -76,3 +76,23 @@ def conv_bench():
 
 if __name__ == "__main__" and len(sys.argv) > 1 and sys.argv[1] == "conv":
     conv_bench()
+
+
+def square_bench():
+    """Square GEMMs (uniform random bf16) to separate kernel quality from shape effects."""
+    dev = "cuda"
+    for S in (4096, 8192):
+        a = (torch.rand(S, S, device=dev) * 2 - 1).to(torch.bfloat16)
+        b = (torch.rand(S, S, device=dev) * 2 - 1).to(torch.bfloat16)
+        c = torch.empty(S, S, device=dev, dtype=torch.bfloat16)
+        fl = 2 * S ** 3
+        res = []
+        for ta, tb in ((0, 0), (0, 1), (1, 1)):
+            t = timeit(lambda: ops.gemm(a, b, c, S, S, S, S, S, S, ta, tb), iters=10)
+            res.append(f"({ta},{tb}) {fl/t/1e9:.0f}")
+        tt = timeit(lambda: torch.matmul(a, b.t()), iters=10)
+        print(f"square {S}^3 plan {ops.gemm_plan(S, S, S)}: " + "  ".join(res) + f" TF   hipBLASLt {fl/tt/1e9:.0f} TF")
+
+
+if __name__ == "__main__" and len(sys.argv) > 1 and sys.argv[1] == "square":
+    square_bench()

@@ -286,6 +286,73 @@ __device__ __forceinline__ int xcd_remap(int bid, int nblk) {
   return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + bid / 8;
 }
 
+// one row segment of 8 consecutive columns (16-B aligned in C): epilogue math with vector loads of
+// C (beta), residual and vector stores; o = the values as stored (for fused statistics)
+template <typename TC>
+__device__ __forceinline__ void epi_row8(TC* __restrict__ C, long long cbase, const EpiParams& ep, long long roff,
+                                         int row, int col0, int z, int M, int N, const float (&v)[8], float (&o)[8]) {
+  float prev[8];
+  if (ep.beta != 0.f) {
+    if constexpr (sizeof(TC) == 2) {
+      bf16x8 pv = *(const bf16x8*)(C + cbase);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) prev[e] = (float)pv[e];
+    } else {
+      float4 p0 = *(const float4*)(C + cbase), p1 = *(const float4*)(C + cbase + 4);
+      prev[0] = p0.x; prev[1] = p0.y; prev[2] = p0.z; prev[3] = p0.w;
+      prev[4] = p1.x; prev[5] = p1.y; prev[6] = p1.z; prev[7] = p1.w;
+    }
+  }
+  float resv[8];
+  if (ep.residual) {
+    const long long ri = roff + (long long)row * ep.ldr + col0;
+    if (ep.res_dt == UVA_DT_BF16 && (ri % 8 == 0)) {
+      bf16x8 rv = *(const bf16x8*)((const bf16*)ep.residual + ri);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) resv[e] = (float)rv[e];
+    } else if (ep.res_dt != UVA_DT_BF16 && (ri % 4 == 0)) {
+      float4 r0 = *(const float4*)((const float*)ep.residual + ri);
+      float4 r1 = *(const float4*)((const float*)ep.residual + ri + 4);
+      resv[0] = r0.x; resv[1] = r0.y; resv[2] = r0.z; resv[3] = r0.w;
+      resv[4] = r1.x; resv[5] = r1.y; resv[6] = r1.z; resv[7] = r1.w;
+    } else {
+#pragma unroll
+      for (int e = 0; e < 8; ++e)
+        resv[e] = ep.res_dt == UVA_DT_BF16 ? (float)((const bf16*)ep.residual)[ri + e]
+                                           : ((const float*)ep.residual)[ri + e];
+    }
+  }
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const int col = col0 + e;
+    float x = ep.alpha * v[e];
+    if (ep.bias) x += ep.bias[col];
+    if (ep.aux) ((TC*)ep.aux)[cbase + e] = from_f32<TC>(x);
+    x = apply_act(ep.act, x);
+    if (ep.drop_thresh)
+      x = dropout_keep(ep.drop_seed, (uint64_t)((long long)z * M * N + (long long)row * N + col), ep.drop_thresh)
+              ? x * ep.drop_scale : 0.f;
+    if (ep.gate) {
+      long long gi = (long long)row * ep.ldg + col;
+      x *= ep.gate_dt == UVA_DT_BF16 ? (float)((const bf16*)ep.gate)[gi] : ((const float*)ep.gate)[gi];
+    }
+    if (ep.residual) x += resv[e];
+    if (ep.beta != 0.f) x += ep.beta * prev[e];
+    o[e] = x;
+  }
+  if constexpr (sizeof(TC) == 2) {
+    bf16x8 ov;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) ov[e] = (bf16)o[e];
+    *(bf16x8*)(C + cbase) = ov;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) o[e] = (float)ov[e];
+  } else {
+    *(float4*)(C + cbase) = make_float4(o[0], o[1], o[2], o[3]);
+    *(float4*)(C + cbase + 4) = make_float4(o[4], o[5], o[6], o[7]);
+  }
+}
+
 // Epilogue staged through LDS: the 128x128 fp32 accumulator tile is written to LDS with
 // compile-time indices (no register-array indexing -> no scratch), then every thread finishes
 // 8 consecutive columns x 8 rows with 16-B vector loads/stores (coalesced, issue-light).
@@ -334,50 +401,7 @@ __device__ __forceinline__ void epilogue_tile(const f32x4 (&acc)[4][4], char* sm
     const long long cbase = coff + (long long)row * ldc + col0;
     if (full) {
       float o[8];
-      float prev[8];
-      if (ep.beta != 0.f) {
-        if constexpr (sizeof(TC) == 2) {
-          bf16x8 pv = *(const bf16x8*)(C + cbase);
-#pragma unroll
-          for (int e = 0; e < 8; ++e) prev[e] = (float)pv[e];
-        } else {
-          float4 p0 = *(const float4*)(C + cbase), p1 = *(const float4*)(C + cbase + 4);
-          prev[0] = p0.x; prev[1] = p0.y; prev[2] = p0.z; prev[3] = p0.w;
-          prev[4] = p1.x; prev[5] = p1.y; prev[6] = p1.z; prev[7] = p1.w;
-        }
-      }
-#pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        const int col = col0 + e;
-        float x = ep.alpha * v[e];
-        if (ep.bias) x += ep.bias[col];
-        if (ep.aux) ((TC*)ep.aux)[cbase + e] = from_f32<TC>(x);
-        x = apply_act(ep.act, x);
-        if (ep.drop_thresh)
-          x = dropout_keep(ep.drop_seed, (uint64_t)((long long)z * M * N + (long long)row * N + col), ep.drop_thresh)
-                  ? x * ep.drop_scale : 0.f;
-        if (ep.gate) {
-          long long gi = (long long)row * ep.ldg + col;
-          x *= ep.gate_dt == UVA_DT_BF16 ? (float)((const bf16*)ep.gate)[gi] : ((const float*)ep.gate)[gi];
-        }
-        if (ep.residual) {
-          long long ri = roff + (long long)row * ep.ldr + col;
-          x += ep.res_dt == UVA_DT_BF16 ? (float)((const bf16*)ep.residual)[ri] : ((const float*)ep.residual)[ri];
-        }
-        if (ep.beta != 0.f) x += ep.beta * prev[e];
-        o[e] = x;
-      }
-      if constexpr (sizeof(TC) == 2) {
-        bf16x8 ov;
-#pragma unroll
-        for (int e = 0; e < 8; ++e) ov[e] = (bf16)o[e];
-        *(bf16x8*)(C + cbase) = ov;
-#pragma unroll
-        for (int e = 0; e < 8; ++e) o[e] = (float)ov[e];
-      } else {
-        *(float4*)(C + cbase) = make_float4(o[0], o[1], o[2], o[3]);
-        *(float4*)(C + cbase + 4) = make_float4(o[4], o[5], o[6], o[7]);
-      }
+      epi_row8<TC>(C, cbase, ep, roff, row, col0, z, M, N, v, o);
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
         gs_s[e] += o[e];
@@ -670,6 +694,448 @@ __global__ __launch_bounds__(256, 2) void gemm_mfma_v2(const bf16* __restrict__ 
                     part ? part + (long long)blockIdx.y * M * N : nullptr, (TA == 2) ? cp.gn_part : nullptr, bm);
 }
 
+// =====================================================================================
+// gemm_8ph -- 256-row block tile, 8 waves, BK = 64, LDS-DMA staging with an 8-phase
+// (2 K-tiles) schedule (cdna_hip_programming.md §5 "256² 8-phase template", T1-T5):
+//   * each K-tile is split into 4 half-tiles: A-h0/A-h1 = the first/second half of every
+//     wave-row's A rows, B-h0/B-h1 likewise for columns; the LDS image of each half is
+//     lane-linear (global_load_lds) with the XOR swizzle applied on the source address;
+//   * phase j of K-tile t reads one operand half into registers -- A-h0, B-h1, A-h1 and (in
+//     phase 3) B-h0 of tile t+1, i.e. 8/4/8/4 ds_read_b128 -- issues one half-tile of DMA for
+//     tile t+2 (B-h0, A-h0, B-h1, A-h1: each ~7 phases ahead of its first read), and runs one
+//     16x16x32 MFMA quadrant (A0B0, A0B1, A1B0, A1B1) between two raw s_barriers;
+//   * the only vmcnt wait is in phase 2 (counted: GA + 2*GB loads stay in flight) and it
+//     retires exactly tile t+1; a half is restaged one phase after the phase whose
+//     lgkmcnt(0) -- issued before that phase's first barrier -- retired its last ds_read;
+//   * waves 4-7 run one barrier behind waves 0-3 (ping-pong: per SIMD one wave's MFMAs overlap
+//     the other's LDS reads); the retire-before-barrier rule keeps the WAR order valid for
+//     both wave groups.
+// BN = 256: waves 2(M) x 4(N) of 128x64;  BN = 128: waves 4(M) x 2(N) of 64x64.
+// =====================================================================================
+template <int W>
+__device__ __forceinline__ int mswz_w(int k) {
+  if constexpr (W == 128) return ((k & 3) << 1) | (((k >> 3) & 1) << 3);   // 256-B rows, 16 chunks
+  else return (((k >> 1) & 1) << 1) | (((k >> 3) & 1) << 2);                // 128-B rows, 8 chunks
+}
+
+// global row (inside the block tile) of row r of half h: rows are grouped per wave-row
+template <int RW>
+__device__ __forceinline__ int half_row(int r, int h) {
+  constexpr int RH = RW / 2;
+  return (r / RH) * RW + h * RH + (r % RH);
+}
+
+// per-lane source of wave-instruction i of half h (G instructions per wave per half)
+template <int T, int RW, int W, int G>
+__device__ __forceinline__ const bf16* dma8_addr(const bf16* __restrict__ P, long long ld, int row0, int nrows, int k0,
+                                                 int K, int h, int i, const ConvParams& cp, const ConvRows& cr) {
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+  const int e = (w * G + i) * 512 + l * 8;
+  if constexpr (T == 1) {
+    const int kr = e / W, cl = (e % W) >> 3;
+    const int m = half_row<RW>((cl ^ mswz_w<W>(kr)) << 3, h);
+    const int gk = k0 + kr, gr = row0 + m;
+    return (gr < nrows && gk < K) ? P + (long long)gk * ld + gr : g_uva_zero_page;
+  } else {
+    const int r = e >> 6, cl = (e & 63) >> 3;
+    const int k = k0 + ((cl ^ (r & 7)) << 3);
+    if constexpr (T == 0) {
+      const int gr = row0 + half_row<RW>(r, h);
+      return (gr < nrows && k < K) ? P + (long long)gr * ld + k : g_uva_zero_page;
+    } else {
+      const int ci_ = h * G + i;
+      if (!cr.ok[ci_] || k >= K) return g_uva_zero_page;
+      const int tap = ((cp.Ci & 63) == 0) ? __builtin_amdgcn_readfirstlane(k0 / cp.Ci) : k / cp.Ci;
+      const int ci = k - tap * cp.Ci;
+      const int kh = cp.ks == 3 ? (tap >= 6 ? 2 : (tap >= 3 ? 1 : 0)) : 0;
+      const int ih = cr.ih0[ci_] + kh, iw = cr.iw0[ci_] + (tap - kh * cp.ks);
+      if (ih < 0 || ih >= cp.Hin || iw < 0 || iw >= cp.Win) return g_uva_zero_page;
+      return P + (((long long)cr.n[ci_] * cp.Hin + ih) * cp.Win + iw) * cp.Ci + ci;
+    }
+  }
+}
+
+template <int T, int RW, int W, int G>
+__device__ __forceinline__ void dma8_half(const bf16* __restrict__ P, long long ld, int row0, int nrows, int k0, int K,
+                                          int h, bf16* img, const ConvParams& cp, const ConvRows& cr) {
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+#pragma unroll
+  for (int i = 0; i < G; ++i) {
+    const bf16* src = dma8_addr<T, RW, W, G>(P, ld, row0, nrows, k0, K, h, i, cp, cr);
+    __builtin_amdgcn_global_load_lds((const void*)src, (__attribute__((address_space(3))) void*)(img + (w * G + i) * 512),
+                                     16, 0, 0);
+  }
+}
+
+// fragment (16 rows x 32 k) from a half image; r0 = first image row / column of the fragment
+template <int T, int W>
+__device__ __forceinline__ bf16x8 frag8(const bf16* img, int r0, int ks) {
+  const int l = threadIdx.x & 63;
+  if constexpr (T != 1) {
+    const int row = r0 + (l & 15);
+    const int c = ks * 4 + (l >> 4);
+    return *(const bf16x8*)(img + row * 64 + ((c ^ (row & 7)) << 3));
+  } else {
+    const int g = l >> 4, q = (l >> 2) & 3, p = l & 3;
+    const int k = ks * 32 + g * 8 + q;
+    const int col = r0 + 4 * p;
+    const int c = col >> 3, w = col & 7;
+    const bf16* a0 = img + k * W + ((c ^ mswz_w<W>(k)) << 3) + w;
+    const bf16* a1 = img + (k + 4) * W + ((c ^ mswz_w<W>(k + 4)) << 3) + w;
+    // inline asm: the intrinsic form makes hipcc wait vmcnt(0) (LDS-DMA alias) before every read;
+    // completion is ordered by the explicit lgkmcnt(0) + sched_barrier before the MFMAs
+    s16x4 lo, hi;
+    asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(lo) : "v"((unsigned)(size_t)LDS_PTR(char, a0)) : "memory");
+    asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(hi) : "v"((unsigned)(size_t)LDS_PTR(char, a1)) : "memory");
+    s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+    return __builtin_bit_cast(bf16x8, v);
+  }
+}
+
+template <int RW>
+__device__ __forceinline__ void conv_rows_init_8(const ConvParams& cp, int row0, int M, ConvRows& cr) {
+  // A halves: 2 x 2 wave-instructions per thread; image row r = ((w*2+i)*512 + l*8) >> 6
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63, hw = cp.Hout * cp.Wout;
+#pragma unroll
+  for (int h = 0; h < 2; ++h)
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int r = ((w * 2 + i) * 512 + l * 8) >> 6;
+      const int m = row0 + half_row<RW>(r, h);
+      const int c = h * 2 + i;
+      cr.ok[c] = m < M;
+      const int mm = cr.ok[c] ? m : 0;
+      const int n = mm / hw, rr = mm % hw;
+      cr.n[c] = n;
+      cr.ih0[c] = (rr / cp.Wout) * cp.stride - cp.pad_t;
+      cr.iw0[c] = (rr % cp.Wout) * cp.stride - cp.pad_l;
+    }
+}
+
+#define EPI8_ROWS 128
+template <int BN>
+struct Gemm8Cfg {
+  static constexpr int BM = 256, WM = (BN == 256) ? 2 : 4, WN = 8 / WM;
+  static constexpr int RWA = BM / WM, RWB = BN / WN;      // rows (cols) per wave
+  static constexpr int FM = RWA / 16, FN = RWB / 16;      // fragments per wave
+  static constexpr int HA = FM / 2, HB = FN / 2;          // fragments per half
+  static constexpr int A_HALF = (BM / 2) * 64, B_HALF = (BN / 2) * 64;   // elements
+  static constexpr int GA = A_HALF / 4096, GB = B_HALF / 4096;          // DMA instrs per thread per half
+  static constexpr int WA = BM / 2, WB = BN / 2;          // M-major image row widths (elements)
+  static constexpr int STAGE = 2 * A_HALF + 2 * B_HALF;   // elements per K-tile stage
+  static constexpr int TP = BN + 4;                       // epilogue fp32 pitch
+  static constexpr int EPI_BYTES = EPI8_ROWS * TP * 4 + 8 * 32 * 8 * 2 * 4;
+  static constexpr int LDS_BYTES = (2 * STAGE * 2 > EPI_BYTES) ? 2 * STAGE * 2 : EPI_BYTES;
+};
+
+// VAR: diagnostic build bits (0 = production): 1 s_memtime stamps per phase segment, 2 no wave-group
+// stagger, 4 no compiler memory fences around barriers, 8 lgkmcnt after the barrier (timing only:
+// breaks the WAR order), 16 no s_setprio
+#define GEMM8_SYNC()                                     \
+  do {                                                   \
+    if constexpr (!(VAR & 4)) asm volatile("" ::: "memory"); \
+  } while (0)
+__device__ unsigned long long g_uva_stamps[16 * 8 * 5];
+
+template <int TA, int TB, int BN, typename TC, int VAR = 0>
+__global__ __launch_bounds__(512, 1) void gemm_8ph(const bf16* __restrict__ A, const bf16* __restrict__ B,
+                                                   TC* __restrict__ C, int M, int N, int K, long long lda,
+                                                   long long ldb, long long ldc, BatchStrides bs, EpiParams ep,
+                                                   ConvParams cp, float* __restrict__ part, int k_per_split) {
+  using G = Gemm8Cfg<BN>;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  bf16* lds = (bf16*)smem;
+  const int z = blockIdx.z, zo = z / bs.binner, zi = z % bs.binner;
+  A += zo * bs.sAo + zi * bs.sAi;
+  B += zo * bs.sBo + zi * bs.sBi;
+  const long long coff = zo * bs.sCo + zi * bs.sCi;
+  const long long roff = zo * ep.sRo + zi * ep.sRi;
+  const int tm = (M + G::BM - 1) / G::BM, tn = (N + BN - 1) / BN;
+  const int nblk = tm * tn;
+  const int pid = xcd_remap(blockIdx.x, nblk);
+  const int GROUP = 8;
+  const int group = pid / (GROUP * tn), first_m = group * GROUP;
+  const int gsz = min(tm - first_m, GROUP);
+  const int bm = first_m + (pid % (GROUP * tn)) % gsz;
+  const int bn = (pid % (GROUP * tn)) / gsz;
+  const int m0 = bm * G::BM, n0 = bn * BN;
+  const int kbeg = blockIdx.y * k_per_split;
+  const int kend = min(K, kbeg + k_per_split);
+  const int nt = (kend - kbeg + 63) / 64;
+  ConvRows cr;
+  if constexpr (TA == 2) conv_rows_init_8<G::RWA>(cp, m0, M, cr);
+  const int wid = threadIdx.x >> 6;
+  const int wr = wid / G::WN, wc = wid % G::WN;
+
+  f32x4 acc[G::FM][G::FN];
+#pragma unroll
+  for (int i = 0; i < G::FM; ++i)
+#pragma unroll
+    for (int j = 0; j < G::FN; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+  // stage layout: [A-h0][A-h1][B-h0][B-h1]
+  auto img_a = [&](int buf, int h) { return lds + buf * G::STAGE + h * G::A_HALF; };
+  auto img_b = [&](int buf, int h) { return lds + buf * G::STAGE + 2 * G::A_HALF + h * G::B_HALF; };
+  // issue half-tile q of K-tile t (q order A-h0, B-h0, B-h1, A-h1; global sequence S = 4t + q)
+  auto stage = [&](auto qc, int t) {
+    constexpr int q = decltype(qc)::value;
+    const int buf = t & 1, k0 = kbeg + t * 64;
+    if constexpr (q == 0 || q == 3) {
+      constexpr int h = q == 0 ? 0 : 1;
+      dma8_half<TA, G::RWA, G::WA, G::GA>(A, lda, m0, M, k0, kend, h, img_a(buf, h), cp, cr);
+    } else {
+      constexpr int h = q - 1;
+      dma8_half<TB, G::RWB, G::WB, G::GB>(B, ldb, n0, N, k0, kend, h, img_b(buf, h), cp, cr);
+    }
+  };
+  using Q0 = std::integral_constant<int, 0>;
+  using Q1 = std::integral_constant<int, 1>;
+  using Q2 = std::integral_constant<int, 2>;
+  using Q3 = std::integral_constant<int, 3>;
+  // DMA order inside a K-tile: B-h0, A-h0, B-h1, A-h1 (the order in which their last reads end)
+  stage(Q1{}, 0);
+  stage(Q0{}, 0);
+  stage(Q2{}, 0);
+  stage(Q3{}, 0);
+  if (nt >= 2) {
+    stage(Q1{}, 1);
+    stage(Q0{}, 1);
+    stage(Q2{}, 1);
+    stage(Q3{}, 1);
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * G::GA + 2 * G::GB) : "memory");
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  GEMM8_SYNC();
+  __builtin_amdgcn_s_barrier();
+  GEMM8_SYNC();
+  bf16x8 fa[G::HA][2], fb0[G::HB][2], fb1[G::HB][2];
+  // B-h0 fragments of tile 0 (afterwards prefetched in phase 3 of the previous tile); every wave
+  // retires them before the common barrier below: phase 0 restages B-h0 of this buffer
+#pragma unroll
+  for (int g = 0; g < G::HB; ++g)
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) fb0[g][ks] = frag8<TB, G::WB>(img_b(0, 0), wc * (G::RWB / 2) + g * 16, ks);
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  GEMM8_SYNC();
+  __builtin_amdgcn_s_barrier();
+  GEMM8_SYNC();
+  // stagger: waves 4-7 run one barrier behind waves 0-3, so on every SIMD one wave's MFMA
+  // cluster overlaps the other wave's LDS reads / DMA issue
+  const int grp = __builtin_amdgcn_readfirstlane(wid >> 2);
+  if (!(VAR & 2) && grp == 1) __builtin_amdgcn_s_barrier();
+  GEMM8_SYNC();
+  unsigned long long st_sum[4] = {0, 0, 0, 0}, st_t0 = 0, st_t1 = 0, st_loop0 = 0;
+#define GEMM8_STAMP(dst)                                                                                  \
+  do {                                                                                                    \
+    if constexpr (VAR & 1) {                                                                              \
+      __builtin_amdgcn_sched_barrier(0);                                                                  \
+      asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(dst)::"memory");                         \
+      __builtin_amdgcn_sched_barrier(0);                                                                  \
+    }                                                                                                     \
+  } while (0)
+  GEMM8_STAMP(st_loop0);
+  st_t0 = st_loop0;
+
+#define GEMM8_QUAD(AH, BH, FB)                                                                            \
+  if constexpr (!(VAR & 16)) __builtin_amdgcn_s_setprio(1);                                               \
+  _Pragma("unroll") for (int f = 0; f < G::HA; ++f)                                                       \
+  _Pragma("unroll") for (int g = 0; g < G::HB; ++g)                                                       \
+  _Pragma("unroll") for (int ks = 0; ks < 2; ++ks)                                                        \
+    acc[AH * G::HA + f][BH * G::HB + g] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(                       \
+        fa[f][ks], FB[g][ks], acc[AH * G::HA + f][BH * G::HB + g], 0, 0, 0);                              \
+  if constexpr (!(VAR & 16)) __builtin_amdgcn_s_setprio(0);                                               \
+  GEMM8_STAMP(st_t1);                                                                                     \
+  st_sum[2] += st_t1 - st_t0;                                                                             \
+  st_t0 = st_t1
+
+#define GEMM8_SYNC_MFMA_BEGIN()                                                                           \
+  if constexpr (!(VAR & 8)) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); /* retire reads BEFORE the barrier */ \
+  GEMM8_STAMP(st_t1);                                                                                     \
+  st_sum[0] += st_t1 - st_t0;                                                                             \
+  st_t0 = st_t1;                                                                                          \
+  GEMM8_SYNC();                                                                                           \
+  __builtin_amdgcn_s_barrier();                                                                           \
+  if constexpr (VAR & 8) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");                              \
+  GEMM8_STAMP(st_t1);                                                                                     \
+  st_sum[1] += st_t1 - st_t0;                                                                             \
+  st_t0 = st_t1;                                                                                          \
+  __builtin_amdgcn_sched_barrier(0)
+
+#define GEMM8_SYNC_MFMA_END()                                                                             \
+  __builtin_amdgcn_s_barrier();                                                                           \
+  GEMM8_SYNC();                                                                                           \
+  GEMM8_STAMP(st_t1);                                                                                     \
+  st_sum[3] += st_t1 - st_t0;                                                                             \
+  st_t0 = st_t1
+
+  for (int t = 0; t < nt; ++t) {
+    const int buf = t & 1;
+    const bool pf = t + 2 < nt;  // tile t+2 exists: stage it into this buffer, one half per phase
+    // ---- phase 0: read A-h0 ; DMA B-h0(t+2) ; MFMA (A0, B0)
+#pragma unroll
+    for (int f = 0; f < G::HA; ++f)
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) fa[f][ks] = frag8<TA, G::WA>(img_a(buf, 0), wr * (G::RWA / 2) + f * 16, ks);
+    if (pf) stage(Q1{}, t + 2);
+    GEMM8_SYNC_MFMA_BEGIN();
+    GEMM8_QUAD(0, 0, fb0);
+    GEMM8_SYNC_MFMA_END();
+    // ---- phase 1: read B-h1 ; DMA A-h0(t+2) ; MFMA (A0, B1)
+#pragma unroll
+    for (int g = 0; g < G::HB; ++g)
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) fb1[g][ks] = frag8<TB, G::WB>(img_b(buf, 1), wc * (G::RWB / 2) + g * 16, ks);
+    if (pf) stage(Q0{}, t + 2);
+    GEMM8_SYNC_MFMA_BEGIN();
+    GEMM8_QUAD(0, 1, fb1);
+    GEMM8_SYNC_MFMA_END();
+    // ---- phase 2: read A-h1 ; DMA B-h1(t+2) ; retire tile t+1 ; MFMA (A1, B0)
+#pragma unroll
+    for (int f = 0; f < G::HA; ++f)
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) fa[f][ks] = frag8<TA, G::WA>(img_a(buf, 1), wr * (G::RWA / 2) + f * 16, ks);
+    if (pf) {
+      stage(Q2{}, t + 2);
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(G::GA + 2 * G::GB) : "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    GEMM8_SYNC_MFMA_BEGIN();
+    GEMM8_QUAD(1, 0, fb0);
+    GEMM8_SYNC_MFMA_END();
+    // ---- phase 3: read B-h0 of tile t+1 (retired in phase 2) ; DMA A-h1(t+2) ; MFMA (A1, B1)
+    if (t + 1 < nt) {
+#pragma unroll
+      for (int g = 0; g < G::HB; ++g)
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks)
+          fb0[g][ks] = frag8<TB, G::WB>(img_b(buf ^ 1, 0), wc * (G::RWB / 2) + g * 16, ks);
+    }
+    if (pf) stage(Q3{}, t + 2);
+    GEMM8_SYNC_MFMA_BEGIN();
+    GEMM8_QUAD(1, 1, fb1);
+    GEMM8_SYNC_MFMA_END();
+  }
+#undef GEMM8_QUAD
+#undef GEMM8_SYNC_MFMA_BEGIN
+#undef GEMM8_SYNC_MFMA_END
+  if constexpr (VAR & 1) {
+    // [read+issue, barrier-1, mfma issue, barrier-2, whole loop] per wave, first 16 blocks
+    GEMM8_STAMP(st_t1);
+    if ((threadIdx.x & 63) == 0 && blockIdx.x < 16 && blockIdx.y == 0 && blockIdx.z == 0) {
+      unsigned long long* o = g_uva_stamps + (blockIdx.x * 8 + wid) * 5;
+      o[0] = st_sum[0]; o[1] = st_sum[1]; o[2] = st_sum[2]; o[3] = st_sum[3]; o[4] = st_t1 - st_loop0;
+    }
+  }
+#undef GEMM8_STAMP
+  if (!(VAR & 2) && grp == 0) __builtin_amdgcn_s_barrier();  // re-align barrier counts: every wave is past its last MFMA
+  GEMM8_SYNC();
+
+  // ---------------- epilogue: 128-row chunks staged through LDS as fp32
+  float* T = (float*)smem;
+  float* pslab = part ? part + (long long)blockIdx.y * M * N : nullptr;
+  float* gn_part = (TA == 2) ? cp.gn_part : nullptr;
+  const int lane = threadIdx.x & 63;
+  constexpr int C8 = BN / 8;             // 8-column chunks per row
+  constexpr int RPP = 512 / C8;          // rows per pass
+  const int c8 = threadIdx.x % C8, rsub = threadIdx.x / C8;
+  const int col0 = n0 + c8 * 8;
+  const bool full = (col0 + 8 <= N) && (ldc % 8 == 0) && ((coff + col0) % 8 == 0);
+#pragma unroll
+  for (int chunk = 0; chunk < 2; ++chunk) {
+    float gs_s[8], gs_q[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) gs_s[e] = gs_q[e] = 0.f;
+    // waves whose rows fall in [chunk*128, chunk*128+128) write their accumulators
+    if ((wr * G::RWA) / EPI8_ROWS == chunk) {
+      const int rbase = wr * G::RWA - chunk * EPI8_ROWS;
+#pragma unroll
+      for (int i = 0; i < G::FM; ++i)
+#pragma unroll
+        for (int j = 0; j < G::FN; ++j)
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            T[(rbase + i * 16 + (lane >> 4) * 4 + r) * G::TP + wc * G::RWB + j * 16 + (lane & 15)] = acc[i][j][r];
+    }
+    __syncthreads();
+    for (int it = 0; it < EPI8_ROWS / RPP; ++it) {
+      const int rl = it * RPP + rsub;
+      const int row = m0 + chunk * EPI8_ROWS + rl;
+      if (row >= M || col0 >= N) break;
+      float v[8];
+      const float4 a = *(const float4*)(T + rl * G::TP + c8 * 8);
+      const float4 b = *(const float4*)(T + rl * G::TP + c8 * 8 + 4);
+      v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+      if (pslab) {
+        float* dst = pslab + (long long)row * N + col0;
+        if (col0 + 8 <= N && N % 4 == 0) {
+          *(float4*)dst = a;
+          *(float4*)(dst + 4) = b;
+        } else {
+          for (int e = 0; e < 8 && col0 + e < N; ++e) dst[e] = v[e];
+        }
+        continue;
+      }
+      const long long cbase = coff + (long long)row * ldc + col0;
+      if (full) {
+        float o[8];
+        epi_row8<TC>(C, cbase, ep, roff, row, col0, z, M, N, v, o);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          gs_s[e] += o[e];
+          gs_q[e] += o[e] * o[e];
+        }
+      } else {
+        for (int e = 0; e < 8 && col0 + e < N; ++e) {
+          const int col = col0 + e;
+          float o = epi_store<TC>(C, ldc, coff, ep, roff, row, col, N,
+                                  (long long)z * M * N + (long long)row * N + col, v[e]);
+          gs_s[e] += o;
+          gs_q[e] += o * o;
+        }
+      }
+    }
+    if constexpr (TA == 2) {
+      if (gn_part) {
+        // per-(128-row chunk, group) sums: lanes sharing c8 inside a wave, then the 8 waves via LDS
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+#pragma unroll
+          for (int o = C8; o < 64; o <<= 1) {
+            gs_s[e] += __shfl_xor(gs_s[e], o, 64);
+            gs_q[e] += __shfl_xor(gs_q[e], o, 64);
+          }
+        }
+        float* red = T + EPI8_ROWS * G::TP;  // [8 waves][C8][8][2]
+        if (lane < C8) {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            red[((wid * C8 + lane) * 8 + e) * 2 + 0] = gs_s[e];
+            red[((wid * C8 + lane) * 8 + e) * 2 + 1] = gs_q[e];
+          }
+        }
+        __syncthreads();
+        const int gsz = N / 32;
+        const int ngroups = min(BN, N - n0) / gsz;
+        if ((int)threadIdx.x < ngroups && m0 + chunk * EPI8_ROWS < M) {
+          float sum = 0.f, sq = 0.f;
+          for (int c = threadIdx.x * gsz; c < ((int)threadIdx.x + 1) * gsz; ++c)
+            for (int w = 0; w < 8; ++w) {
+              sum += red[((w * C8 + (c >> 3)) * 8 + (c & 7)) * 2 + 0];
+              sq += red[((w * C8 + (c >> 3)) * 8 + (c & 7)) * 2 + 1];
+            }
+          const int g = n0 / gsz + threadIdx.x;
+          const long long tile = (long long)bm * 2 + chunk;
+          gn_part[(tile * 32 + g) * 2 + 0] = sum;
+          gn_part[(tile * 32 + g) * 2 + 1] = sq;
+        }
+      }
+    }
+    __syncthreads();
+  }
+}
+
 template <typename TC>
 __global__ __launch_bounds__(256) void splitk_reduce(const float* __restrict__ part, int splits, TC* __restrict__ C,
                                                      int M, int N, long long ldc, EpiParams ep) {
@@ -702,10 +1168,137 @@ static int launch_generic(int ta, int tb, const void* A, const void* B, void* C,
   return 0;
 }
 
+static int env_int(const char* name, int dflt) {
+  const char* e = getenv(name);
+  return e ? atoi(e) : dflt;
+}
+
+struct Plan8 {
+  int bn, splits, kps;
+  long long nblk;
+};
+
+// shape -> 8-phase configuration (bn = 0: not for this kernel)
+static Plan8 plan_8ph(int ta, int M, int N, int K, int batch, bool gn_prologue, bool have_ws, long long ws_floats) {
+  static const int mode = env_int("UVA_GEMM_8PH", 1);          // 0 off, 1 auto, 2 force BN=128, 3 force BN=256
+  static const int f128 = env_int("UVA_8PH_BN128_PCT", 90);    // relative per-CU efficiency of BN=128
+  Plan8 p{0, 1, K, 0};
+  if (mode == 0 || M < 256 || N < 128 || (ta == 2 && gn_prologue)) return p;
+  auto tiles = [&](int bn) { return (long long)((M + 255) / 256) * ((N + bn - 1) / bn); };
+  auto score = [&](int bn) {
+    long long t = tiles(bn) * batch;
+    long long rounds = (t + 255) / 256;
+    double occ = (double)t / (double)(rounds * 256);
+    double useful = (double)M * N / ((double)((M + 255) / 256) * 256 * ((N + bn - 1) / bn) * bn);
+    return occ * useful * (bn == 128 ? f128 / 100.0 : 1.0);
+  };
+  const bool splitk_regime = batch == 1 && have_ws && tiles(128) < 128 && K >= 8 * 64;
+  // measured (tools_kbench.py): BN=256 beats the 128x128 LDS-DMA kernel on every UVA shape it is
+  // chosen for; BN=128 does not yet, so it is opt-in (UVA_GEMM_8PH=2) and auto mode falls back
+  int bn = 128;
+  if (mode == 3) bn = 256;
+  else if (mode == 1) {
+    if (N < 256 || !(splitk_regime || score(256) >= score(128))) return p;
+    bn = 256;
+  }
+  const long long nblk = tiles(bn);
+  int splits = 1;
+  if (batch == 1 && have_ws && nblk < 128 && K >= 8 * 64) {
+    splits = (int)((256 + nblk / 2) / nblk);
+    int kmax = K / (4 * 64);
+    if (splits > kmax) splits = kmax;
+    while (splits > 1 && (long long)splits * M * N > ws_floats) --splits;
+  }
+  if (nblk * splits * batch < 96) return p;  // too small to fill the chip with 1 block/CU
+  int kps = K;
+  if (splits > 1) {
+    kps = ((K + splits - 1) / splits + 63) / 64 * 64;
+    splits = (K + kps - 1) / kps;
+  }
+  p.bn = bn;
+  p.splits = splits;
+  p.kps = kps;
+  p.nblk = nblk;
+  return p;
+}
+
+// 8-phase 256-row kernel: returns 1 if launched, 0 if the shape is not for it, <0 on error
+template <typename TC>
+static int launch_8ph(int ta, int tb, const void* A, const void* B, void* C, int M, int N, int K, long long lda,
+                      long long ldb, long long ldc, int batch, const BatchStrides& bs, const EpiParams& ep,
+                      const ConvParams& cp, float* ws, long long ws_floats, hipStream_t s) {
+  const Plan8 pl = plan_8ph(ta, M, N, K, batch, cp.gn_scale != nullptr, ws != nullptr, ws_floats);
+  if (pl.bn == 0) return 0;
+  const int bn = pl.bn, splits = pl.splits, kps = pl.kps;
+  const long long nblk = pl.nblk;
+  float* part = splits > 1 ? ws : nullptr;
+  dim3 grid((unsigned)nblk, splits, batch);
+#define G8(a, b, BNV)                                                                                       \
+  do {                                                                                                      \
+    static bool attr = false;                                                                               \
+    const int lb = Gemm8Cfg<BNV>::LDS_BYTES;                                                                \
+    if (!attr) {                                                                                            \
+      (void)hipFuncSetAttribute((const void*)gemm_8ph<a, b, BNV, TC>, hipFuncAttributeMaxDynamicSharedMemorySize, lb); \
+      attr = true;                                                                                          \
+    }                                                                                                       \
+    gemm_8ph<a, b, BNV, TC><<<grid, 512, lb, s>>>((const bf16*)A, (const bf16*)B, (TC*)C, M, N, K, lda, ldb, ldc, \
+                                                  bs, ep, cp, part, kps);                                   \
+  } while (0)
+#define G8B(a, b) do { if (bn == 256) G8(a, b, 256); else G8(a, b, 128); } while (0)
+  static const int var = env_int("UVA_8PH_VAR", 0);
+#define G8V(V)                                                                                              \
+  do {                                                                                                      \
+    static bool attr = false;                                                                               \
+    const int lb = Gemm8Cfg<256>::LDS_BYTES;                                                                \
+    if (!attr) {                                                                                            \
+      (void)hipFuncSetAttribute((const void*)gemm_8ph<0, 0, 256, TC, V>, hipFuncAttributeMaxDynamicSharedMemorySize, lb); \
+      attr = true;                                                                                          \
+    }                                                                                                       \
+    gemm_8ph<0, 0, 256, TC, V><<<grid, 512, lb, s>>>((const bf16*)A, (const bf16*)B, (TC*)C, M, N, K, lda, ldb, \
+                                                     ldc, bs, ep, cp, part, kps);                           \
+  } while (0)
+  if (var && ta == 0 && tb == 0 && bn == 256 && sizeof(TC) == 2) {
+    switch (var) {
+      case 1: G8V(1); break;
+      case 2: G8V(2); break;
+      case 3: G8V(3); break;
+      case 4: G8V(4); break;
+      case 8: G8V(8); break;
+      case 9: G8V(9); break;
+      case 16: G8V(16); break;
+      case 12: G8V(12); break;
+      default: return -(int)hipErrorInvalidValue;
+    }
+  } else
+#undef G8V
+  if (ta == 2 && tb == 0) G8B(2, 0);
+  else if (ta == 0 && tb == 0) G8B(0, 0);
+  else if (ta == 0 && tb == 1) G8B(0, 1);
+  else if (ta == 1 && tb == 0) G8B(1, 0);
+  else if (ta == 1 && tb == 1) G8B(1, 1);
+  else return -(int)hipErrorInvalidValue;
+#undef G8B
+#undef G8
+  UVA_LAUNCH_CHECK();
+  if (part) {
+    long long n = (long long)M * N;
+    long long blocks = (n + 255) / 256;
+    if (blocks > 4096) blocks = 4096;
+    splitk_reduce<TC><<<dim3((unsigned)blocks), 256, 0, s>>>(part, splits, (TC*)C, M, N, ldc, ep);
+    UVA_LAUNCH_CHECK();
+  }
+  return 1;
+}
+
 template <typename TC>
 static int launch_mfma(int ta, int tb, const void* A, const void* B, void* C, int M, int N, int K, long long lda,
                        long long ldb, long long ldc, int batch, const BatchStrides& bs, const EpiParams& ep,
                        const ConvParams& cp, float* ws, long long ws_floats, hipStream_t s) {
+  {
+    int r = launch_8ph<TC>(ta, tb, A, B, C, M, N, K, lda, ldb, ldc, batch, bs, ep, cp, ws, ws_floats, s);
+    if (r < 0) return -r;
+    if (r > 0) return 0;
+  }
   const int nblk = ((M + MB_M - 1) / MB_M) * ((N + MB_N - 1) / MB_N);
   // split-K when the output tiling cannot fill the chip (dW GEMMs: few tiles, K = tokens)
   int splits = 1;
@@ -847,6 +1440,21 @@ extern "C" int uva_gemm(int in_dtype, int out_dtype, int ta, int tb, const void*
   ConvParams cp{};
   return gemm_dispatch(in_dtype, out_dtype, ta, tb, A, B, C, M, N, K, lda, ldb, ldc, batch, bs, ep, cp, force_generic,
                        workspace, ws_floats, stream);
+}
+
+extern "C" int uva_debug_gemm8_stamps(unsigned long long* host) {
+  return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_uva_stamps), sizeof(g_uva_stamps));
+}
+
+extern "C" long long uva_gemm_plan(int in_dtype, int ta, int tb, int M, int N, int K, int batch, int gn_prologue,
+                                   long long ws_floats) {
+  // kernel | BN << 4 | splits << 16   (kernel: 0 generic VALU, 1 mfma register-staged, 2 mfma LDS-DMA 128x128,
+  // 3 mfma 8-phase 256-row); assumes 16-B aligned operands
+  if (in_dtype != UVA_DT_BF16 || K % 8 != 0 || (tb == 1 && N % 8 != 0) || (ta == 1 && M % 8 != 0)) return 0;
+  const Plan8 p = plan_8ph(ta, M, N, K, batch, gn_prologue != 0, ws_floats > 0, ws_floats);
+  if (p.bn) return 3 | ((long long)p.bn << 4) | ((long long)p.splits << 16);
+  static const int use_v1 = env_int("UVA_GEMM_V1", 0);
+  return (use_v1 || (ta == 2 && gn_prologue)) ? 1 : 2;
 }
 
 extern "C" int uva_conv2d(int dtype, const void* in, const void* w, void* out, const float* bias, const void* residual,

@@ -76,6 +76,14 @@ def gemm(A, B, C, M, N, K, lda, ldb, ldc, ta=0, tb=0, batch=1, inner=1, sA=(0, 0
 SPLITK_WS_FLOATS = 1 << 25  # 128 MB fp32 partial slabs
 
 
+def gemm_plan(M, N, K, ta=0, tb=0, batch=1, splitk=True, gn_prologue=False, dtype=torch.bfloat16):
+    """(kernel, BN, splits) the native dispatcher picks for a bf16 GEMM of this shape:
+    kernel 0 VALU, 1 MFMA register-staged, 2 MFMA LDS-DMA 128x128, 3 MFMA 8-phase 256-row."""
+    code = lib().query("uva_gemm_plan", 1 if dtype == torch.bfloat16 else 0, ta, tb, M, N, K, batch, int(gn_prologue),
+                       SPLITK_WS_FLOATS if splitk else 0)
+    return code & 15, (code >> 4) & 4095, code >> 16
+
+
 def linear(x, w, out, bias=None, act="none", aux=None, residual=None, drop_p=0.0, seed=0, beta=0.0, gate=None):
     """out[M,N] = epi(x[M,K] @ w[N,K]^T) -- nn.Linear forward."""
     M, K = x.shape
