@@ -145,13 +145,23 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const bf16* __restrict__ 
       float rs = 0.f;
       const long long qrow = (long long)bh * N + (q0 + qt * 16 + li);
 #pragma unroll
-      for (int kt = 0; kt < 4; ++kt)
+      for (int kt = 0; kt < 4; ++kt) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           float p = exp2f(s[kt][qt][r] * scale_log2 - mnew);
           rs += p;
-          s[kt][qt][r] = drop_apply(p, drop, seed, (uint64_t)(qrow * N + kv * 64 + kt * 16 + 4 * g + r), th, dsc);
+          s[kt][qt][r] = p;
         }
+        if (drop) {  // lane owns 4 consecutive keys: two mask pairs
+#pragma unroll
+          for (int r = 0; r < 4; r += 2) {
+            bool k0, k1;
+            dropout_keep2(seed, (uint64_t)(qrow * N + kv * 64 + kt * 16 + 4 * g + r), th, k0, k1);
+            s[kt][qt][r] = k0 ? s[kt][qt][r] * dsc : 0.f;
+            s[kt][qt][r + 1] = k1 ? s[kt][qt][r + 1] * dsc : 0.f;
+          }
+        }
+      }
       rs += __shfl_xor(rs, 16, 64);
       rs += __shfl_xor(rs, 32, 64);
       lsum[qt] = lsum[qt] * alpha + rs;
@@ -425,14 +435,21 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(const bf16* __restrict
     for (int qt = 0; qt < 2; ++qt) {
       const long long qrow = (long long)bh * N + (q0 + qt * 16 + li);
 #pragma unroll
-      for (int kt = 0; kt < 4; ++kt)
+      for (int kt = 0; kt < 4; ++kt) {
+        bool keep[4] = {true, true, true, true};
+        if (drop) {
+#pragma unroll
+          for (int r = 0; r < 4; r += 2)
+            dropout_keep2(seed, (uint64_t)(qrow * N + kv * 64 + kt * 16 + 4 * g + r), th, keep[r], keep[r + 1]);
+        }
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const float p = exp2f(s[kt][qt][r] * scale_log2 - L[qt]);
           float dpt = dp[kt][qt][r];
-          if (drop) dpt = dropout_keep(seed, (uint64_t)(qrow * N + kv * 64 + kt * 16 + 4 * g + r), th) ? dpt * dsc : 0.f;
+          if (drop) dpt = keep[r] ? dpt * dsc : 0.f;
           s[kt][qt][r] = p * (dpt - Dq[qt]);
         }
+      }
     }
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
@@ -468,8 +485,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(const bf16* __restrict
 }
 
 static inline void drop_params(float p, uint32_t* th, float* ds) {
-  *th = p > 0.f ? (uint32_t)fminf(p * 4294967296.0f, 4294967295.0f) : 0u;
-  *ds = p > 0.f ? 1.0f / (1.0f - p) : 1.0f;
+  uva_drop_params(p, th, ds);
 }
 
 extern "C" int uva_attn_fwd(const void* qkv, void* out, float* lse2, int B, int N, int H, float scale, float drop_p,

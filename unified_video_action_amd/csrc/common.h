@@ -1,6 +1,7 @@
 // Shared device helpers for the UVA MI355X (gfx950 / CDNA4) kernels.
 #pragma once
 #include <hip/hip_runtime.h>
+#include <math.h>
 #include <stdint.h>
 
 typedef __bf16 bf16;
@@ -46,17 +47,51 @@ __device__ __forceinline__ float group16_max(float v) {
 }
 
 // ---- counter-based dropout mask (identical in forward and backward kernels) ------------
-__device__ __forceinline__ uint32_t mix32(uint64_t x) {
-  x ^= x >> 33;
-  x *= 0xff51afd7ed558ccdULL;
-  x ^= x >> 33;
-  x *= 0xc4ceb9fe1a85ec53ULL;
-  x ^= x >> 33;
-  return (uint32_t)x;
+// ---- dropout mask ----------------------------------------------------------------------
+// Stateless counter-based mask shared by every kernel that drops (GEMM epilogues, attention
+// fwd/bwd, softmax, activation backward), so forward and backward regenerate identical masks.
+// Element idx belongs to pair idx >> 1; one 32-bit hash per pair (3 x v_mul_lo_u32, no 64-bit
+// multiplies) yields two 16-bit uniforms: low half -> even idx, high half -> odd idx.
+// keep iff u16 >= thresh, thresh = round(p * 65536); kept values scale by 65536 / (65536 - thresh).
+__device__ __forceinline__ uint32_t drop_key(uint64_t seed) {
+  uint32_t k = (uint32_t)seed ^ (((uint32_t)(seed >> 32)) * 0x9E3779B1u);
+  k ^= k >> 16;
+  k *= 0x7feb352du;
+  k ^= k >> 15;
+  return k;
 }
-// keep with probability 1-p: threshold = p * 2^32 (host computes, passed as uint32)
+__device__ __forceinline__ uint32_t drop_hash(uint32_t key, uint64_t pair) {
+  uint32_t x = ((uint32_t)pair * 0x9E3779B1u) ^ (key + __builtin_rotateleft32((uint32_t)(pair >> 32), 11));
+  x ^= x >> 16;
+  x *= 0x7feb352du;
+  x ^= x >> 15;
+  x *= 0x846ca68bu;
+  x ^= x >> 16;
+  return x;
+}
 __device__ __forceinline__ bool dropout_keep(uint64_t seed, uint64_t idx, uint32_t thresh) {
-  return mix32(seed ^ (idx * 0x9E3779B97F4A7C15ULL)) >= thresh;
+  const uint32_t h = drop_hash(drop_key(seed), idx >> 1);
+  return ((idx & 1) ? (h >> 16) : (h & 0xFFFFu)) >= thresh;
+}
+// both elements of the pair (idx_even, idx_even + 1); idx_even must be even
+__device__ __forceinline__ void dropout_keep2(uint64_t seed, uint64_t idx_even, uint32_t thresh, bool& k0, bool& k1) {
+  const uint32_t h = drop_hash(drop_key(seed), idx_even >> 1);
+  k0 = (h & 0xFFFFu) >= thresh;
+  k1 = (h >> 16) >= thresh;
+}
+
+// host: p -> (16-bit threshold, keep scale); thresh 0 = no dropout
+static inline void uva_drop_params(float p, uint32_t* thresh, float* scale) {
+  if (!(p > 0.f)) {
+    *thresh = 0;
+    *scale = 1.0f;
+    return;
+  }
+  long t = lrintf(p * 65536.0f);
+  if (t < 1) t = 1;
+  if (t > 65535) t = 65535;
+  *thresh = (uint32_t)t;
+  *scale = 65536.0f / (float)(65536 - t);
 }
 
 // ---- activations ---------------------------------------------------------------------

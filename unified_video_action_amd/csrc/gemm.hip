@@ -322,6 +322,17 @@ __device__ __forceinline__ void epi_row8(TC* __restrict__ C, long long cbase, co
                                            : ((const float*)ep.residual)[ri + e];
     }
   }
+  bool keep[8] = {true, true, true, true, true, true, true, true};
+  if (ep.drop_thresh) {
+    const uint64_t d0 = (uint64_t)((long long)z * M * N + (long long)row * N + col0);
+    if ((d0 & 1) == 0) {
+#pragma unroll
+      for (int e = 0; e < 8; e += 2) dropout_keep2(ep.drop_seed, d0 + e, ep.drop_thresh, keep[e], keep[e + 1]);
+    } else {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) keep[e] = dropout_keep(ep.drop_seed, d0 + e, ep.drop_thresh);
+    }
+  }
 #pragma unroll
   for (int e = 0; e < 8; ++e) {
     const int col = col0 + e;
@@ -329,9 +340,7 @@ __device__ __forceinline__ void epi_row8(TC* __restrict__ C, long long cbase, co
     if (ep.bias) x += ep.bias[col];
     if (ep.aux) ((TC*)ep.aux)[cbase + e] = from_f32<TC>(x);
     x = apply_act(ep.act, x);
-    if (ep.drop_thresh)
-      x = dropout_keep(ep.drop_seed, (uint64_t)((long long)z * M * N + (long long)row * N + col), ep.drop_thresh)
-              ? x * ep.drop_scale : 0.f;
+    if (ep.drop_thresh) x = keep[e] ? x * ep.drop_scale : 0.f;
     if (ep.gate) {
       long long gi = (long long)row * ep.ldg + col;
       x *= ep.gate_dt == UVA_DT_BF16 ? (float)((const bf16*)ep.gate)[gi] : ((const float*)ep.gate)[gi];
@@ -1388,8 +1397,7 @@ static EpiParams make_epi(const float* bias, const void* residual, long long ldr
   ep.act = act;
   ep.alpha = alpha;
   ep.beta = beta;
-  ep.drop_thresh = drop_p > 0.f ? (uint32_t)fminf(drop_p * 4294967296.0f, 4294967295.0f) : 0u;
-  ep.drop_scale = drop_p > 0.f ? 1.0f / (1.0f - drop_p) : 1.0f;
+  uva_drop_params(drop_p, &ep.drop_thresh, &ep.drop_scale);
   ep.drop_seed = drop_seed;
   ep.ldr = ldr;
   ep.sRo = sRo;

@@ -400,8 +400,9 @@ extern "C" long long uva_colsum_workspace(int rows, int cols) { return (long lon
 extern "C" int uva_softmax_fwd(int dtype, const void* S, void* P, void* Pd, long long rows, int L, float scale,
                                float drop_p, unsigned long long seed, hipStream_t stream) {
   if (rows <= 0) return 0;
-  uint32_t th = drop_p > 0.f ? (uint32_t)fminf(drop_p * 4294967296.0f, 4294967295.0f) : 0u;
-  float ds = drop_p > 0.f ? 1.0f / (1.0f - drop_p) : 1.0f;
+  uint32_t th;
+  float ds;
+  uva_drop_params(drop_p, &th, &ds);
   dim3 grid((unsigned)((rows + 3) / 4));
   if (dtype == UVA_DT_BF16)
     softmax_fwd_kernel<bf16><<<grid, 256, 0, stream>>>((const bf16*)S, (bf16*)P, th ? (bf16*)Pd : nullptr, rows, L, scale, th, ds, seed);
@@ -414,8 +415,9 @@ extern "C" int uva_softmax_fwd(int dtype, const void* S, void* P, void* Pd, long
 extern "C" int uva_softmax_bwd(int dtype, const void* P, const void* dPd, void* dS, long long rows, int L, float scale,
                                float drop_p, unsigned long long seed, hipStream_t stream) {
   if (rows <= 0) return 0;
-  uint32_t th = drop_p > 0.f ? (uint32_t)fminf(drop_p * 4294967296.0f, 4294967295.0f) : 0u;
-  float ds = drop_p > 0.f ? 1.0f / (1.0f - drop_p) : 1.0f;
+  uint32_t th;
+  float ds;
+  uva_drop_params(drop_p, &th, &ds);
   dim3 grid((unsigned)((rows + 3) / 4));
   if (dtype == UVA_DT_BF16)
     softmax_bwd_kernel<bf16><<<grid, 256, 0, stream>>>((const bf16*)P, (const bf16*)dPd, (bf16*)dS, rows, L, scale, th, ds, seed);
