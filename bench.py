@@ -39,6 +39,7 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-trace", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=0)
+    ap.add_argument("--trace-out", default="", help="write every traced kernel row (tag, launches, avg ms) here")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r01.json"))
     return ap.parse_args()
 
@@ -185,6 +186,10 @@ def main():
                            "unit": "TFLOP/s", "frac": round(ach / PEAK_BF16_TFLOPS, 4), "traffic": traffic,
                            "launches_timed": n, "avg_ms": round(avg, 4),
                            "share_of_traced_time": round(tot / sum(r[0] for r in rows), 4)}
+        if args.trace_out:
+            with open(args.trace_out, "w") as f:
+                json.dump([{"kernel": t_, "launches_per_step": n_ / args.steps, "total_ms_per_step": a / args.steps,
+                            "avg_ms": av, "tflops": f_ / (av * 1e-3) / 1e12} for a, t_, n_, av, f_ in rows], f, indent=1)
         out["top_kernels"] = [{"kernel": t_, "total_ms_per_step": round(a / args.steps, 3),
                                "avg_ms": round(av, 4), "tflops": round(f_ / (av * 1e-3) / 1e12, 1)}
                               for a, t_, n_, av, f_ in rows[:8]]

@@ -70,6 +70,14 @@ int uva_conv2d(int dtype, const void* in, const void* w, void* out, const float*
                int Hin, int Win, int Ci, int Co, int ks, int stride, int pad_t, int pad_l, int Hout, int Wout,
                const float* gn_scale, const float* gn_shift, int gn_silu, int act, float* gn_part,
                int force_generic, hipStream_t stream);
+/* Direct 3x3/s1/p1 conv with the input halo staged once per 64-channel chunk in LDS and the
+ * GroupNorm-apply(+SiLU) prologue fused into that staging (ResnetBlock conv1/conv2,
+ * vaekl.py:56-113 incl. Normalize+swish :94-104).  uva_conv2d routes eligible shapes here;
+ * _bn returns the output-channel tile (0 = shape not eligible: H, W % 16, Ci % 64, Co % 128). */
+int uva_conv3x3_halo_bn(int Nimg, int H, int W, int Ci, int Co);
+int uva_conv3x3_halo(const void* in, const void* w, void* out, const float* bias, const void* residual, int Nimg,
+                     int H, int W, int Ci, int Co, const float* gn_scale, const float* gn_shift, int gn_silu,
+                     float* gn_part, hipStream_t stream);
 /* gn_part (bf16 MFMA path): the epilogue also writes per-(128-row tile, group) (sum, sumsq) of
  * the stored output for the NEXT GroupNorm(32) -> uva_groupnorm_finalize_tiles.  Needs
  * (Hout*Wout) % 128 == 0, Co % 32 == 0; buffer [M/128][32][2] floats. */
@@ -108,6 +116,14 @@ int uva_act_fwd(int xdt, const void* x, int ydt, void* y, long long n, int act, 
 int uva_act_bwd(int pdt, const void* pre, int gdt, const void* dy, long long ld_dy, int xdt, void* dx,
                 long long ld_dx, long long rows, int cols, int act, float drop_p, unsigned long long seed, int accum,
                 hipStream_t stream);
+/* act_bwd fused with the bias gradient: dbias[c] (+)= sum_r dx[r][c] (the values as stored);
+ * the nn.Linear bias grad of timm Mlp fc1/fc2 and Attention proj (mar_con_unified.py:201-249),
+ * SimpleMLPAdaLN res-block linears (diffusion_loss.py:142-167).  cols % 8 == 0, 16-B aligned
+ * operands; workspace: uva_act_bwd_bias_workspace(rows, cols) floats. */
+int uva_act_bwd_bias(int pdt, const void* pre, int gdt, const void* dy, long long ld_dy, int xdt, void* dx,
+                     long long ld_dx, long long rows, int cols, int act, float drop_p, unsigned long long seed,
+                     int accum, float* dbias, int accum_bias, float* workspace, hipStream_t stream);
+long long uva_act_bwd_bias_workspace(long long rows, int cols); /* floats */
 int uva_gate_bwd(const float* dout, int hdt, const void* h, int gtdt, const void* gate, long long ldg, int dhdt,
                  void* dh, void* dgate, long long rows, int cols, hipStream_t stream);
 int uva_fill(float* p, long long n, float v, hipStream_t stream);

@@ -1,0 +1,68 @@
+"""Direct 3x3 halo-tile convolution (csrc/conv.hip) against a plain PyTorch fp32 reference of the
+same op: out = bias + residual + conv3x3(silu(x * scale + shift)) over NHWC bf16, zero padding
+applied after the activation (F.conv2d of the activated tensor, vaekl.py:94-104), and the fused
+per-128-pixel GroupNorm(32) partial sums of the stored output.  Tolerance: bf16 operands against
+an fp32 reference on the SAME bf16-rounded activated input -> 1e-2 relative to the output scale;
+GroupNorm scale/shift from the fused partials 1e-4."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def rel_err(a, b):
+    a, b = a.double(), b.double()
+    return ((a - b).abs().max() / (b.abs().max() + 1e-12)).item()
+
+
+@pytest.mark.parametrize("n,H,W,Ci,Co", [(4, 32, 32, 128, 128), (2, 16, 16, 256, 512), (2, 64, 32, 64, 256),
+                                         (1, 48, 16, 192, 128)])
+@pytest.mark.parametrize("gn", [False, True])
+@pytest.mark.parametrize("residual", [False, True])
+def test_conv_halo_matches_torch(n, H, W, Ci, Co, gn, residual):
+    from unified_video_action_amd.native import ops
+    torch.manual_seed(n * 1000 + H + Ci + Co + int(gn) * 7 + int(residual))
+    assert ops.conv_fuses_gn(n, H, W, Ci, Co, 3, 1)
+    x = torch.randn(n, H, W, Ci, device=DEV).to(torch.bfloat16)
+    w = (torch.randn(Co, 3, 3, Ci, device=DEV) * 0.05).to(torch.bfloat16)
+    bias = torch.randn(Co, device=DEV) * 0.1
+    sc = (torch.rand(n, Ci, device=DEV) + 0.5) if gn else None
+    sh = (torch.randn(n, Ci, device=DEV) * 0.3) if gn else None
+    res = torch.randn(n, H, W, Co, device=DEV).to(torch.bfloat16) if residual else None
+    out = torch.empty(n, H, W, Co, device=DEV, dtype=torch.bfloat16)
+    part = torch.empty(n * H * W // 128, 32, 2, device=DEV)
+    ops.conv2d(x, w, out, n, H, W, Ci, Co, 3, 1, 1, 1, H, W, bias=bias, residual=res, gn_scale=sc, gn_shift=sh,
+               gn_silu=True, gn_part=part)
+    a = x.float()
+    if gn:
+        a = F.silu(a * sc[:, None, None, :] + sh[:, None, None, :]).to(torch.bfloat16).float()
+    ref = F.conv2d(a.permute(0, 3, 1, 2), w.float().permute(0, 3, 1, 2), bias, padding=1).permute(0, 2, 3, 1)
+    if residual:
+        ref = ref + res.float()
+    assert rel_err(out.float(), ref) < 1e-2
+    # fused GroupNorm partials of the stored output -> finalize == GroupNorm statistics of `out`
+    gamma = torch.randn(Co, device=DEV)
+    beta = torch.randn(Co, device=DEV)
+    gsc = torch.empty(n, Co, device=DEV)
+    gsh = torch.empty(n, Co, device=DEV)
+    ops.groupnorm_finalize_tiles(part, n, H * W, Co, gamma, beta, gsc, gsh, eps=1e-6)
+    o = out.double().reshape(n, H * W, 32, Co // 32)
+    mean = o.mean(dim=(1, 3))
+    var = o.var(dim=(1, 3), unbiased=False)
+    rstd = (var + 1e-6).rsqrt()
+    sc_ref = gamma.double()[None] * rstd.repeat_interleave(Co // 32, dim=1)
+    sh_ref = beta.double()[None] - mean.repeat_interleave(Co // 32, dim=1) * sc_ref
+    assert rel_err(gsc, sc_ref) < 1e-4
+    assert rel_err(gsh, sh_ref) < 1e-4
+
+
+def test_conv_halo_eligibility():
+    from unified_video_action_amd.native import ops
+    assert ops.conv_fuses_gn(256, 256, 256, 128, 128, 3, 1)
+    assert ops.conv_fuses_gn(256, 16, 16, 512, 512, 3, 1)
+    assert not ops.conv_fuses_gn(256, 16, 16, 512, 32, 3, 1)    # conv_out: Co % 128
+    assert not ops.conv_fuses_gn(256, 256, 256, 8, 128, 3, 1)   # conv_in: Ci % 64
+    assert not ops.conv_fuses_gn(256, 256, 256, 128, 128, 3, 2)  # downsample
+    assert not ops.conv_fuses_gn(4, 24, 24, 128, 128, 3, 1)     # 16 does not tile 24

@@ -105,9 +105,10 @@ def test_conv8_with_groupnorm_stats(residual):
     """3x3 conv (NHWC implicit GEMM) + bias (+residual) through the 8-phase kernel, and the per-128-row
     GroupNorm(32) partial sums of its stored output -> finalize == GroupNorm of the output."""
     from unified_video_action_amd.native import ops
-    n, H, W, Ci, Co = 16, 64, 64, 128, 256
+    n, H, W, Ci, Co = 16, 64, 64, 96, 256  # Ci % 64 != 0: not a halo-kernel shape (test_conv_halo_gpu.py)
     M = n * H * W
     assert ops.gemm_plan(M, Co, 9 * Ci, 2, 0, splitk=False) == (3, 256, 1)
+    assert not ops.conv_fuses_gn(n, H, W, Ci, Co, 3, 1)
     x = torch.randn(n, H, W, Ci, device=DEV).to(torch.bfloat16)
     w = (torch.randn(Co, 3, 3, Ci, device=DEV) * 0.05).to(torch.bfloat16)
     bias = torch.randn(Co, device=DEV) * 0.1

@@ -187,6 +187,33 @@ def test_colsum_and_cast():
     assert torch.equal(xb, x.to(torch.bfloat16))
 
 
+@pytest.mark.parametrize("rows,cols", [(5000, 296), (33000, 768)])
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_colsum_vectorized_tall(rows, cols, dtype):
+    from unified_video_action_amd.native import ops
+    x = torch.randn(rows, cols, device=DEV).to(dtype)
+    out = torch.full((cols,), 0.5, device=DEV)
+    ops.colsum(x, out, accum=True)
+    assert rel_err(out - 0.5, x.float().sum(0)) < 1e-5
+
+
+@pytest.mark.parametrize("act,drop", [("none", 0.1), ("gelu", 0.1), ("silu", 0.0)])
+@pytest.mark.parametrize("gdt", [torch.float32, torch.bfloat16])
+def test_act_bwd_bias_matches_act_bwd_plus_colsum(act, drop, gdt):
+    """fused activation/dropout backward + bias gradient == act_bwd then colsum (same mask)."""
+    from unified_video_action_amd.native import ops
+    R, C = 1000, 520
+    pre = torch.randn(R, C, device=DEV).to(torch.bfloat16)
+    dy = torch.randn(R, C, device=DEV).to(gdt)
+    ref = torch.empty(R, C, device=DEV, dtype=torch.bfloat16)
+    ops.act_bwd(pre if act != "none" else None, dy, ref, act, drop_p=drop, seed=77)
+    got = torch.empty_like(ref)
+    db = torch.ones(C, device=DEV)
+    ops.act_bwd_bias(pre if act != "none" else None, dy, got, db, act, drop_p=drop, seed=77)
+    assert torch.equal(got, ref)
+    assert rel_err(db - 1, ref.float().sum(0)) < 1e-5
+
+
 def test_act_fwd_bwd():
     from unified_video_action_amd.native import ops
     x = torch.randn(1000, 64, device=DEV)

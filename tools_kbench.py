@@ -71,7 +71,15 @@ def conv_bench():
         out = torch.empty(n, H, H, Co, device=dev, dtype=torch.bfloat16)
         fl = 2 * n * H * H * Co * 9 * Ci
         t = timeit(lambda: ops.conv2d(x, w, out, n, H, H, Ci, Co, 3, 1, 1, 1, H, H), iters=5)
-        print(f"conv3x3 n{n} {H}x{H} Ci{Ci} Co{Co}: {t:.2f} ms {fl/t/1e9:.0f} TF")
+        sc = torch.rand(n, Ci, device=dev) + 0.5
+        sh = torch.randn(n, Ci, device=dev) * 0.3
+        res = torch.randn(n, H, H, Co, device=dev).to(torch.bfloat16)
+        bias = torch.randn(Co, device=dev)
+        part = torch.empty(n * H * H // 128, 32, 2, device=dev)
+        t2 = timeit(lambda: ops.conv2d(x, w, out, n, H, H, Ci, Co, 3, 1, 1, 1, H, H, bias=bias, residual=res,
+                                       gn_scale=sc, gn_shift=sh, gn_part=part), iters=5)
+        print(f"conv3x3 n{n} {H}x{H} Ci{Ci} Co{Co}: {t:.2f} ms {fl/t/1e9:.0f} TF   "
+              f"+GN/SiLU prologue, bias, residual, GN stats: {t2:.2f} ms {fl/t2/1e9:.0f} TF")
 
 
 if __name__ == "__main__" and len(sys.argv) > 1 and sys.argv[1] == "conv":

@@ -1,0 +1,317 @@
+// Direct 3x3 / stride-1 / pad-1 convolution over NHWC bf16 with the input patch staged ONCE
+// per 64-channel chunk into LDS (halo tile) and GroupNorm-apply + SiLU fused into that staging.
+//
+// Replaces nn.Conv2d(k=3, s=1, p=1) of the KL-VAE encoder ResnetBlock conv1/conv2 and conv_out
+// (reference vae/vaekl.py:56-113, 246-273) together with the Normalize + nonlinearity that
+// precede them (vaekl.py:9-17, 94-104, 270-271): out = bias + residual + conv(silu(gn(x))).
+//
+// Work decomposition (one 512-thread workgroup per output tile, 1 workgroup / CU):
+//   * output tile = 16 x 16 pixels x BN output channels (BN = 128 or 256);
+//   * K loop = (64-channel chunk cc) x (9 taps); per chunk the 18 x 18 x 64 input halo is
+//     loaded to registers at tap 0, normalised + SiLU'd (zero padding applied AFTER the
+//     activation, as F.conv2d pads the activated tensor) and written to the other halo buffer
+//     at tap 8 -- every input element is read from HBM/L2 once per chunk instead of 9x
+//     (implicit-GEMM im2col) and the GroupNorm output never round-trips through HBM;
+//   * the weight tile of each (chunk, tap) step -- BN rows x 64 k -- is staged by LDS-DMA
+//     (global_load_lds, 16 B/lane) one step ahead into a 2-deep ring;
+//   * A fragments (16 pixels of one tile row x 32 channels) are read from the halo image at
+//     the tap's (kh, kw) offset: pixel p's 16-B channel chunk c sits at slot c ^ (p & 7), which
+//     is bank-conflict-free for every tap offset (ds_read_b128, 16-lane groups);
+//   * v_mfma_f32_16x16x32_bf16, fp32 accumulation; waves 2(M) x 4(N) of 128 px x 64 co (BN 256)
+//     or 4(M) x 2(N) of 64 x 64 (BN 128);
+//   * epilogue through LDS (128-pixel halves of the tile, fp32), bias + bf16 residual, 16-B
+//     stores, and the deterministic per-(128-pixel half, group) GroupNorm(32) partial sums of
+//     the stored output for the NEXT GroupNorm (uva_groupnorm_finalize_tiles, tile_rows 128).
+#include "common.h"
+
+#define CH_T 16
+#define CH_H 18
+#define CH_HPIX (CH_H * CH_H)
+#define CH_HALO_ELEMS (CH_HPIX * 64)
+#define CH_ROUNDS ((CH_HPIX * 8 + 511) / 512)
+
+template <int BN>
+struct ConvHCfg {
+  static constexpr int WM = BN == 256 ? 2 : 4, WN = 8 / WM;
+  static constexpr int FM = CH_T / WM;          // tile rows (16-pixel fragments) per wave
+  static constexpr int FN = BN / WN / 16;       // 16-channel fragments per wave
+  static constexpr int BT = BN * 64;            // weight tile elements
+  static constexpr int NI = BT / 4096;          // DMA instructions per thread per weight tile
+  static constexpr int MAIN_BYTES = (2 * CH_HALO_ELEMS + 2 * BT) * 2;
+  static constexpr int TP = BN + 4;             // epilogue fp32 pitch
+  static constexpr int EPI_BYTES = 128 * TP * 4 + 8 * (BN / 8) * 8 * 2 * 4;
+  static constexpr int LDS_BYTES = MAIN_BYTES > EPI_BYTES ? MAIN_BYTES : EPI_BYTES;
+};
+
+__device__ __forceinline__ int ch_xcd_remap(int bid, int nblk) {
+  int q = nblk / 8, r = nblk % 8, x = bid % 8;
+  return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + bid / 8;
+}
+
+template <int BN, bool GN>
+__global__ __launch_bounds__(512, 1) void conv3x3_halo(const bf16* __restrict__ in, const bf16* __restrict__ wt,
+                                                       bf16* __restrict__ out, const float* __restrict__ bias,
+                                                       const bf16* __restrict__ residual,
+                                                       const float* __restrict__ gn_scale,
+                                                       const float* __restrict__ gn_shift, int gn_silu,
+                                                       float* __restrict__ gn_part, int Nimg, int H, int W, int Ci,
+                                                       int Co) {
+  using G = ConvHCfg<BN>;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  bf16* halo = (bf16*)smem;
+  bf16* bimg = halo + 2 * CH_HALO_ELEMS;
+  const int tiles_x = W / CH_T, tiles_y = H / CH_T, ncb = Co / BN;
+  const int nblk = Nimg * tiles_y * tiles_x * ncb;
+  const int pid = ch_xcd_remap(blockIdx.x, nblk);
+  const int cb = pid % ncb;
+  const int sp = pid / ncb;  // spatial tile id, image-major
+  const int tx = sp % tiles_x, ty = (sp / tiles_x) % tiles_y, n = sp / (tiles_x * tiles_y);
+  const int oh0 = ty * CH_T, ow0 = tx * CH_T, n0 = cb * BN;
+  const int K = 9 * Ci, nch = Ci / 64, S = nch * 9;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wid / G::WN, wn = wid % G::WN;
+
+  // ---- weight tile of step s (chunk s/9, tap s%9) -> ring slot b; K-major [BN][64] image,
+  //      16-B chunk c of row r at slot c ^ (r & 7), swizzle applied on the per-lane source
+  auto dma_w = [&](int s, int b) {
+    const int cc = s / 9, tap = s - cc * 9;
+    const bf16* base = wt + (long long)n0 * K + tap * Ci + cc * 64;
+    bf16* img = bimg + b * G::BT;
+#pragma unroll
+    for (int i = 0; i < G::NI; ++i) {
+      const int e = (wid * G::NI + i) * 512 + lane * 8;
+      const int row = e >> 6, slot = (e & 63) >> 3;
+      const bf16* src = base + (long long)row * K + ((slot ^ (row & 7)) << 3);
+      __builtin_amdgcn_global_load_lds((const void*)src,
+                                       (__attribute__((address_space(3))) void*)(img + (wid * G::NI + i) * 512), 16,
+                                       0, 0);
+    }
+  };
+
+  // ---- halo: thread t owns 16-B chunk c = t & 7 of pixels p = (t + 512 i) >> 3
+  const int hc = tid & 7;
+  bf16x8 hreg[CH_ROUNDS];
+  float gsc[8], gsh[8];
+  auto halo_load = [&](int cc) {
+#pragma unroll
+    for (int i = 0; i < CH_ROUNDS; ++i) {
+      const int p = min((tid + i * 512) >> 3, CH_HPIX - 1);
+      const int hy = p / CH_H, hx = p - hy * CH_H;
+      const int ih = min(max(oh0 - 1 + hy, 0), H - 1), iw = min(max(ow0 - 1 + hx, 0), W - 1);  // clamped: always in bounds
+      hreg[i] = *(const bf16x8*)(in + (((long long)n * H + ih) * W + iw) * Ci + cc * 64 + hc * 8);
+    }
+    if constexpr (GN) {
+      const float* sc = gn_scale + (long long)n * Ci + cc * 64 + hc * 8;
+      const float* sh = gn_shift + (long long)n * Ci + cc * 64 + hc * 8;
+      const float4 s0 = *(const float4*)sc, s1 = *(const float4*)(sc + 4);
+      const float4 h0 = *(const float4*)sh, h1 = *(const float4*)(sh + 4);
+      gsc[0] = s0.x; gsc[1] = s0.y; gsc[2] = s0.z; gsc[3] = s0.w; gsc[4] = s1.x; gsc[5] = s1.y; gsc[6] = s1.z; gsc[7] = s1.w;
+      gsh[0] = h0.x; gsh[1] = h0.y; gsh[2] = h0.z; gsh[3] = h0.w; gsh[4] = h1.x; gsh[5] = h1.y; gsh[6] = h1.z; gsh[7] = h1.w;
+    }
+  };
+  auto halo_store = [&](int hb) {
+    bf16* img = halo + hb * CH_HALO_ELEMS;
+#pragma unroll
+    for (int i = 0; i < CH_ROUNDS; ++i) {
+      const int p = (tid + i * 512) >> 3;
+      if (p < CH_HPIX) {
+        const int hy = p / CH_H, hx = p - hy * CH_H;
+        const int ih = oh0 - 1 + hy, iw = ow0 - 1 + hx;
+        bf16x8 v = hreg[i];
+        if (ih < 0 || ih >= H || iw < 0 || iw >= W) {
+          v = (bf16x8){};
+        } else if constexpr (GN) {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            const float u = (float)v[j] * gsc[j] + gsh[j];
+            v[j] = (bf16)(gn_silu ? silu(u) : u);
+          }
+        }
+        *(bf16x8*)(img + p * 64 + ((hc ^ (p & 7)) << 3)) = v;
+      }
+    }
+  };
+
+  f32x4 acc[G::FM][G::FN];
+#pragma unroll
+  for (int i = 0; i < G::FM; ++i)
+#pragma unroll
+    for (int j = 0; j < G::FN; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+  // ---- prologue: weight tile 0 + halo of chunk 0
+  dma_w(0, 0);
+  halo_load(0);
+  halo_store(0);
+  asm volatile("s_waitcnt vmcnt(0)\n\ts_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+
+  const int frow = lane & 15, fk = lane >> 4;
+  for (int cc = 0; cc < nch; ++cc) {
+    const bf16* hcur = halo + (cc & 1) * CH_HALO_ELEMS;
+    const bool more = cc + 1 < nch;
+#pragma unroll 1
+    for (int tap = 0; tap < 9; ++tap) {
+      const int s = cc * 9 + tap;
+      // ring slot (s+1)&1 was last read in step s-1; every wave passed the barrier that ended it
+      if (s + 1 < S) dma_w(s + 1, (s + 1) & 1);
+      if (tap == 0 && more) halo_load(cc + 1);
+      const bf16* bcur = bimg + (s & 1) * G::BT;
+      const int kh = tap / 3, kw = tap % 3;
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        const int c = ks * 4 + fk;
+        bf16x8 fa[G::FM], fb[G::FN];
+#pragma unroll
+        for (int f = 0; f < G::FM; ++f) {
+          const int p = (wm * G::FM + f + kh) * CH_H + frow + kw;
+          fa[f] = *(const bf16x8*)(hcur + p * 64 + ((c ^ (p & 7)) << 3));
+        }
+#pragma unroll
+        for (int g = 0; g < G::FN; ++g) {
+          const int r = wn * (G::FN * 16) + g * 16 + frow;
+          fb[g] = *(const bf16x8*)(bcur + r * 64 + ((c ^ (r & 7)) << 3));
+        }
+        __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int f = 0; f < G::FM; ++f)
+#pragma unroll
+          for (int g = 0; g < G::FN; ++g)
+            acc[f][g] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[f], fb[g], acc[f][g], 0, 0, 0);
+        __builtin_amdgcn_s_setprio(0);
+      }
+      if (tap == 8 && more) halo_store((cc + 1) & 1);  // buffer last read in chunk cc-1
+      asm volatile("s_waitcnt vmcnt(0)\n\ts_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+    }
+  }
+
+  // ---- epilogue: two 128-pixel halves (tile rows 0-7, 8-15) staged through LDS as fp32
+  float* T = (float*)smem;
+  constexpr int C8 = BN / 8, RPP = 512 / C8;
+  const int c8 = tid % C8, rsub = tid / C8;
+  const int col0 = n0 + c8 * 8;
+  float bv[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) bv[e] = bias ? bias[col0 + e] : 0.f;
+  const int tiles_img = tiles_x * tiles_y;
+#pragma unroll
+  for (int half = 0; half < 2; ++half) {
+    if ((wm * G::FM) / 8 == half) {
+#pragma unroll
+      for (int f = 0; f < G::FM; ++f)
+#pragma unroll
+        for (int g = 0; g < G::FN; ++g)
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            T[((wm * G::FM + f - half * 8) * 16 + fk * 4 + r) * G::TP + wn * (G::FN * 16) + g * 16 + frow] = acc[f][g][r];
+    }
+    __syncthreads();
+    float gs[8], gq[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) gs[e] = gq[e] = 0.f;
+    for (int it = 0; it < 128 / RPP; ++it) {
+      const int rl = it * RPP + rsub;  // pixel inside the half: row half*8 + rl/16, column rl%16
+      const int oh = oh0 + half * 8 + (rl >> 4), ow = ow0 + (rl & 15);
+      const long long ob = (((long long)n * H + oh) * W + ow) * Co + col0;
+      const float4 a = *(const float4*)(T + rl * G::TP + c8 * 8);
+      const float4 b = *(const float4*)(T + rl * G::TP + c8 * 8 + 4);
+      float v[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+      if (residual) {
+        const bf16x8 rv = *(const bf16x8*)(residual + ob);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] += bv[e], v[e] += (float)rv[e];
+      } else {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] += bv[e];
+      }
+      bf16x8 o;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) o[e] = (bf16)v[e];
+      *(bf16x8*)(out + ob) = o;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float q = (float)o[e];
+        gs[e] += q;
+        gq[e] += q * q;
+      }
+    }
+    if (gn_part) {
+      // per-column sums over the half's 128 pixels (lanes sharing c8, then the 8 waves via LDS)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+#pragma unroll
+        for (int o = C8; o < 64; o <<= 1) {
+          gs[e] += __shfl_xor(gs[e], o, 64);
+          gq[e] += __shfl_xor(gq[e], o, 64);
+        }
+      }
+      float* red = T + 128 * G::TP;  // [8 waves][C8][8][2]
+      if (lane < C8) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          red[((wid * C8 + lane) * 8 + e) * 2 + 0] = gs[e];
+          red[((wid * C8 + lane) * 8 + e) * 2 + 1] = gq[e];
+        }
+      }
+      __syncthreads();
+      const int gsz = Co / 32;
+      const int ngroups = BN / gsz;
+      if (tid < ngroups) {
+        float sum = 0.f, sq = 0.f;
+        for (int c = tid * gsz; c < (tid + 1) * gsz; ++c) {
+          for (int w = 0; w < 8; ++w) {
+            sum += red[((w * C8 + (c >> 3)) * 8 + (c & 7)) * 2 + 0];
+            sq += red[((w * C8 + (c >> 3)) * 8 + (c & 7)) * 2 + 1];
+          }
+        }
+        const int g = n0 / gsz + tid;
+        const long long t128 = ((long long)n * tiles_img + (sp % tiles_img)) * 2 + half;
+        gn_part[(t128 * 32 + g) * 2 + 0] = sum;
+        gn_part[(t128 * 32 + g) * 2 + 1] = sq;
+      }
+    }
+    __syncthreads();
+  }
+}
+
+// eligibility of the halo kernel (host side mirror: native/ops.py conv_halo_ok)
+static int halo_bn(int Nimg, int H, int W, int Ci, int Co) {
+  if (H % CH_T || W % CH_T || Ci % 64 || Ci < 64) return 0;
+  const long long tiles = (long long)Nimg * (H / CH_T) * (W / CH_T);
+  (void)tiles;  // BN = 256 (2 x 4 waves of 128 x 64) spills at 256 VGPRs in this form: 128 only
+  if (Co % 128 == 0) return 128;
+  return 0;
+}
+
+extern "C" int uva_conv3x3_halo_bn(int Nimg, int H, int W, int Ci, int Co) { return halo_bn(Nimg, H, W, Ci, Co); }
+
+extern "C" int uva_conv3x3_halo(const void* in, const void* w, void* out, const float* bias, const void* residual,
+                                int Nimg, int H, int W, int Ci, int Co, const float* gn_scale, const float* gn_shift,
+                                int gn_silu, float* gn_part, hipStream_t stream) {
+  if (Nimg <= 0) return 0;
+  const int bn = halo_bn(Nimg, H, W, Ci, Co);
+  if (!bn || (((uintptr_t)in | (uintptr_t)w | (uintptr_t)out | (uintptr_t)residual) % 16)) return (int)hipErrorInvalidValue;
+  if ((gn_scale == nullptr) != (gn_shift == nullptr)) return (int)hipErrorInvalidValue;
+  const long long nblk = (long long)Nimg * (H / CH_T) * (W / CH_T) * (Co / bn);
+  if (nblk >= (1ll << 31)) return (int)hipErrorInvalidValue;
+#define CH_LAUNCH(BNV, GNV)                                                                                    \
+  do {                                                                                                         \
+    static bool attr = false;                                                                                  \
+    const int lb = ConvHCfg<BNV>::LDS_BYTES;                                                                   \
+    if (!attr) {                                                                                               \
+      (void)hipFuncSetAttribute((const void*)conv3x3_halo<BNV, GNV>, hipFuncAttributeMaxDynamicSharedMemorySize, lb); \
+      attr = true;                                                                                             \
+    }                                                                                                          \
+    conv3x3_halo<BNV, GNV><<<dim3((unsigned)nblk), 512, lb, stream>>>(                                         \
+        (const bf16*)in, (const bf16*)w, (bf16*)out, bias, (const bf16*)residual, gn_scale, gn_shift, gn_silu, \
+        gn_part, Nimg, H, W, Ci, Co);                                                                          \
+  } while (0)
+  if (gn_scale) CH_LAUNCH(128, true);
+  else CH_LAUNCH(128, false);
+#undef CH_LAUNCH
+  UVA_LAUNCH_CHECK();
+  return 0;
+}

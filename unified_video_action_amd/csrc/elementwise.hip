@@ -123,6 +123,145 @@ __global__ void act_bwd_vec_kernel(const void* pre, int pdt, const GT* __restric
   }
 }
 
+// Activation/dropout backward fused with the bias gradient (nn.Linear bias grad = column sum
+// of the pre-activation gradient, the tensor the dW GEMM consumes): block = 32 column groups
+// (8 columns, 16-B loads) x 8 row lanes over a chunk of COLSUM_RPB rows; the LDS-reduced chunk
+// sums go to part[chunk][cols] (fp32, sums of the values as stored), reduced by colsum_final.
+// STORE = false: plain column-sum partials of dy (no act, no store) -- uva_colsum's tall path.
+#define COLSUM_RPB 128
+template <typename GT, typename XT, bool STORE>
+__global__ __launch_bounds__(256) void act_bwd_colsum_kernel(const void* pre, int pdt, const GT* __restrict__ dy,
+                                                             XT* __restrict__ dx, int rows, int cols, long long ld_dy,
+                                                             long long ld_dx, int act, uint32_t thresh, float dscale,
+                                                             uint64_t seed, int accum, float* __restrict__ part) {
+  __shared__ float red[8][32 * 8 + 4];
+  const int cg = threadIdx.x & 31, rl = threadIdx.x >> 5;
+  const int c0 = (blockIdx.x * 32 + cg) * 8;
+  const int r0 = blockIdx.y * COLSUM_RPB, r1 = min(rows, r0 + COLSUM_RPB);
+  float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  if (c0 < cols) {
+#pragma unroll 4
+    for (int r = r0 + rl; r < r1; r += 8) {
+      float g[8];
+      ld8<GT>(dy + (long long)r * ld_dy + c0, g);
+      if (STORE) {
+        if (thresh) {
+          const uint64_t e0 = (uint64_t)r * cols + c0;
+#pragma unroll
+          for (int e = 0; e < 8; e += 2) {
+            bool k0, k1;
+            dropout_keep2(seed, e0 + e, thresh, k0, k1);
+            g[e] = k0 ? g[e] * dscale : 0.f;
+            g[e + 1] = k1 ? g[e + 1] * dscale : 0.f;
+          }
+        }
+        if (act != ACT_NONE) {
+          float pv[8];
+          const long long pi = (long long)r * cols + c0;
+          if (pdt == UVA_DT_BF16) ld8<bf16>((const bf16*)pre + pi, pv);
+          else ld8<float>((const float*)pre + pi, pv);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) g[e] *= act_grad(act, pv[e]);
+        }
+        XT* o = dx + (long long)r * ld_dx + c0;
+        if (accum) {
+          float prev[8];
+          ld8<XT>(o, prev);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) g[e] += prev[e];
+        }
+        st8<XT>(o, g);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) s[e] += to_f32(from_f32<XT>(g[e]));
+      } else {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) s[e] += g[e];
+      }
+    }
+  }
+#pragma unroll
+  for (int e = 0; e < 8; ++e) red[rl][cg * 8 + e] = s[e];
+  __syncthreads();
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  if (c < cols) {
+    float t = 0.f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) t += red[j][threadIdx.x];
+    part[(long long)blockIdx.y * cols + c] = t;
+  }
+}
+
+// out[c] (+)= sum_j part[j][c]: 32 columns x 8 row lanes per block
+__global__ __launch_bounds__(256) void colsum_final_kernel(const float* __restrict__ part, int nrows, int cols,
+                                                           float* __restrict__ out, int accum) {
+  __shared__ float red[8][33];
+  const int cl = threadIdx.x & 31, rl = threadIdx.x >> 5;
+  const int c = blockIdx.x * 32 + cl;
+  float s = 0.f;
+  if (c < cols) {
+#pragma unroll 8
+    for (int j = rl; j < nrows; j += 8) s += part[(long long)j * cols + c];
+  }
+  red[rl][cl] = s;
+  __syncthreads();
+  if (rl == 0 && c < cols) {
+    float t = 0.f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) t += red[j][cl];
+    out[c] = accum ? out[c] + t : t;
+  }
+}
+
+extern "C" long long uva_act_bwd_bias_workspace(long long rows, int cols) {
+  return (rows + COLSUM_RPB - 1) / COLSUM_RPB * (long long)cols;
+}
+
+// uva_act_bwd + dbias (+)= column sums of dx (as stored); bf16/fp32, cols % 8 == 0, 16-B aligned
+extern "C" int uva_act_bwd_bias(int pdt, const void* pre, int gdt, const void* dy, long long ld_dy, int xdt, void* dx,
+                                long long ld_dx, long long rows, int cols, int act, float drop_p,
+                                unsigned long long seed, int accum, float* dbias, int accum_bias, float* workspace,
+                                hipStream_t s) {
+  if (rows <= 0 || cols <= 0) return 0;
+  if (cols % 8 || ld_dy % 8 || ld_dx % 8 || rows >= (1ll << 31) ||
+      (((uintptr_t)dy | (uintptr_t)dx | (uintptr_t)pre) % 16) || !dbias || !workspace)
+    return (int)hipErrorInvalidValue;
+  uint32_t th;
+  float ds;
+  uva_drop_params(drop_p, &th, &ds);
+  const int nch = (int)((rows + COLSUM_RPB - 1) / COLSUM_RPB);
+  dim3 g1((cols / 8 + 31) / 32, nch);
+#define AB(GT, XT)                                                                                               \
+  act_bwd_colsum_kernel<GT, XT, true><<<g1, 256, 0, s>>>(pre, pdt, (const GT*)dy, (XT*)dx, (int)rows, cols, ld_dy, \
+                                                         ld_dx, act, th, ds, seed, accum, workspace)
+  if (gdt == UVA_DT_BF16 && xdt == UVA_DT_BF16) AB(bf16, bf16);
+  else if (gdt == UVA_DT_BF16) AB(bf16, float);
+  else if (xdt == UVA_DT_BF16) AB(float, bf16);
+  else AB(float, float);
+#undef AB
+  UVA_LAUNCH_CHECK();
+  colsum_final_kernel<<<dim3((cols + 31) / 32), 256, 0, s>>>(workspace, nch, cols, dbias, accum_bias);
+  UVA_LAUNCH_CHECK();
+  return 0;
+}
+
+// vectorized tall column sum (uva_colsum fast path): returns 1 if handled
+int uva_colsum_vec(int dtype, const void* in, long long ld, float* out, int rows, int cols, int accum,
+                   float* workspace, hipStream_t s) {
+  if (cols % 8 || ld % 8 || ((uintptr_t)in % 16) || !workspace || rows < 2 * COLSUM_RPB) return 0;
+  const int nch = (rows + COLSUM_RPB - 1) / COLSUM_RPB;
+  dim3 g1((cols / 8 + 31) / 32, nch);
+  if (dtype == UVA_DT_BF16)
+    act_bwd_colsum_kernel<bf16, bf16, false><<<g1, 256, 0, s>>>(nullptr, 0, (const bf16*)in, nullptr, rows, cols, ld,
+                                                                0, 0, 0, 1.f, 0, 0, workspace);
+  else
+    act_bwd_colsum_kernel<float, float, false><<<g1, 256, 0, s>>>(nullptr, 0, (const float*)in, nullptr, rows, cols,
+                                                                  ld, 0, 0, 0, 1.f, 0, 0, workspace);
+  if (hipGetLastError() != hipSuccess) return -1;
+  colsum_final_kernel<<<dim3((cols + 31) / 32), 256, 0, s>>>(workspace, nch, cols, out, accum);
+  if (hipGetLastError() != hipSuccess) return -1;
+  return 1;
+}
+
 // out = x + gate*h  backward:  dgate = dout*h ; dh = dout*gate   (gate/dgate strided by ldg)
 __global__ void gate_bwd_kernel(const float* dout, const void* h, int hdt, const void* gate, int gtdt, long long ldg,
                                 void* dh, int dhdt, void* dgate, long long rows, int cols) {

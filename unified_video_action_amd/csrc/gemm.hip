@@ -1465,12 +1465,23 @@ extern "C" long long uva_gemm_plan(int in_dtype, int ta, int tb, int M, int N, i
   return (use_v1 || (ta == 2 && gn_prologue)) ? 1 : 2;
 }
 
+extern "C" int uva_conv3x3_halo_bn(int Nimg, int H, int W, int Ci, int Co);
+extern "C" int uva_conv3x3_halo(const void* in, const void* w, void* out, const float* bias, const void* residual,
+                                int Nimg, int H, int W, int Ci, int Co, const float* gn_scale, const float* gn_shift,
+                                int gn_silu, float* gn_part, hipStream_t stream);
+
 extern "C" int uva_conv2d(int dtype, const void* in, const void* w, void* out, const float* bias, const void* residual,
                           int Nimg, int Hin, int Win, int Ci, int Co, int ks, int stride, int pad_t, int pad_l,
                           int Hout, int Wout, const float* gn_scale, const float* gn_shift, int gn_silu, int act,
                           float* gn_part, int force_generic, hipStream_t stream) {
   const int M = Nimg * Hout * Wout, K = ks * ks * Ci;
   if (M <= 0) return 0;
+  // 3x3 / s1 / p1 with 16x16-tileable maps and 64 | Ci, 128 | Co: direct halo-tile kernel (conv.hip)
+  static const int halo_mode = env_int("UVA_CONV_HALO", 1);
+  if (halo_mode && !force_generic && dtype == UVA_DT_BF16 && ks == 3 && stride == 1 && pad_t == 1 && pad_l == 1 &&
+      Hout == Hin && Wout == Win && act == ACT_NONE && uva_conv3x3_halo_bn(Nimg, Hin, Win, Ci, Co) > 0)
+    return uva_conv3x3_halo(in, w, out, bias, residual, Nimg, Hin, Win, Ci, Co, gn_scale, gn_shift, gn_silu, gn_part,
+                            stream);
   BatchStrides bs{0, 0, 0, 0, 0, 0, 1};
   EpiParams ep = make_epi(bias, residual, Co, 0, 0, nullptr, act, 1.0f, 0.0f, 0.0f, 0);
   ep.res_dt = dtype;

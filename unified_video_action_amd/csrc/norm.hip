@@ -377,9 +377,17 @@ extern "C" long long uva_layernorm_bwd_workspace(int rows, int D) {
 }
 
 // out[c] (+)= sum_r in[r*ld + c]; tall inputs go through a partial buffer (floats: ceil(rows/512)*cols)
+int uva_colsum_vec(int dtype, const void* in, long long ld, float* out, int rows, int cols, int accum,
+                   float* workspace, hipStream_t s);  // elementwise.hip
+
 extern "C" int uva_colsum(int dtype, const void* in, long long ld, float* out, int rows, int cols, int accum,
                           float* workspace, hipStream_t stream) {
   if (rows <= 0 || cols <= 0) return 0;
+  {
+    const int r = uva_colsum_vec(dtype, in, ld, out, rows, cols, accum, workspace, stream);
+    if (r < 0) return (int)hipErrorLaunchFailure;
+    if (r > 0) return 0;
+  }
   const int rpb = 512;
   int nb = (rows + rpb - 1) / rpb;
   dim3 g1((cols + 63) / 64, nb);
@@ -395,7 +403,10 @@ extern "C" int uva_colsum(int dtype, const void* in, long long ld, float* out, i
   return 0;
 }
 
-extern "C" long long uva_colsum_workspace(int rows, int cols) { return (long long)((rows + 511) / 512) * cols; }
+extern "C" long long uva_colsum_workspace(int rows, int cols) {
+  // max of the 512-row scalar path and the 128-row vectorized path (elementwise.hip COLSUM_RPB)
+  return (long long)((rows + 127) / 128) * cols;
+}
 
 extern "C" int uva_softmax_fwd(int dtype, const void* S, void* P, void* Pd, long long rows, int L, float scale,
                                float drop_p, unsigned long long seed, hipStream_t stream) {

@@ -79,9 +79,14 @@ class LinearFn(torch.autograd.Function):
         xc, weight, bias, aux = ctx.saved_tensors
         act, drop_p, seed, xdt, has_res = ctx.cfg
         M, N = g.shape
+        fused_bias = False
         if act != "none" or drop_p > 0:
             dpre = torch.empty(M, N, dtype=cdt(), device=g.device)
-            ops.act_bwd(aux, g.contiguous(), dpre, act, drop_p=drop_p, seed=seed)
+            if bias is not None and N % 8 == 0:
+                ops.act_bwd_bias(aux, g.contiguous(), dpre, grad_buf(bias), act, drop_p=drop_p, seed=seed)
+                fused_bias = True
+            else:
+                ops.act_bwd(aux, g.contiguous(), dpre, act, drop_p=drop_p, seed=seed)
         else:
             dpre = as_dtype(g, cdt())
         gx = None
@@ -90,7 +95,7 @@ class LinearFn(torch.autograd.Function):
             ops.linear_dx(dpre, compute_weight(weight), gx)
             gx = as_dtype(gx, xdt)
         ops.linear_dw(dpre, xc, grad_buf(weight))
-        if bias is not None:
+        if bias is not None and not fused_bias:
             ops.colsum(dpre, grad_buf(bias), accum=True)
         return gx, None, None, None, None, None, (g if has_res else None)
 
@@ -263,19 +268,17 @@ class BlockFn(torch.autograd.Function):
         g2 = as_dtype(g2, F32)
         # fc2 (+drop2, residual)
         dpre2 = torch.empty(M, D, dtype=c, device=dev)
-        ops.act_bwd(None, g2, dpre2, "none", drop_p=p_proj, seed=seeds[3])
+        ops.act_bwd_bias(None, g2, dpre2, grad_buf(fc2b), "none", drop_p=p_proj, seed=seeds[3])
         ops.linear_dw(dpre2, a, grad_buf(fc2w))
-        ops.colsum(dpre2, grad_buf(fc2b))
         Hd = fc1w.shape[0]
         da = torch.empty(M, Hd, dtype=c, device=dev)
         ops.linear_dx(dpre2, compute_weight(fc2w), da)
         del dpre2
         # fc1 (gelu + drop1)
         dpre1 = torch.empty(M, Hd, dtype=c, device=dev)
-        ops.act_bwd(pre1, da, dpre1, "gelu", drop_p=p_proj, seed=seeds[2])
+        ops.act_bwd_bias(pre1, da, dpre1, grad_buf(fc1b), "gelu", drop_p=p_proj, seed=seeds[2])
         del da
         ops.linear_dw(dpre1, h2, grad_buf(fc1w))
-        ops.colsum(dpre1, grad_buf(fc1b))
         dh2 = torch.empty(M, D, dtype=F32, device=dev)
         ops.linear_dx(dpre1, compute_weight(fc1w), dh2)
         del dpre1
@@ -285,9 +288,8 @@ class BlockFn(torch.autograd.Function):
         del dh2
         # proj (+proj_drop, residual)
         dprep = torch.empty(M, D, dtype=c, device=dev)
-        ops.act_bwd(None, g1, dprep, "none", drop_p=p_proj, seed=seeds[1])
+        ops.act_bwd_bias(None, g1, dprep, grad_buf(projb), "none", drop_p=p_proj, seed=seeds[1])
         ops.linear_dw(dprep, o, grad_buf(projw))
-        ops.colsum(dprep, grad_buf(projb))
         do = torch.empty(M, D, dtype=c, device=dev)
         ops.linear_dx(dprep, compute_weight(projw), do)
         del dprep
@@ -404,9 +406,8 @@ class AdaLNTrunkFn(torch.autograd.Function):
             da = torch.empty(R, W, dtype=c, device=dev)
             ops.linear_dx(dhm2, compute_weight(w2), da)
             dpre1 = torch.empty(R, W, dtype=c, device=dev)
-            ops.act_bwd(pre1, da, dpre1, "silu")
+            ops.act_bwd_bias(pre1, da, dpre1, grad_buf(b1), "silu")
             ops.linear_dw(dpre1, h, grad_buf(w1))
-            ops.colsum(dpre1, grad_buf(b1))
             dh = torch.empty(R, W, dtype=F32, device=dev)
             ops.linear_dx(dpre1, compute_weight(w1), dh)
             dxn = torch.empty(R, W, dtype=F32, device=dev)

@@ -184,6 +184,15 @@ def act_bwd(pre, dy, dx, act, drop_p=0.0, seed=0, accum=False):
                stream())
 
 
+def act_bwd_bias(pre, dy, dx, dbias, act, drop_p=0.0, seed=0, accum=False, accum_bias=True):
+    """act_bwd + dbias (+)= column sums of dx (one pass: the nn.Linear bias gradient)."""
+    rows, cols = dy.shape
+    ws = workspace(lib().query("uva_act_bwd_bias_workspace", rows, cols), dy.device)
+    lib().call("uva_act_bwd_bias", dt(pre) if pre is not None else F32, ptr(pre), dt(dy), ptr(dy), _ld(dy), dt(dx),
+               ptr(dx), _ld(dx), rows, cols, ACT[act], float(drop_p), int(seed) & 0xFFFFFFFFFFFFFFFF, int(accum),
+               ptr(dbias), int(accum_bias), ptr(ws), stream())
+
+
 def gate_bwd(dout, h, gate, dh, dgate):
     rows, cols = dout.shape
     lib().call("uva_gate_bwd", ptr(dout), dt(h), ptr(h), dt(gate), ptr(gate), _ld(gate), dt(dh), ptr(dh),
@@ -275,6 +284,13 @@ def _conv_call(x, w, out, Nimg, Hin, Win, Ci, Co, ks, stride, pad_t, pad_l, Hout
     lib().call("uva_conv2d", dt(x), ptr(x), ptr(w), ptr(out), ptr(bias), ptr(residual), Nimg, Hin, Win, Ci, Co, ks,
                stride, pad_t, pad_l, Hout, Wout, ptr(gn_scale), ptr(gn_shift), int(gn_silu), ACT[act], ptr(gn_part),
                int(force_generic), stream())
+
+
+def conv_fuses_gn(Nimg, H, W, Ci, Co, ks, stride, dtype=torch.bfloat16):
+    """True when uva_conv2d runs this conv on the halo kernel, which applies a GroupNorm(+SiLU)
+    prologue while staging its input tile (no separate GN-apply pass needed)."""
+    return (dtype == torch.bfloat16 and ks == 3 and stride == 1 and
+            lib().query("uva_conv3x3_halo_bn", Nimg, H, W, Ci, Co) > 0)
 
 
 def groupnorm_finalize_tiles(part, Nimg, HW, C, gamma, beta, scale, shift, eps=1e-6, tile_rows=128):

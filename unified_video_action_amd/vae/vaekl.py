@@ -154,11 +154,12 @@ class AutoencoderKL(nn.Module):
             ops.groupnorm_stats(x, n, hw, c, norm.weight.detach(), norm.bias.detach(), sc, sh, eps=norm.eps)
         return sc, sh
 
-    def _norm_act(self, x, stats, norm, n, hw, c, silu=True):
-        """GN(+SiLU) applied ONCE per element (fused path) -> (input for the next conv, prologue or None)."""
+    def _norm_act(self, x, stats, norm, n, hw, c, silu=True, in_conv=False):
+        """GN(+SiLU) applied ONCE per element (fused path) -> (input for the next conv, prologue or None).
+        in_conv: the consuming conv applies the prologue while staging its input tile (halo kernel)."""
         g = self._gn(x, stats, norm, n, hw, c)
-        if not self._fused():
-            return x, g  # fp32 path: apply inside the conv A-loader
+        if not self._fused() or in_conv:
+            return x, g  # fp32 path: apply inside the conv A-loader; halo path: inside the halo staging
         y = torch.empty_like(x)
         ops.groupnorm_apply(x, g[0], g[1], y, n, hw, c, silu)
         return y, None
@@ -183,9 +184,11 @@ class AutoencoderKL(nn.Module):
 
     def _resblock(self, P, name, blk, x, xs_stats, n, H, W):
         c_in, c_out = blk.in_channels, blk.out_channels
-        a, g1 = self._norm_act(x, xs_stats, blk.norm1, n, H * W, c_in)
+        halo1 = self._fused() and ops.conv_fuses_gn(n, H, W, c_in, c_out, 3, 1)
+        halo2 = self._fused() and ops.conv_fuses_gn(n, H, W, c_out, c_out, 3, 1)
+        a, g1 = self._norm_act(x, xs_stats, blk.norm1, n, H * W, c_in, in_conv=halo1)
         h, _, _, hs = self._conv(P, name + ".conv1", a, n, H, W, gn=g1, stats=True)
-        a2, g2 = self._norm_act(h, hs, blk.norm2, n, H * W, c_out)
+        a2, g2 = self._norm_act(h, hs, blk.norm2, n, H * W, c_out, in_conv=halo2)
         xs = self._conv(P, name + ".nin_shortcut", x, n, H, W)[0] if c_in != c_out else x
         out, _, _, os_ = self._conv(P, name + ".conv2", a2, n, H, W, gn=g2, residual=xs, stats=True)
         return out, os_
