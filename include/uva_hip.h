@@ -78,6 +78,10 @@ int uva_conv3x3_halo_bn(int Nimg, int H, int W, int Ci, int Co);
 int uva_conv3x3_halo(const void* in, const void* w, void* out, const float* bias, const void* residual, int Nimg,
                      int H, int W, int Ci, int Co, const float* gn_scale, const float* gn_shift, int gn_silu,
                      float* gn_part, hipStream_t stream);
+/* Encoder.conv_in (vaekl.py:246-249) on the 8-channel padded frame -> 128 channels, bf16, bias, optional
+ * fused GN partials; H, W % 16 == 0.  uva_conv2d routes Ci == 8, Co == 128 3x3/s1/p1 here. */
+int uva_conv_in8(const void* in, const void* w, void* out, const float* bias, int Nimg, int H, int W,
+                 float* gn_part, hipStream_t stream);
 /* gn_part (bf16 MFMA path): the epilogue also writes per-(128-row tile, group) (sum, sumsq) of
  * the stored output for the NEXT GroupNorm(32) -> uva_groupnorm_finalize_tiles.  Needs
  * (Hout*Wout) % 128 == 0, Co % 32 == 0; buffer [M/128][32][2] floats. */

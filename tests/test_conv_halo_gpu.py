@@ -66,3 +66,32 @@ def test_conv_halo_eligibility():
     assert not ops.conv_fuses_gn(256, 256, 256, 8, 128, 3, 1)   # conv_in: Ci % 64
     assert not ops.conv_fuses_gn(256, 256, 256, 128, 128, 3, 2)  # downsample
     assert not ops.conv_fuses_gn(4, 24, 24, 128, 128, 3, 1)     # 16 does not tile 24
+
+
+@pytest.mark.parametrize("n,H,W", [(3, 32, 48), (1, 256, 256)])
+def test_conv_in8_matches_torch(n, H, W):
+    """Encoder.conv_in on the 8-channel padded frame (channels 3..7 zero, as uva_resize_select writes)."""
+    from unified_video_action_amd.native import ops
+    torch.manual_seed(5 + H)
+    x = torch.zeros(n, H, W, 8, device=DEV)
+    x[..., :3] = torch.rand(n, H, W, 3, device=DEV) * 2 - 1
+    x = x.to(torch.bfloat16)
+    w = torch.zeros(128, 3, 3, 8, device=DEV)
+    w[..., :3] = torch.randn(128, 3, 3, 3, device=DEV) * 0.2
+    w = w.to(torch.bfloat16)
+    bias = torch.randn(128, device=DEV) * 0.1
+    out = torch.empty(n, H, W, 128, device=DEV, dtype=torch.bfloat16)
+    part = torch.empty(n * H * W // 128, 32, 2, device=DEV)
+    ops.conv2d(x, w, out, n, H, W, 8, 128, 3, 1, 1, 1, H, W, bias=bias, gn_part=part)
+    ref = F.conv2d(x.float().permute(0, 3, 1, 2), w.float().permute(0, 3, 1, 2), bias, padding=1).permute(0, 2, 3, 1)
+    assert rel_err(out.float(), ref) < 1e-2
+    gamma = torch.ones(128, device=DEV)
+    beta = torch.zeros(128, device=DEV)
+    gsc = torch.empty(n, 128, device=DEV)
+    gsh = torch.empty(n, 128, device=DEV)
+    ops.groupnorm_finalize_tiles(part, n, H * W, 128, gamma, beta, gsc, gsh, eps=1e-6)
+    o = out.double().reshape(n, H * W, 32, 4)
+    mean = o.mean(dim=(1, 3))
+    rstd = (o.var(dim=(1, 3), unbiased=False) + 1e-6).rsqrt()
+    assert rel_err(gsc, rstd.repeat_interleave(4, dim=1)) < 1e-4
+    assert rel_err(gsh, -mean.repeat_interleave(4, dim=1) * rstd.repeat_interleave(4, dim=1)) < 1e-4

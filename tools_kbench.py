@@ -65,6 +65,12 @@ if __name__ == "__main__" and len(sys.argv) == 1:
 
 def conv_bench():
     dev = "cuda"
+    x = torch.rand(256, 256, 256, 8, device=dev).to(torch.bfloat16)
+    w = (torch.randn(128, 3, 3, 8, device=dev) * 0.05).to(torch.bfloat16)
+    out = torch.empty(256, 256, 256, 128, device=dev, dtype=torch.bfloat16)
+    part = torch.empty(256 * 256 * 256 // 128, 32, 2, device=dev)
+    t = timeit(lambda: ops.conv2d(x, w, out, 256, 256, 256, 8, 128, 3, 1, 1, 1, 256, 256, gn_part=part), iters=5)
+    print(f"conv_in n256 256x256 Ci8 Co128: {t:.3f} ms, output stream {out.numel() * 2 / t / 1e6:.0f} GB/s")
     for (n, H, Ci, Co) in ((256, 256, 128, 128), (256, 128, 128, 128), (256, 64, 256, 256), (256, 16, 512, 512)):
         x = torch.randn(n, H, H, Ci, device=dev).to(torch.bfloat16)
         w = (torch.randn(Co, 3, 3, Ci, device=dev) * 0.05).to(torch.bfloat16)

@@ -11,7 +11,10 @@
 //     loaded to registers at tap 0, normalised + SiLU'd (zero padding applied AFTER the
 //     activation, as F.conv2d pads the activated tensor) and written to the other halo buffer
 //     at tap 8 -- every input element is read from HBM/L2 once per chunk instead of 9x
-//     (implicit-GEMM im2col) and the GroupNorm output never round-trips through HBM;
+//     (implicit-GEMM im2col).  The GN prologue is supported, but its VALU work is not hidden
+//     under the MFMAs (level-0 conv 8.8 ms fused vs 5.5 ms + 1.6 ms separate apply pass; a
+//     variant streaming one activated round per tap between the MFMA k-steps measured 10.9 ms),
+//     so the VAE runs this kernel on pre-activated inputs (vae/vaekl.py _resblock);
 //   * the weight tile of each (chunk, tap) step -- BN rows x 64 k -- is staged by LDS-DMA
 //     (global_load_lds, 16 B/lane) one step ahead into a 2-deep ring;
 //   * A fragments (16 pixels of one tile row x 32 channels) are read from the halo image at
@@ -312,6 +315,139 @@ extern "C" int uva_conv3x3_halo(const void* in, const void* w, void* out, const 
   if (gn_scale) CH_LAUNCH(128, true);
   else CH_LAUNCH(128, false);
 #undef CH_LAUNCH
+  UVA_LAUNCH_CHECK();
+  return 0;
+}
+
+// =====================================================================================
+// conv_in: 3x3 / s1 / p1 from the 8-channel padded RGB frame (vaekl.py:246-249 Encoder.conv_in,
+// Ci = 3 zero-padded to 8 by uva_resize_select) to Co = 128.  K = 9 taps x 8 = 72 -> three
+// 16x16x32 MFMA k-steps (k-group = one tap; taps 9..11 are zero).  The op is bound by its
+// 16.8 MB/image bf16 output stream, so the kernel is built around the store:
+//   * transposed product D^T = W . X^T: rows = output channels, so each lane's accumulator
+//     holds 4 CONSECUTIVE channels = exactly one GroupNorm(32) group of one pixel;
+//   * the 16 x 16 x 8 input tile + halo (5 KB) is staged once in LDS; weights live in registers;
+//   * per 16-pixel row: 24 MFMAs, bias, bf16, GN partial sums, then the 16 px x 128 ch tile goes
+//     through a per-wave LDS slab so the global stores are 4 fully contiguous 1-KiB wave stores.
+// =====================================================================================
+__global__ __launch_bounds__(256) void conv_in_kernel(const bf16* __restrict__ in, const bf16* __restrict__ wt,
+                                                      const float* __restrict__ bias, bf16* __restrict__ out,
+                                                      float* __restrict__ gn_part, int Nimg, int H, int W) {
+  __shared__ __attribute__((aligned(16))) bf16 sx[CH_HPIX * 8];
+  __shared__ __attribute__((aligned(16))) bf16 slab[4][16 * 128];
+  __shared__ float red[4][32][2];
+  const int tiles_x = W / CH_T, tiles_y = H / CH_T;
+  const int sp = blockIdx.x;
+  const int tx = sp % tiles_x, ty = (sp / tiles_x) % tiles_y, n = sp / (tiles_x * tiles_y);
+  const int oh0 = ty * CH_T, ow0 = tx * CH_T;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int frow = lane & 15, fk = lane >> 4;
+  // halo: 324 pixels x 16 B
+  for (int p = tid; p < CH_HPIX; p += 256) {
+    const int hy = p / CH_H, hx = p - hy * CH_H;
+    const int ih = oh0 - 1 + hy, iw = ow0 - 1 + hx;
+    bf16x8 v = (bf16x8){};
+    if (ih >= 0 && ih < H && iw >= 0 && iw < W) v = *(const bf16x8*)(in + (((long long)n * H + ih) * W + iw) * 8);
+    *(bf16x8*)(sx + p * 8) = v;
+  }
+  // weights [128][72] -> A fragments (row = channel f*16 + frow, k-group = tap ks*4 + fk)
+  bf16x8 wf[8][3];
+#pragma unroll
+  for (int f = 0; f < 8; ++f)
+#pragma unroll
+    for (int ks = 0; ks < 3; ++ks) {
+      const int tap = ks * 4 + fk;
+      wf[f][ks] = tap < 9 ? *(const bf16x8*)(wt + (f * 16 + frow) * 72 + tap * 8) : (bf16x8){};
+    }
+  float bv[8][4];
+#pragma unroll
+  for (int f = 0; f < 8; ++f)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) bv[f][r] = bias ? bias[f * 16 + fk * 4 + r] : 0.f;
+  __syncthreads();
+  float gs[8], gq[8];
+#pragma unroll
+  for (int f = 0; f < 8; ++f) gs[f] = gq[f] = 0.f;
+  bf16* myslab = slab[wid];
+#pragma unroll 1
+  for (int rr = 0; rr < 4; ++rr) {
+    const int row = wid * 4 + rr;  // tile row
+    bf16x8 xf[3];
+#pragma unroll
+    for (int ks = 0; ks < 3; ++ks) {
+      const int tap = ks * 4 + fk;
+      const int kh = tap / 3, kw = tap % 3;
+      xf[ks] = tap < 9 ? *(const bf16x8*)(sx + ((row + kh) * CH_H + frow + kw) * 8) : (bf16x8){};
+    }
+    f32x4 acc[8];
+#pragma unroll
+    for (int f = 0; f < 8; ++f) {
+      acc[f] = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ks = 0; ks < 3; ++ks) acc[f] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[f][ks], xf[ks], acc[f], 0, 0, 0);
+    }
+    // acc[f][r] = out[pixel frow][channel f*16 + fk*4 + r]
+#pragma unroll
+    for (int f = 0; f < 8; ++f) {
+      bf16x4 o;
+      float s = 0.f, q = 0.f;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        o[r] = (bf16)(acc[f][r] + bv[f][r]);
+        const float v = (float)o[r];
+        s += v;
+        q += v * v;
+      }
+      gs[f] += s;
+      gq[f] += q;
+      *(bf16x4*)(myslab + frow * 128 + f * 16 + fk * 4) = o;
+    }
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): slab writes done (wave-private slab)
+    __builtin_amdgcn_wave_barrier();
+    const long long ob = (((long long)n * H + oh0 + row) * W + ow0) * 128;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int e = (i * 64 + lane) * 8;  // 16 px x 128 ch contiguous in NHWC
+      *(bf16x8*)(out + ob + e) = *(const bf16x8*)(myslab + e);
+    }
+    __builtin_amdgcn_wave_barrier();
+  }
+  if (gn_part) {
+    // group g = f*4 + fk: reduce over the 16 pixel lanes sharing fk
+#pragma unroll
+    for (int f = 0; f < 8; ++f) {
+#pragma unroll
+      for (int o = 1; o < 16; o <<= 1) {
+        gs[f] += __shfl_xor(gs[f], o, 64);
+        gq[f] += __shfl_xor(gq[f], o, 64);
+      }
+    }
+    if (frow == 0) {
+#pragma unroll
+      for (int f = 0; f < 8; ++f) {
+        red[wid][f * 4 + fk][0] = gs[f];
+        red[wid][f * 4 + fk][1] = gq[f];
+      }
+    }
+    __syncthreads();
+    if (tid < 64) {
+      const int half = tid >> 5, g = tid & 31;  // half 0 = waves 0,1 (tile rows 0-7)
+      const float s = red[half * 2][g][0] + red[half * 2 + 1][g][0];
+      const float q = red[half * 2][g][1] + red[half * 2 + 1][g][1];
+      const long long t128 = ((long long)n * tiles_x * tiles_y + (sp % (tiles_x * tiles_y))) * 2 + half;
+      gn_part[(t128 * 32 + g) * 2 + 0] = s;
+      gn_part[(t128 * 32 + g) * 2 + 1] = q;
+    }
+  }
+}
+
+extern "C" int uva_conv_in8(const void* in, const void* w, void* out, const float* bias, int Nimg, int H, int W,
+                            float* gn_part, hipStream_t stream) {
+  if (Nimg <= 0) return 0;
+  if (H % CH_T || W % CH_T || (((uintptr_t)in | (uintptr_t)w | (uintptr_t)out) % 16)) return (int)hipErrorInvalidValue;
+  const long long nblk = (long long)Nimg * (H / CH_T) * (W / CH_T);
+  conv_in_kernel<<<dim3((unsigned)nblk), 256, 0, stream>>>((const bf16*)in, (const bf16*)w, bias, (bf16*)out, gn_part,
+                                                           Nimg, H, W);
   UVA_LAUNCH_CHECK();
   return 0;
 }

@@ -322,6 +322,23 @@ __device__ __forceinline__ void epi_row8(TC* __restrict__ C, long long cbase, co
                                            : ((const float*)ep.residual)[ri + e];
     }
   }
+  float bv[8], gv[8];
+  if (ep.bias) {
+    const float4 b0 = *(const float4*)(ep.bias + col0), b1 = *(const float4*)(ep.bias + col0 + 4);
+    bv[0] = b0.x; bv[1] = b0.y; bv[2] = b0.z; bv[3] = b0.w; bv[4] = b1.x; bv[5] = b1.y; bv[6] = b1.z; bv[7] = b1.w;
+  }
+  if (ep.gate) {
+    const long long gi = (long long)row * ep.ldg + col0;
+    if (ep.gate_dt == UVA_DT_BF16 && gi % 8 == 0) {
+      const bf16x8 g8 = *(const bf16x8*)((const bf16*)ep.gate + gi);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) gv[e] = (float)g8[e];
+    } else {
+#pragma unroll
+      for (int e = 0; e < 8; ++e)
+        gv[e] = ep.gate_dt == UVA_DT_BF16 ? (float)((const bf16*)ep.gate)[gi + e] : ((const float*)ep.gate)[gi + e];
+    }
+  }
   bool keep[8] = {true, true, true, true, true, true, true, true};
   if (ep.drop_thresh) {
     const uint64_t d0 = (uint64_t)((long long)z * M * N + (long long)row * N + col0);
@@ -333,21 +350,45 @@ __device__ __forceinline__ void epi_row8(TC* __restrict__ C, long long cbase, co
       for (int e = 0; e < 8; ++e) keep[e] = dropout_keep(ep.drop_seed, d0 + e, ep.drop_thresh);
     }
   }
+  float x[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) x[e] = ep.alpha * v[e] + (ep.bias ? bv[e] : 0.f);
+  if (ep.aux) {  // pre-activation copy, one 16-B (bf16) / 2 x 16-B (fp32) store
+    if constexpr (sizeof(TC) == 2) {
+      bf16x8 av;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) av[e] = (bf16)x[e];
+      *(bf16x8*)((TC*)ep.aux + cbase) = av;
+    } else {
+      *(float4*)((TC*)ep.aux + cbase) = make_float4(x[0], x[1], x[2], x[3]);
+      *(float4*)((TC*)ep.aux + cbase + 4) = make_float4(x[4], x[5], x[6], x[7]);
+    }
+  }
+  // activation: one uniform branch per row segment, not per element
+  switch (ep.act) {
+    case ACT_GELU:
+#pragma unroll
+      for (int e = 0; e < 8; ++e) x[e] = gelu_erf(x[e]);
+      break;
+    case ACT_SILU:
+#pragma unroll
+      for (int e = 0; e < 8; ++e) x[e] = silu(x[e]);
+      break;
+    case ACT_RELU:
+#pragma unroll
+      for (int e = 0; e < 8; ++e) x[e] = x[e] > 0.f ? x[e] : 0.f;
+      break;
+    default:
+      break;
+  }
 #pragma unroll
   for (int e = 0; e < 8; ++e) {
-    const int col = col0 + e;
-    float x = ep.alpha * v[e];
-    if (ep.bias) x += ep.bias[col];
-    if (ep.aux) ((TC*)ep.aux)[cbase + e] = from_f32<TC>(x);
-    x = apply_act(ep.act, x);
-    if (ep.drop_thresh) x = keep[e] ? x * ep.drop_scale : 0.f;
-    if (ep.gate) {
-      long long gi = (long long)row * ep.ldg + col;
-      x *= ep.gate_dt == UVA_DT_BF16 ? (float)((const bf16*)ep.gate)[gi] : ((const float*)ep.gate)[gi];
-    }
-    if (ep.residual) x += resv[e];
-    if (ep.beta != 0.f) x += ep.beta * prev[e];
-    o[e] = x;
+    float t = x[e];
+    if (ep.drop_thresh) t = keep[e] ? t * ep.drop_scale : 0.f;
+    if (ep.gate) t *= gv[e];
+    if (ep.residual) t += resv[e];
+    if (ep.beta != 0.f) t += ep.beta * prev[e];
+    o[e] = t;
   }
   if constexpr (sizeof(TC) == 2) {
     bf16x8 ov;
@@ -1470,6 +1511,9 @@ extern "C" int uva_conv3x3_halo(const void* in, const void* w, void* out, const 
                                 int Nimg, int H, int W, int Ci, int Co, const float* gn_scale, const float* gn_shift,
                                 int gn_silu, float* gn_part, hipStream_t stream);
 
+extern "C" int uva_conv_in8(const void* in, const void* w, void* out, const float* bias, int Nimg, int H, int W,
+                            float* gn_part, hipStream_t stream);
+
 extern "C" int uva_conv2d(int dtype, const void* in, const void* w, void* out, const float* bias, const void* residual,
                           int Nimg, int Hin, int Win, int Ci, int Co, int ks, int stride, int pad_t, int pad_l,
                           int Hout, int Wout, const float* gn_scale, const float* gn_shift, int gn_silu, int act,
@@ -1482,6 +1526,11 @@ extern "C" int uva_conv2d(int dtype, const void* in, const void* w, void* out, c
       Hout == Hin && Wout == Win && act == ACT_NONE && uva_conv3x3_halo_bn(Nimg, Hin, Win, Ci, Co) > 0)
     return uva_conv3x3_halo(in, w, out, bias, residual, Nimg, Hin, Win, Ci, Co, gn_scale, gn_shift, gn_silu, gn_part,
                             stream);
+  // the 8-channel (padded RGB) input conv: store-bound special form (conv.hip)
+  if (halo_mode && !force_generic && dtype == UVA_DT_BF16 && ks == 3 && stride == 1 && pad_t == 1 && pad_l == 1 &&
+      Hout == Hin && Wout == Win && act == ACT_NONE && Ci == 8 && Co == 128 && !residual && !gn_scale &&
+      Hin % 16 == 0 && Win % 16 == 0)
+    return uva_conv_in8(in, w, out, bias, Nimg, Hin, Win, gn_part, stream);
   BatchStrides bs{0, 0, 0, 0, 0, 0, 1};
   EpiParams ep = make_epi(bias, residual, Co, 0, 0, nullptr, act, 1.0f, 0.0f, 0.0f, 0);
   ep.res_dt = dtype;

@@ -95,16 +95,18 @@ __global__ __launch_bounds__(256) void ln_fwd(const TI* __restrict__ x, const fl
     int col0 = col_of<VEC>(c, lane, 0);
     if (col0 >= D) continue;
     float o[VEC];
-    float sc[VEC], sh[VEC];
+    float sc[VEC], sh[VEC], wv[VEC], bv[VEC];
     if (scale) {
       ldv<VEC>(scale + (long long)row * ldm + col0, sc);
       ldv<VEC>(shift + (long long)row * ldm + col0, sh);
     }
+    if (w) ldv<VEC>(w + col0, wv);  // vector loads: per-element scalar loads were issue-bound
+    if (b) ldv<VEC>(b + col0, bv);
 #pragma unroll
     for (int i = 0; i < VEC; ++i) {
       float h = (v[c][i] - mean) * rstd;
-      if (w) h = h * w[col0 + i];
-      if (b) h = h + b[col0 + i];
+      if (w) h = h * wv[i];
+      if (b) h = h + bv[i];
       if (scale) h = h * (1.0f + sc[i]) + sh[i];
       o[i] = h;
     }
@@ -149,10 +151,12 @@ __global__ __launch_bounds__(256) void ln_bwd(const TI* __restrict__ x, const fl
         for (int i = 0; i < VEC; ++i) xh[c][i] = g[c][i] = 0.f;
         continue;
       }
-      float xv[VEC], dv[VEC], sc[VEC];
+      float xv[VEC], dv[VEC], sc[VEC], wv[VEC], bv[VEC];
       ldv<VEC>(x + (long long)row * D + col0, xv);
       ldv<VEC>(dy + (long long)row * D + col0, dv);
       if (scale) ldv<VEC>(scale + (long long)row * ldm + col0, sc);
+      if (w) ldv<VEC>(w + col0, wv);
+      if (b) ldv<VEC>(b + col0, bv);
       float ds[VEC], dsh[VEC];
 #pragma unroll
       for (int i = 0; i < VEC; ++i) {
@@ -160,7 +164,7 @@ __global__ __launch_bounds__(256) void ln_bwd(const TI* __restrict__ x, const fl
         // y_aff = xhat*w + b ; h = y_aff*(1+scale) + shift (modulated) or h = y_aff
         float da = dv[i];
         if (scale) {
-          float ya = w ? xh[c][i] * w[col0 + i] + (b ? b[col0 + i] : 0.f) : xh[c][i];
+          float ya = w ? xh[c][i] * wv[i] + (b ? bv[i] : 0.f) : xh[c][i];
           da = dv[i] * (1.0f + sc[i]);
           ds[i] = dv[i] * ya;
           dsh[i] = dv[i];
@@ -168,7 +172,7 @@ __global__ __launch_bounds__(256) void ln_bwd(const TI* __restrict__ x, const fl
         if (w) {
           pw[c][i] += da * xh[c][i];
           pb[c][i] += da;
-          g[c][i] = da * w[col0 + i];
+          g[c][i] = da * wv[i];
         } else {
           g[c][i] = da;
         }
