@@ -18,4 +18,4 @@ def test_workspace_queries_are_pure_host():
     from unified_video_action_amd.native.lib import lib
     L = lib()
     assert L.query("uva_layernorm_bwd_workspace", 1000, 768) == 16 * 768 * 2
-    assert L.query("uva_colsum_workspace", 1024, 10) == 2 * 10
+    assert L.query("uva_colsum_workspace", 1024, 10) == 8 * 10  # one partial row per 128-row slab
