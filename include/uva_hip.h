@@ -153,13 +153,19 @@ int uva_adamw_ema(float* p, const float* g, float* m, float* v, float* ema, void
                   float ema_decay, hipStream_t stream);
 
 /* ---- fused attention, head_dim 64, bf16 (timm Attention / SDPA with attn dropout,
- *      mar_con_unified.py:201-249).  qkv: [B,N,3,H,64] (the qkv GEMM output), out/dout:
- *      [B,N,H,64], lse2: [B,H,N] log2-domain row log-sum-exp, Dvec: [B,H,N] workspace,
- *      dqkv: [B,N,3,H,64].  N % 64 == 0.  dropout = counter hash (p, seed). */
-int uva_attn_fwd(const void* qkv, void* out, float* lse2, int B, int N, int H, float scale, float drop_p,
-                 unsigned long long seed, hipStream_t stream);
-int uva_attn_bwd(const void* qkv, const void* out, const void* dout, const float* lse2, float* Dvec, void* dqkv,
-                 int B, int N, int H, float scale, float drop_p, unsigned long long seed, hipStream_t stream);
+ *      mar_con_unified.py:201-249 -> timm 0.9.7 Attention.forward, F.scaled_dot_product_attention).
+ *      qkv: [B,N,3,H,64] (the qkv GEMM output), out/dout: [B,N,H,64], lse2: [B,H,N] log2-domain
+ *      row log-sum-exp, Dvec: [B,H,N] scratch, dqkv: [B,N,3,H,64].  N % 64 == 0.
+ * uva_attn_dropmask: keep-mask bit planes (uva_attn_mask_bytes bytes) of the counter-hash
+ *      dropout (p, seed) -- generated once per step, consumed by fwd and bwd (drop_p > 0).
+ * uva_attn_bwd: workspace of uva_attn_bwd_workspace bytes (dO/(1-p) when drop_p > 0, else none). */
+long long uva_attn_mask_bytes(int B, int N, int H);
+long long uva_attn_bwd_workspace(int B, int N, int H, float drop_p);
+int uva_attn_dropmask(void* mask, int B, int N, int H, float drop_p, unsigned long long seed, hipStream_t stream);
+int uva_attn_fwd(const void* qkv, void* out, float* lse2, const void* mask, int B, int N, int H, float scale,
+                 float drop_p, hipStream_t stream);
+int uva_attn_bwd(const void* qkv, const void* out, const void* dout, const float* lse2, const void* mask, float* Dvec,
+                 void* dqkv, void* workspace, int B, int N, int H, float scale, float drop_p, hipStream_t stream);
 
 /* ---- KL-VAE encoder plumbing (vae/vaekl.py, utils/data_utils.py) ---------------------
  * uva_resize_select: obs image [B,T,3,Hin,Win] fp32 in [0,1] -> NHWC [B*nsel,256,256,Cpad]

@@ -57,16 +57,8 @@ def test_flash_rescale_branch_forced():
     assert rel_err(out.float(), ref) < 2e-2
 
 
-def test_flash_dropout_matches_materialised_path():
+def _materialised_keep(qkv, B, N, H, p, seed):
     from unified_video_action_amd.native import ops
-    torch.manual_seed(1)
-    B, N, H, p, seed = 1, 256, 2, 0.1, 777
-    qkv = torch.randn(B, N, 3 * H * 64, device=DEV).to(torch.bfloat16)
-    out = torch.empty(B, N, H * 64, device=DEV, dtype=torch.bfloat16)
-    lse = torch.empty(B, H, N, device=DEV)
-    ops.attn_fwd(qkv, out, lse, B, N, H, 0.125, drop_p=p, seed=seed)
-    # materialised: S = Q K^T (fp32), P = softmax, Pd = dropout(P) with the same hash
-    q = qkv.float().view(B, N, 3, H, 64)
     ld = 3 * H * 64
     qf = qkv.float()
     S = torch.empty(B, H, N, N, device=DEV)
@@ -75,6 +67,50 @@ def test_flash_dropout_matches_materialised_path():
     P = torch.empty_like(S)
     Pd = torch.empty_like(S)
     ops.softmax_fwd(S, P, Pd, N, 0.125, drop_p=p, seed=seed)
+    return Pd
+
+
+def _mask_pos(k):
+    return ((k >> 2) & 3) * 16 + (k >> 4) * 4 + (k & 3)
+
+
+@pytest.mark.parametrize("B,N,H", [(1, 256, 2), (1, 1088, 1)])
+def test_dropmask_planes_match_counter_hash(B, N, H):
+    """MQ/MK bit planes == the keep pattern of the materialised softmax (same counter hash)."""
+    from unified_video_action_amd.native import ops
+    p, seed = 0.1, 4242
+    torch.manual_seed(3)
+    qkv = torch.randn(B, N, 3 * H * 64, device=DEV).to(torch.bfloat16)
+    keep = (_materialised_keep(qkv, B, N, H, p, seed) != 0)  # [B,H,N,N]
+    mask = ops.attn_dropmask(B, N, H, p, seed, DEV)
+    nt = N // 64
+    words = mask.view(torch.int64)
+    mq = words[:B * H * nt * N].view(B * H, nt, N)
+    mk = words[B * H * nt * N:].view(B * H, nt, N)
+    pos = torch.tensor([_mask_pos(k) for k in range(64)], device=DEV)
+    # MQ[bh][kv][q] bit pos(k) <-> key kv*64+k
+    bq = (mq.unsqueeze(-1) >> pos) & 1                              # [BH, kv, q, k]
+    bq = bq.permute(0, 2, 1, 3).reshape(B * H, N, N).bool()         # [BH, q, key]
+    assert torch.equal(bq, keep.view(B * H, N, N))
+    # MK[bh][qb][key] bit pos(j) <-> query qb*64+j
+    bk = (mk.unsqueeze(-1) >> pos) & 1                              # [BH, qb, key, j]
+    bk = bk.permute(0, 1, 3, 2).reshape(B * H, N, N).bool()         # [BH, q, key]
+    assert torch.equal(bk, keep.view(B * H, N, N))
+    assert abs(keep.float().mean().item() - 0.9) < 0.01
+
+
+@pytest.mark.parametrize("B,N,H", [(1, 256, 2), (1, 1088, 2)])
+def test_flash_dropout_matches_materialised_path(B, N, H):
+    from unified_video_action_amd.native import ops
+    torch.manual_seed(1)
+    p, seed = 0.1, 777
+    qkv = torch.randn(B, N, 3 * H * 64, device=DEV).to(torch.bfloat16)
+    out = torch.empty(B, N, H * 64, device=DEV, dtype=torch.bfloat16)
+    lse = torch.empty(B, H, N, device=DEV)
+    ops.attn_fwd(qkv, out, lse, B, N, H, 0.125, drop_p=p, seed=seed)
+    # materialised: S = Q K^T (fp32), P = softmax, Pd = dropout(P) with the same hash
+    q = qkv.float().view(B, N, 3, H, 64)
+    Pd = _materialised_keep(qkv, B, N, H, p, seed)
     keep = (Pd != 0).float()
     assert abs(keep.mean().item() - 0.9) < 0.01
     ref = (Pd @ q[:, :, 2].permute(0, 2, 1, 3)).transpose(1, 2).reshape(B, N, H * 64)

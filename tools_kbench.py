@@ -18,10 +18,10 @@ def timeit(fn, iters=20):
     return s.elapsed_time(e) / iters
 
 
-def main():
+def main(attn_only=False):
     dev = "cuda"
     M = 32 * 1024
-    for (N, K) in ((2304, 768), (768, 768), (3072, 768), (768, 3072)):
+    for (N, K) in () if attn_only else ((2304, 768), (768, 768), (3072, 768), (768, 3072)):
         x = torch.randn(M, K, device=dev).to(torch.bfloat16)
         w = torch.randn(N, K, device=dev).to(torch.bfloat16)
         y = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
@@ -43,10 +43,12 @@ def main():
     dvec = torch.empty(B, H, N, device=dev)
     fl = 4 * B * H * N * N * 64
     for p in (0.0, 0.1):
-        t1 = timeit(lambda: ops.attn_fwd(qkv, out, lse, B, N, H, 0.125, p, 1))
-        t2 = timeit(lambda: ops.attn_bwd(qkv, out, out, lse, dvec, dqkv, B, N, H, 0.125, p, 1))
-        print(f"attn B={B} N={N} H={H} p={p}: fwd {t1:.3f} ms {fl/t1/1e9:.0f} TF, bwd {t2:.3f} ms "
-              f"{2.5*fl/t2/1e9:.0f} TF(alg)")
+        mask = ops.attn_dropmask(B, N, H, p, 1, dev) if p > 0 else None
+        tm = timeit(lambda: ops.attn_dropmask(B, N, H, p, 1, dev)) if p > 0 else 0.0
+        t1 = timeit(lambda: ops.attn_fwd(qkv, out, lse, B, N, H, 0.125, p, 1, mask=mask))
+        t2 = timeit(lambda: ops.attn_bwd(qkv, out, out, lse, dvec, dqkv, B, N, H, 0.125, p, 1, mask=mask))
+        print(f"attn B={B} N={N} H={H} p={p}: mask {tm:.3f} ms, fwd {t1:.3f} ms {fl/t1/1e9:.0f} TF, bwd {t2:.3f} ms "
+              f"{2*fl/t2/1e9:.0f} TF(alg 8N^2d)")
     q = qkv.view(B, N, 3, H, 64).permute(2, 0, 3, 1, 4)
     ts = timeit(lambda: torch.nn.functional.scaled_dot_product_attention(q[0], q[1], q[2]))
     print(f"torch sdpa fwd {ts:.3f} ms {fl/ts/1e9:.0f} TF")
@@ -61,6 +63,8 @@ def main():
 
 if __name__ == "__main__" and len(sys.argv) == 1:
     main()
+if __name__ == "__main__" and sys.argv[1:] == ["attn"]:
+    main(attn_only=True)
 
 
 def conv_bench():

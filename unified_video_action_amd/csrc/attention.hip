@@ -3,20 +3,34 @@
 // dropout_p = attn_drop while training).  Reads Q/K/V straight from the qkv GEMM output
 // [B, N, 3, H, 64] and writes O as [B, N, H, 64] (the proj GEMM input) -- no permutes.
 //
-// Layout trick (CDNA4 v_mfma_f32_16x16x32_bf16, 64-lane waves): scores are computed
+// Layout trick (CDNA4 v_mfma_f32_16x16x32_bf16, 64-lane waves): forward scores are computed
 // transposed, S^T = K Q^T, so each lane owns one query column (lane & 15) and 16 keys in
 // registers.  P^T then feeds O^T = V^T P^T directly as the B operand (no LDS round trip):
 // the k order inside each 32-deep step is the permutation pi(8g+j) = tileA*16+4g+j (j<4),
 // tileB*16+4g+j-4 (j>=4), matched on the V side by choosing the row bases of the two
-// ds_read_b64_tr_b16 transposed reads.  Softmax statistics are per lane (query), so the
-// O^T rescale needs no shuffles.  K/V tiles (64 keys) are register-staged into
-// double-buffered LDS ([row][72] bf16 images serve both row and transposed reads).
+// ds_read_b64_tr_b16 transposed reads.  Softmax statistics are per lane (query); the O^T
+// rescale is lazy (only when a row max grows by > 2^8, wave-uniform branch) and the row sum
+// stays lane-partial until the epilogue.
 //
-// Backward (FA2 recompute, two kernels, no atomics):
-//   attn_bwd_dkdv : block = 128 keys, sweeps all query tiles -> dK, dV
-//   attn_bwd_dq   : block = 128 queries, sweeps all key tiles -> dQ
-// Dropout keep-mask = counter hash of ((b*H+h)*N + q)*N + key, identical in all kernels
-// and in the materialised fp32 path (norm.hip softmax kernels).
+// Dropout (attn_drop p): the keep decision of element (b,h,q,key) is the counter hash of
+// ((b*H+h)*N+q)*N+key (common.h, shared with the materialised softmax path).  One mask
+// kernel evaluates it once per step and writes two bit planes in the lane orders of the
+// MFMA kernels, so forward and backward only test bits (v_bfe_i32 + v_and per element):
+//   MQ [bh][key tile kv][q]   u64, bit g*16+kt*4+r  <-> key kv*64 + kt*16 + 4g + r
+//   MK [bh][query tile qb][key] u64, bit g*16+qt*4+r <-> query qb*64 + qt*16 + 4g + r
+// (the 16 bits a lane of quad g needs are the u16 at offset g).  MK comes from MQ's rows by
+// 64 wave ballots (lane L computes the query whose MK bit is L).
+//
+// Backward (two kernels, FA2 recompute, no atomics -> bitwise reproducible):
+//   attn_bwd_dkdv : block = 128 keys (4 waves x 32), sweeps all 64-query tiles; S and dP with
+//                   the key on the lane, so Pd and dS are already the B operands of
+//                   dV^T += dO'^T Pd and dK^T += Q^T dS (pi order).
+//   attn_bwd_dq   : block = 128 queries, sweeps all 64-key tiles (forward's lane view).
+// A fused single pass with dQ summed by fp32 atomics was measured slower at this shape: d = 64
+// gives only 640 FLOP per atomic byte, so the 0.8 GB of dQ adds per layer ran at the chip's
+// atomic rate (+0.28 ms per layer), more than the recomputed S/dP of the dQ kernel costs.
+// dO' = dO / (1 - p) is prepared by the pre kernel (with D = rowsum(dO * O)), so the dropout
+// scale costs nothing inside the loops.
 #include "common.h"
 
 #define AT_LD 72
@@ -65,17 +79,79 @@ __device__ __forceinline__ void stage_store(bf16* lds, const bf16x8 (&r)[2]) {
   }
 }
 
-__device__ __forceinline__ float drop_apply(float v, bool on, uint64_t seed, uint64_t idx, uint32_t th, float ds) {
-  if (!on) return v;
-  return dropout_keep(seed, idx, th) ? v * ds : 0.f;
+// workgroup barrier that orders LDS only: outstanding global loads / atomics stay in flight
+// (__syncthreads would drain vmcnt, i.e. wait for every dQ atomic of the tile)
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+__device__ __forceinline__ float exp2_fast(float x) { return __builtin_amdgcn_exp2f(x); }
+// keep-bit b of a mask word as an all-ones / all-zeros 32-bit mask
+__device__ __forceinline__ float keep_and(float v, uint32_t w, int b) {
+  return __int_as_float(__float_as_int(v) & __builtin_amdgcn_sbfe(w, b, 1));
+}
+// position of element k (0..63) of a 64-wide tile inside an MQ / MK word (an involution)
+__host__ __device__ constexpr int mask_pos(int k) { return ((k >> 2) & 3) * 16 + (k >> 4) * 4 + (k & 3); }
+
+// =====================================================================================
+// dropout bit planes: one wave per (bh, query tile qb, key tile kv)
+// =====================================================================================
+__global__ __launch_bounds__(256) void attn_mask_kernel(uint64_t* __restrict__ MQ, uint64_t* __restrict__ MK, int N,
+                                                        int nt, long long tasks, uint32_t th, uint64_t seed) {
+  const long long task = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (task >= tasks) return;  // wave-uniform
+  const int L = threadIdx.x & 63;
+  const int kv = (int)(task % nt);
+  const long long t2 = task / nt;
+  const int qb = (int)(t2 % nt);
+  const long long bh = t2 / nt;
+  const int q = qb * 64 + mask_pos(L);  // lane L holds the query whose MK bit is L
+  const uint32_t key = drop_key(seed);
+  const uint64_t pair0 = (((uint64_t)bh * N + q) * (uint64_t)N + (uint64_t)kv * 64) >> 1;
+  uint32_t lo = 0, hi = 0;  // MQ word of this lane's query (bit mask_pos(k) <-> key kv*64 + k)
+#pragma unroll
+  for (int j = 0; j < 32; ++j) {
+    const uint32_t hv = drop_hash(key, pair0 + j);
+    const uint32_t k0 = (hv & 0xFFFFu) >= th, k1 = (hv >> 16) >= th;
+    const int p0 = mask_pos(2 * j), p1 = mask_pos(2 * j + 1);
+    if (p0 < 32) lo |= k0 << p0; else hi |= k0 << (p0 - 32);
+    if (p1 < 32) lo |= k1 << p1; else hi |= k1 << (p1 - 32);
+  }
+  MQ[((long long)bh * nt + kv) * N + q] = ((uint64_t)hi << 32) | lo;
+  // 64x64 bit transpose across the wave (rows = lanes): afterwards lane L' holds, at bit L, the
+  // bit mask_pos(L') of lane L, i.e. keep(query with MK position L, key kv*64 + mask_pos(L')).
+  {
+    const bool up = L & 32;
+    const uint32_t r = (uint32_t)__shfl_xor((int)(up ? lo : hi), 32, 64);
+    if (up) lo = r; else hi = r;
+  }
+#define UVA_TSTAGE(J, M)                                                                    \
+  {                                                                                         \
+    const bool up = L & (J);                                                                \
+    const uint32_t sl = up ? (lo & (M)) : ((lo >> (J)) & (M));                              \
+    const uint32_t sh = up ? (hi & (M)) : ((hi >> (J)) & (M));                              \
+    const uint32_t rl = (uint32_t)__shfl_xor((int)sl, (J), 64);                             \
+    const uint32_t rh = (uint32_t)__shfl_xor((int)sh, (J), 64);                             \
+    lo = up ? ((lo & ~(M)) | rl) : ((lo & (M)) | (rl << (J)));                               \
+    hi = up ? ((hi & ~(M)) | rh) : ((hi & (M)) | (rh << (J)));                               \
+  }
+  UVA_TSTAGE(16, 0x0000FFFFu)
+  UVA_TSTAGE(8, 0x00FF00FFu)
+  UVA_TSTAGE(4, 0x0F0F0F0Fu)
+  UVA_TSTAGE(2, 0x33333333u)
+  UVA_TSTAGE(1, 0x55555555u)
+#undef UVA_TSTAGE
+  MK[((long long)bh * nt + qb) * N + (long long)kv * 64 + mask_pos(L)] = ((uint64_t)hi << 32) | lo;
 }
 
 // =====================================================================================
 // forward
 // =====================================================================================
+template <bool DROP>
 __global__ __launch_bounds__(256) void attn_fwd_kernel(const bf16* __restrict__ qkv, bf16* __restrict__ out,
-                                                       float* __restrict__ lse2, int N, int H, float scale_log2,
-                                                       uint32_t th, float dsc, uint64_t seed) {
+                                                       float* __restrict__ lse2, const uint64_t* __restrict__ MQ,
+                                                       int N, int H, float c, float dsc) {
   __shared__ __attribute__((aligned(16))) bf16 sK[2][AT_TILE];
   __shared__ __attribute__((aligned(16))) bf16 sV[2][AT_TILE];
   const int bh = blockIdx.y, b = bh / H, h = bh % H;
@@ -85,17 +161,20 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const bf16* __restrict__ 
   const bf16* Vg = Qg + 2 * H * 64;
   const int w = threadIdx.x >> 6, l = threadIdx.x & 63, g = l >> 4, li = l & 15;
   const int q0 = blockIdx.x * 128 + w * 32;
-  const bool drop = th != 0;
+  const int nkv = N / 64;
+  const uint16_t* mq = DROP ? (const uint16_t*)(MQ + (long long)bh * nkv * N) : nullptr;  // [kv][q][4 x u16]
 
   bf16x8 qf[2][2];
+  uint32_t mw[2] = {0u, 0u}, mwn[2] = {0u, 0u};
 #pragma unroll
-  for (int qt = 0; qt < 2; ++qt)
+  for (int qt = 0; qt < 2; ++qt) {
+    const int row = q0 + qt * 16 + li;
 #pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
-      int row = q0 + qt * 16 + li;
+    for (int ks = 0; ks < 2; ++ks)
       qf[qt][ks] = row < N ? *(const bf16x8*)(Qg + (long long)row * ld + ks * 32 + 8 * g) : (bf16x8){};
-    }
-  float m[2] = {-INFINITY, -INFINITY}, lsum[2] = {0.f, 0.f};
+    if (DROP) mw[qt] = row < N ? mq[(long long)row * 4 + g] : 0u;
+  }
+  float m[2] = {-INFINITY, -INFINITY}, rs[2] = {0.f, 0.f};
   f32x4 o[2][4];
 #pragma unroll
   for (int qt = 0; qt < 2; ++qt)
@@ -108,13 +187,19 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const bf16* __restrict__ 
   stage_store(sK[0], rk);
   stage_store(sV[0], rv);
   __syncthreads();
-  const int nkv = N / 64;
   int cur = 0;
   for (int kv = 0; kv < nkv; ++kv) {
     const bool more = kv + 1 < nkv;
     if (more) {
       stage_load(Kg, ld, (kv + 1) * 64, N, rk);
       stage_load(Vg, ld, (kv + 1) * 64, N, rv);
+      if (DROP) {
+#pragma unroll
+        for (int qt = 0; qt < 2; ++qt) {
+          const int row = q0 + qt * 16 + li;
+          mwn[qt] = row < N ? mq[((long long)(kv + 1) * N + row) * 4 + g] : 0u;
+        }
+      }
     }
     f32x4 s[4][2];
 #pragma unroll
@@ -131,43 +216,43 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const bf16* __restrict__ 
 #pragma unroll
         for (int qt = 0; qt < 2; ++qt) s[kt][qt] = mfma16(kf[kt], qf[qt][ks], s[kt][qt]);
     }
+    // row max (lane: 16 keys of its query; the 4 quads of a query meet through two shuffles)
+    float mx[2];
+    bool need = false;
 #pragma unroll
     for (int qt = 0; qt < 2; ++qt) {
-      float mx = -INFINITY;
+      float a = fmaxf(fmaxf(s[0][qt][0], s[0][qt][1]), fmaxf(s[0][qt][2], s[0][qt][3]));
+#pragma unroll
+      for (int kt = 1; kt < 4; ++kt)
+        a = fmaxf(a, fmaxf(fmaxf(s[kt][qt][0], s[kt][qt][1]), fmaxf(s[kt][qt][2], s[kt][qt][3])));
+      a = fmaxf(a, __shfl_xor(a, 16, 64));
+      a = fmaxf(a, __shfl_xor(a, 32, 64));
+      mx[qt] = a * c;
+      need |= mx[qt] > m[qt] + 8.0f;
+    }
+    // lazy rescale: the reference max only moves when some row grew by more than 2^8
+    if (__builtin_amdgcn_ballot_w64(need)) {
+#pragma unroll
+      for (int qt = 0; qt < 2; ++qt) {
+        const float mnew = fmaxf(m[qt], mx[qt]);
+        const float alpha = exp2_fast(m[qt] - mnew);
+        rs[qt] *= alpha;
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt) o[qt][dt] *= alpha;
+        m[qt] = mnew;
+      }
+    }
+#pragma unroll
+    for (int qt = 0; qt < 2; ++qt) {
+      const float nm = -m[qt];
 #pragma unroll
       for (int kt = 0; kt < 4; ++kt)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) mx = fmaxf(mx, s[kt][qt][r]);
-      mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
-      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-      const float mnew = fmaxf(m[qt], mx * scale_log2);
-      const float alpha = exp2f(m[qt] - mnew);
-      float rs = 0.f;
-      const long long qrow = (long long)bh * N + (q0 + qt * 16 + li);
-#pragma unroll
-      for (int kt = 0; kt < 4; ++kt) {
-#pragma unroll
         for (int r = 0; r < 4; ++r) {
-          float p = exp2f(s[kt][qt][r] * scale_log2 - mnew);
-          rs += p;
-          s[kt][qt][r] = p;
+          const float p = exp2_fast(fmaf(s[kt][qt][r], c, nm));
+          rs[qt] += p;
+          s[kt][qt][r] = DROP ? keep_and(p, mw[qt], kt * 4 + r) : p;
         }
-        if (drop) {  // lane owns 4 consecutive keys: two mask pairs
-#pragma unroll
-          for (int r = 0; r < 4; r += 2) {
-            bool k0, k1;
-            dropout_keep2(seed, (uint64_t)(qrow * N + kv * 64 + kt * 16 + 4 * g + r), th, k0, k1);
-            s[kt][qt][r] = k0 ? s[kt][qt][r] * dsc : 0.f;
-            s[kt][qt][r + 1] = k1 ? s[kt][qt][r + 1] * dsc : 0.f;
-          }
-        }
-      }
-      rs += __shfl_xor(rs, 16, 64);
-      rs += __shfl_xor(rs, 32, 64);
-      lsum[qt] = lsum[qt] * alpha + rs;
-      m[qt] = mnew;
-#pragma unroll
-      for (int dt = 0; dt < 4; ++dt) o[qt][dt] *= alpha;
     }
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
@@ -184,6 +269,7 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const bf16* __restrict__ 
     if (more) {
       stage_store(sK[cur ^ 1], rk);
       stage_store(sV[cur ^ 1], rv);
+      if (DROP) { mw[0] = mwn[0]; mw[1] = mwn[1]; }
     }
     __syncthreads();
     cur ^= 1;
@@ -191,9 +277,12 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const bf16* __restrict__ 
   const long long ldo = (long long)H * 64;
 #pragma unroll
   for (int qt = 0; qt < 2; ++qt) {
+    float lsum = rs[qt];
+    lsum += __shfl_xor(lsum, 16, 64);
+    lsum += __shfl_xor(lsum, 32, 64);
     const int q = q0 + qt * 16 + li;
     if (q >= N) continue;
-    const float inv = 1.0f / lsum[qt];
+    const float inv = dsc / lsum;
     bf16* orow = out + ((long long)b * N + q) * ldo + h * 64;
 #pragma unroll
     for (int dt = 0; dt < 4; ++dt) {
@@ -201,57 +290,87 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const bf16* __restrict__ 
                   (bf16)(o[qt][dt][3] * inv)};
       *(bf16x4*)(orow + dt * 16 + 4 * g) = v;
     }
-    if (g == 0) lse2[(long long)bh * N + q] = m[qt] + __log2f(lsum[qt]);
+    if (g == 0) lse2[(long long)bh * N + q] = m[qt] + __log2f(lsum);
   }
 }
 
-// Dvec[bh][q] = sum_d dO[q][d] * O[q][d]
+// =====================================================================================
+// backward prologue: D[bh][q] = sum_d dO*O; dO' = dO * dsc when dropping (so the keep scale
+// costs nothing in the loops).  8 lanes per (b, q, h) row of 64, 16-B loads.
+// =====================================================================================
 __global__ __launch_bounds__(256) void attn_bwd_pre_kernel(const bf16* __restrict__ out, const bf16* __restrict__ dout,
-                                                           float* __restrict__ Dvec, int B, int N, int H) {
-  const long long idx = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);  // (b, q, h)
-  const int l = threadIdx.x & 63;
-  if (idx >= (long long)B * N * H) return;
-  const int h = idx % H;
-  const long long bq = idx / H;
-  const int b = bq / N, q = bq % N;
-  float v = (float)out[idx * 64 + l] * (float)dout[idx * 64 + l];
-  v = wave_sum(v);
-  if (l == 0) Dvec[((long long)b * H + h) * N + q] = v;
+                                                           float* __restrict__ Dvec, bf16* __restrict__ dOs,
+                                                           long long rows, int N, int H, float dsc) {
+  const long long t = (long long)blockIdx.x * 256 + threadIdx.x;
+  const long long row = t >> 3;  // (b*N + q)*H + h
+  const int sub = threadIdx.x & 7;
+  const bool ok = row < rows;
+  float v = 0.f;
+  if (ok) {
+    const long long e = row * 64 + sub * 8;
+    const bf16x8 o = *(const bf16x8*)(out + e);
+    const bf16x8 d = *(const bf16x8*)(dout + e);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v += (float)o[j] * (float)d[j];
+    if (dOs) {
+      bf16x8 sc;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) sc[j] = (bf16)((float)d[j] * dsc);
+      *(bf16x8*)(dOs + e) = sc;
+    }
+  }
+  v += __shfl_xor(v, 1, 64);
+  v += __shfl_xor(v, 2, 64);
+  v += __shfl_xor(v, 4, 64);
+  if (ok && sub == 0) {
+    const int h = (int)(row % H);
+    const long long bq = row / H;
+    const long long b = bq / N, q = bq % N;
+    Dvec[(b * H + h) * N + q] = v;
+  }
 }
 
 // =====================================================================================
-// backward: dK, dV  (block = 4 waves x 32 keys)
+// backward dK, dV (block = 4 waves x 32 keys, sweeps all 64-query tiles)
+//   lane view of S / dP / Pd / dS: q = qt*16 + 4g + r, key = k0 + kt*16 + li
 // =====================================================================================
-__global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(const bf16* __restrict__ qkv, const bf16* __restrict__ dout,
-                                                            const float* __restrict__ lse2,
-                                                            const float* __restrict__ Dvec, bf16* __restrict__ dqkv,
-                                                            int N, int H, float scale, float scale_log2, uint32_t th,
-                                                            float dsc, uint64_t seed) {
+template <bool DROP>
+__global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_kernel(const bf16* __restrict__ qkv,
+                                                               const bf16* __restrict__ dOs,
+                                                               const float* __restrict__ lse2,
+                                                               const float* __restrict__ Dvec,
+                                                               const uint64_t* __restrict__ MK, bf16* __restrict__ dqkv,
+                                                               int N, int H, float scale, float c) {
   __shared__ __attribute__((aligned(16))) bf16 sQ[2][AT_TILE];
   __shared__ __attribute__((aligned(16))) bf16 sO[2][AT_TILE];
-  __shared__ float sL[2][64], sD[2][64];
+  __shared__ __attribute__((aligned(16))) float sL[2][64];
+  __shared__ __attribute__((aligned(16))) float sD[2][64];
   const int bh = blockIdx.y, b = bh / H, h = bh % H;
   const long long ld = 3LL * H * 64, ldo = (long long)H * 64;
   const bf16* Qg = qkv + (long long)b * N * ld + h * 64;
   const bf16* Kg = Qg + H * 64;
   const bf16* Vg = Qg + 2 * H * 64;
-  const bf16* dOg = dout + (long long)b * N * ldo + h * 64;
+  const bf16* dOg = dOs + (long long)b * N * ldo + h * 64;
   const float* Lg = lse2 + (long long)bh * N;
   const float* Dg = Dvec + (long long)bh * N;
   const int w = threadIdx.x >> 6, l = threadIdx.x & 63, g = l >> 4, li = l & 15;
   const int k0 = blockIdx.x * 128 + w * 32;
-  const bool drop = th != 0;
+  const int nq = N / 64;
+  const uint16_t* mk = DROP ? (const uint16_t*)(MK + (long long)bh * nq * N) : nullptr;  // [qb][key][4 x u16]
 
   bf16x8 kf[2][2], vf[2][2];
+  uint32_t mw[2] = {0u, 0u}, mwn[2] = {0u, 0u};
 #pragma unroll
-  for (int kt = 0; kt < 2; ++kt)
+  for (int kt = 0; kt < 2; ++kt) {
+    const int row = k0 + kt * 16 + li;
+    const bool ok = row < N;
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
-      int row = k0 + kt * 16 + li;
-      bool ok = row < N;
       kf[kt][ks] = ok ? *(const bf16x8*)(Kg + (long long)row * ld + ks * 32 + 8 * g) : (bf16x8){};
       vf[kt][ks] = ok ? *(const bf16x8*)(Vg + (long long)row * ld + ks * 32 + 8 * g) : (bf16x8){};
     }
+    if (DROP) mw[kt] = ok ? mk[(long long)row * 4 + g] : 0u;
+  }
   f32x4 dv[4][2], dk[4][2];
 #pragma unroll
   for (int dt = 0; dt < 4; ++dt)
@@ -265,7 +384,6 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(const bf16* __restri
   stage_store(sO[0], ro);
   if (threadIdx.x < 64) { sL[0][threadIdx.x] = Lg[threadIdx.x]; sD[0][threadIdx.x] = Dg[threadIdx.x]; }
   __syncthreads();
-  const int nq = N / 64;
   int cur = 0;
   for (int qi = 0; qi < nq; ++qi) {
     const bool more = qi + 1 < nq;
@@ -274,8 +392,15 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(const bf16* __restri
       stage_load(Qg, ld, (qi + 1) * 64, N, rq);
       stage_load(dOg, ldo, (qi + 1) * 64, N, ro);
       if (threadIdx.x < 64) { nl = Lg[(qi + 1) * 64 + threadIdx.x]; nd = Dg[(qi + 1) * 64 + threadIdx.x]; }
+      if (DROP) {
+#pragma unroll
+        for (int kt = 0; kt < 2; ++kt) {
+          const int row = k0 + kt * 16 + li;
+          mwn[kt] = row < N ? mk[((long long)(qi + 1) * N + row) * 4 + g] : 0u;
+        }
+      }
     }
-    // S[q][key] = Q K^T ; dP[q][key] = dO V^T   (lane: q = qt*16+4g+r, key = kt*16+li)
+    // S[q][key] = Q K^T ; dP'[q][key] = dO' V^T
     f32x4 s[4][2], dp[4][2];
 #pragma unroll
     for (int qt = 0; qt < 4; ++qt)
@@ -286,35 +411,33 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(const bf16* __restri
 #pragma unroll
       for (int qt = 0; qt < 4; ++qt) {
         bf16x8 a = lds_row_frag(sQ[cur], qt * 16, ks);
-        bf16x8 c = lds_row_frag(sO[cur], qt * 16, ks);
+        bf16x8 e = lds_row_frag(sO[cur], qt * 16, ks);
 #pragma unroll
         for (int kt = 0; kt < 2; ++kt) {
           s[qt][kt] = mfma16(a, kf[kt][ks], s[qt][kt]);
-          dp[qt][kt] = mfma16(c, vf[kt][ks], dp[qt][kt]);
+          dp[qt][kt] = mfma16(e, vf[kt][ks], dp[qt][kt]);
         }
       }
-    // P, dropout, dS   (s <- Pd, dp <- dS)
+    // P = exp2(S c - L);  Pd = keep P;  dS = P (keep dP' - D)      (s <- Pd, dp <- dS)
 #pragma unroll
-    for (int qt = 0; qt < 4; ++qt)
+    for (int qt = 0; qt < 4; ++qt) {
+      const f32x4 Lq = *(const f32x4*)&sL[cur][qt * 16 + 4 * g];
+      const f32x4 Dq = *(const f32x4*)&sD[cur][qt * 16 + 4 * g];
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int ql = qt * 16 + 4 * g + r;
-        const float L = sL[cur][ql], Dq = sD[cur][ql];
-        const long long qrow = (long long)bh * N + qi * 64 + ql;
+      for (int r = 0; r < 4; ++r)
 #pragma unroll
         for (int kt = 0; kt < 2; ++kt) {
-          const float p = exp2f(s[qt][kt][r] * scale_log2 - L);
+          const float p = exp2_fast(fmaf(s[qt][kt][r], c, -Lq[r]));
           float pd = p, dpt = dp[qt][kt][r];
-          if (drop) {
-            bool keep = dropout_keep(seed, (uint64_t)(qrow * N + k0 + kt * 16 + li), th);
-            pd = keep ? p * dsc : 0.f;
-            dpt = keep ? dpt * dsc : 0.f;
+          if (DROP) {
+            pd = keep_and(p, mw[kt], qt * 4 + r);
+            dpt = keep_and(dpt, mw[kt], qt * 4 + r);
           }
           s[qt][kt][r] = pd;
-          dp[qt][kt][r] = p * (dpt - Dq);
+          dp[qt][kt][r] = p * (dpt - Dq[r]);
         }
-      }
-    // dV^T[d][key] += dO^T Pd ; dK^T[d][key] += Q^T dS      (k = q, permuted by pi)
+    }
+    // dV^T[d][key] += dO'^T Pd ; dK^T[d][key] += Q^T dS      (k = q, permuted by pi)
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
       bf16x8 pb[2], sb[2];
@@ -338,8 +461,9 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(const bf16* __restri
       stage_store(sQ[cur ^ 1], rq);
       stage_store(sO[cur ^ 1], ro);
       if (threadIdx.x < 64) { sL[cur ^ 1][threadIdx.x] = nl; sD[cur ^ 1][threadIdx.x] = nd; }
+      if (DROP) { mw[0] = mwn[0]; mw[1] = mwn[1]; }
     }
-    __syncthreads();
+    lds_barrier();
     cur ^= 1;
   }
   // lane holds [d = dt*16+4g+r][key = kt*16+li]
@@ -353,21 +477,24 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(const bf16* __restri
     for (int dt = 0; dt < 4; ++dt) {
       bf16x4 a = {(bf16)(dk[dt][kt][0] * scale), (bf16)(dk[dt][kt][1] * scale), (bf16)(dk[dt][kt][2] * scale),
                   (bf16)(dk[dt][kt][3] * scale)};
-      bf16x4 c = {(bf16)dv[dt][kt][0], (bf16)dv[dt][kt][1], (bf16)dv[dt][kt][2], (bf16)dv[dt][kt][3]};
+      bf16x4 e = {(bf16)dv[dt][kt][0], (bf16)dv[dt][kt][1], (bf16)dv[dt][kt][2], (bf16)dv[dt][kt][3]};
       *(bf16x4*)(krow + dt * 16 + 4 * g) = a;
-      *(bf16x4*)(vrow + dt * 16 + 4 * g) = c;
+      *(bf16x4*)(vrow + dt * 16 + 4 * g) = e;
     }
   }
 }
 
 // =====================================================================================
-// backward: dQ (block = 4 waves x 32 queries)
+// backward dQ (block = 4 waves x 32 queries, sweeps all 64-key tiles; transposed lane view as
+// in the forward: q = qt*16 + li, key = kt*16 + 4g + r)
+//   S^T = K Q^T, dP'^T = V dO'^T, dQ^T[d][q] += K^T dS^T  (dS^T packed in pi order as the B operand)
 // =====================================================================================
-__global__ __launch_bounds__(256) void attn_bwd_dq_kernel(const bf16* __restrict__ qkv, const bf16* __restrict__ dout,
-                                                          const float* __restrict__ lse2,
-                                                          const float* __restrict__ Dvec, bf16* __restrict__ dqkv,
-                                                          int N, int H, float scale, float scale_log2, uint32_t th,
-                                                          float dsc, uint64_t seed) {
+template <bool DROP>
+__global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(const bf16* __restrict__ qkv, const bf16* __restrict__ dOs,
+                                                             const float* __restrict__ lse2,
+                                                             const float* __restrict__ Dvec,
+                                                             const uint64_t* __restrict__ MQ, bf16* __restrict__ dqkv,
+                                                             int N, int H, float scale, float c) {
   __shared__ __attribute__((aligned(16))) bf16 sK[2][AT_TILE];
   __shared__ __attribute__((aligned(16))) bf16 sV[2][AT_TILE];
   const int bh = blockIdx.y, b = bh / H, h = bh % H;
@@ -375,17 +502,19 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(const bf16* __restrict
   const bf16* Qg = qkv + (long long)b * N * ld + h * 64;
   const bf16* Kg = Qg + H * 64;
   const bf16* Vg = Qg + 2 * H * 64;
-  const bf16* dOg = dout + (long long)b * N * ldo + h * 64;
+  const bf16* dOg = dOs + (long long)b * N * ldo + h * 64;
   const int w = threadIdx.x >> 6, l = threadIdx.x & 63, g = l >> 4, li = l & 15;
   const int q0 = blockIdx.x * 128 + w * 32;
-  const bool drop = th != 0;
+  const int nkv = N / 64;
+  const uint16_t* mq = DROP ? (const uint16_t*)(MQ + (long long)bh * nkv * N) : nullptr;  // [kv][q][4 x u16]
 
   bf16x8 qf[2][2], of[2][2];
   float L[2], Dq[2];
+  uint32_t mw[2] = {0u, 0u}, mwn[2] = {0u, 0u};
 #pragma unroll
   for (int qt = 0; qt < 2; ++qt) {
-    int row = q0 + qt * 16 + li;
-    bool ok = row < N;
+    const int row = q0 + qt * 16 + li;
+    const bool ok = row < N;
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
       qf[qt][ks] = ok ? *(const bf16x8*)(Qg + (long long)row * ld + ks * 32 + 8 * g) : (bf16x8){};
@@ -393,6 +522,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(const bf16* __restrict
     }
     L[qt] = ok ? lse2[(long long)bh * N + row] : 0.f;
     Dq[qt] = ok ? Dvec[(long long)bh * N + row] : 0.f;
+    if (DROP) mw[qt] = ok ? mq[(long long)row * 4 + g] : 0u;
   }
   f32x4 dq[4][2];
 #pragma unroll
@@ -406,13 +536,19 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(const bf16* __restrict
   stage_store(sK[0], rk);
   stage_store(sV[0], rv);
   __syncthreads();
-  const int nkv = N / 64;
   int cur = 0;
   for (int kv = 0; kv < nkv; ++kv) {
     const bool more = kv + 1 < nkv;
     if (more) {
       stage_load(Kg, ld, (kv + 1) * 64, N, rk);
       stage_load(Vg, ld, (kv + 1) * 64, N, rv);
+      if (DROP) {
+#pragma unroll
+        for (int qt = 0; qt < 2; ++qt) {
+          const int row = q0 + qt * 16 + li;
+          mwn[qt] = row < N ? mq[((long long)(kv + 1) * N + row) * 4 + g] : 0u;
+        }
+      }
     }
     f32x4 s[4][2], dp[4][2];
 #pragma unroll
@@ -423,8 +559,8 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(const bf16* __restrict
     for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
       for (int kt = 0; kt < 4; ++kt) {
-        bf16x8 ka = lds_row_frag(sK[cur], kt * 16, ks);
-        bf16x8 va = lds_row_frag(sV[cur], kt * 16, ks);
+        const bf16x8 ka = lds_row_frag(sK[cur], kt * 16, ks);
+        const bf16x8 va = lds_row_frag(sV[cur], kt * 16, ks);
 #pragma unroll
         for (int qt = 0; qt < 2; ++qt) {
           s[kt][qt] = mfma16(ka, qf[qt][ks], s[kt][qt]);
@@ -432,25 +568,16 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(const bf16* __restrict
         }
       }
 #pragma unroll
-    for (int qt = 0; qt < 2; ++qt) {
-      const long long qrow = (long long)bh * N + (q0 + qt * 16 + li);
+    for (int qt = 0; qt < 2; ++qt)
 #pragma unroll
-      for (int kt = 0; kt < 4; ++kt) {
-        bool keep[4] = {true, true, true, true};
-        if (drop) {
-#pragma unroll
-          for (int r = 0; r < 4; r += 2)
-            dropout_keep2(seed, (uint64_t)(qrow * N + kv * 64 + kt * 16 + 4 * g + r), th, keep[r], keep[r + 1]);
-        }
+      for (int kt = 0; kt < 4; ++kt)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const float p = exp2f(s[kt][qt][r] * scale_log2 - L[qt]);
+          const float p = exp2_fast(fmaf(s[kt][qt][r], c, -L[qt]));
           float dpt = dp[kt][qt][r];
-          if (drop) dpt = keep[r] ? dpt * dsc : 0.f;
+          if (DROP) dpt = keep_and(dpt, mw[qt], kt * 4 + r);
           s[kt][qt][r] = p * (dpt - Dq[qt]);
         }
-      }
-    }
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
       bf16x8 sb[2];
@@ -458,7 +585,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(const bf16* __restrict
       for (int qt = 0; qt < 2; ++qt) sb[qt] = pack_pi(s[2 * ks][qt], s[2 * ks + 1][qt]);
 #pragma unroll
       for (int dt = 0; dt < 4; ++dt) {
-        bf16x8 ka = lds_tr_frag(sK[cur], 32 * ks, 32 * ks + 16, dt * 16);
+        const bf16x8 ka = lds_tr_frag(sK[cur], 32 * ks, 32 * ks + 16, dt * 16);
 #pragma unroll
         for (int qt = 0; qt < 2; ++qt) dq[dt][qt] = mfma16(ka, sb[qt], dq[dt][qt]);
       }
@@ -466,10 +593,12 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(const bf16* __restrict
     if (more) {
       stage_store(sK[cur ^ 1], rk);
       stage_store(sV[cur ^ 1], rv);
+      if (DROP) { mw[0] = mwn[0]; mw[1] = mwn[1]; }
     }
-    __syncthreads();
+    lds_barrier();
     cur ^= 1;
   }
+  // lane holds dQ^T[d = dt*16+4g+r][q = qt*16+li]
 #pragma unroll
   for (int qt = 0; qt < 2; ++qt) {
     const int q = q0 + qt * 16 + li;
@@ -484,39 +613,78 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(const bf16* __restrict
   }
 }
 
-static inline void drop_params(float p, uint32_t* th, float* ds) {
-  uva_drop_params(p, th, ds);
+// =====================================================================================
+// C ABI
+// =====================================================================================
+extern "C" long long uva_attn_mask_bytes(int B, int N, int H) {
+  return 2LL * B * H * (long long)N * (N / 64) * 8;
 }
 
-extern "C" int uva_attn_fwd(const void* qkv, void* out, float* lse2, int B, int N, int H, float scale, float drop_p,
-                            unsigned long long seed, hipStream_t s) {
-  if (N % 64 != 0) return (int)hipErrorInvalidValue;
+extern "C" long long uva_attn_bwd_workspace(int B, int N, int H, float drop_p) {
+  return drop_p > 0.f ? (long long)B * N * H * 64 * 2 : 0;  // dO / (1 - p), bf16
+}
+
+extern "C" int uva_attn_dropmask(void* mask, int B, int N, int H, float drop_p, unsigned long long seed,
+                                 hipStream_t s) {
+  if (N % 64 != 0 || !(drop_p > 0.f) || mask == nullptr) return (int)hipErrorInvalidValue;
   uint32_t th;
   float ds;
-  drop_params(drop_p, &th, &ds);
-  dim3 grid((N + 127) / 128, B * H);
-  attn_fwd_kernel<<<grid, 256, 0, s>>>((const bf16*)qkv, (bf16*)out, lse2, N, H, scale * 1.4426950408889634f, th, ds,
-                                       seed);
+  uva_drop_params(drop_p, &th, &ds);
+  const int nt = N / 64;
+  uint64_t* MQ = (uint64_t*)mask;
+  uint64_t* MK = MQ + (long long)B * H * N * nt;
+  const long long tasks = (long long)B * H * nt * nt;
+  attn_mask_kernel<<<dim3((unsigned)((tasks + 3) / 4)), 256, 0, s>>>(MQ, MK, N, nt, tasks, th, seed);
   UVA_LAUNCH_CHECK();
   return 0;
 }
 
-extern "C" int uva_attn_bwd(const void* qkv, const void* out, const void* dout, const float* lse2, float* Dvec,
-                            void* dqkv, int B, int N, int H, float scale, float drop_p, unsigned long long seed,
-                            hipStream_t s) {
+extern "C" int uva_attn_fwd(const void* qkv, void* out, float* lse2, const void* mask, int B, int N, int H,
+                            float scale, float drop_p, hipStream_t s) {
   if (N % 64 != 0) return (int)hipErrorInvalidValue;
+  const bool drop = drop_p > 0.f;
+  if (drop && mask == nullptr) return (int)hipErrorInvalidValue;
   uint32_t th;
   float ds;
-  drop_params(drop_p, &th, &ds);
-  long long rows = (long long)B * N * H;
-  attn_bwd_pre_kernel<<<dim3((unsigned)((rows + 3) / 4)), 256, 0, s>>>((const bf16*)out, (const bf16*)dout, Dvec, B, N,
-                                                                        H);
+  uva_drop_params(drop_p, &th, &ds);
   dim3 grid((N + 127) / 128, B * H);
-  const float sl2 = scale * 1.4426950408889634f;
-  attn_bwd_dkdv_kernel<<<grid, 256, 0, s>>>((const bf16*)qkv, (const bf16*)dout, lse2, Dvec, (bf16*)dqkv, N, H, scale,
-                                            sl2, th, ds, seed);
-  attn_bwd_dq_kernel<<<grid, 256, 0, s>>>((const bf16*)qkv, (const bf16*)dout, lse2, Dvec, (bf16*)dqkv, N, H, scale,
-                                          sl2, th, ds, seed);
+  const float c = scale * 1.4426950408889634f;
+  if (drop)
+    attn_fwd_kernel<true><<<grid, 256, 0, s>>>((const bf16*)qkv, (bf16*)out, lse2, (const uint64_t*)mask, N, H, c, ds);
+  else
+    attn_fwd_kernel<false><<<grid, 256, 0, s>>>((const bf16*)qkv, (bf16*)out, lse2, nullptr, N, H, c, 1.0f);
+  UVA_LAUNCH_CHECK();
+  return 0;
+}
+
+extern "C" int uva_attn_bwd(const void* qkv, const void* out, const void* dout, const float* lse2, const void* mask,
+                            float* Dvec, void* dqkv, void* workspace, int B, int N, int H, float scale, float drop_p,
+                            hipStream_t s) {
+  if (N % 64 != 0) return (int)hipErrorInvalidValue;
+  const bool drop = drop_p > 0.f;
+  if (drop && (mask == nullptr || workspace == nullptr)) return (int)hipErrorInvalidValue;
+  uint32_t th;
+  float ds;
+  uva_drop_params(drop_p, &th, &ds);
+  const long long rows = (long long)B * N * H;
+  bf16* dOs = drop ? (bf16*)workspace : nullptr;
+  attn_bwd_pre_kernel<<<(unsigned)((rows * 8 + 255) / 256), 256, 0, s>>>((const bf16*)out, (const bf16*)dout, Dvec,
+                                                                         dOs, rows, N, H, ds);
+  const int nt = N / 64;
+  const uint64_t* MQ = (const uint64_t*)mask;
+  const uint64_t* MK = drop ? MQ + (long long)B * H * N * nt : nullptr;
+  const bf16* dO = drop ? dOs : (const bf16*)dout;
+  dim3 grid((N + 127) / 128, B * H);
+  const float c = scale * 1.4426950408889634f;
+  if (drop) {
+    attn_bwd_dkdv_kernel<true><<<grid, 256, 0, s>>>((const bf16*)qkv, dO, lse2, Dvec, MK, (bf16*)dqkv, N, H, scale, c);
+    attn_bwd_dq_kernel<true><<<grid, 256, 0, s>>>((const bf16*)qkv, dO, lse2, Dvec, MQ, (bf16*)dqkv, N, H, scale, c);
+  } else {
+    attn_bwd_dkdv_kernel<false><<<grid, 256, 0, s>>>((const bf16*)qkv, dO, lse2, Dvec, nullptr, (bf16*)dqkv, N, H,
+                                                     scale, c);
+    attn_bwd_dq_kernel<false><<<grid, 256, 0, s>>>((const bf16*)qkv, dO, lse2, Dvec, nullptr, (bf16*)dqkv, N, H, scale,
+                                                   c);
+  }
   UVA_LAUNCH_CHECK();
   return 0;
 }

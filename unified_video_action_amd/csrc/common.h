@@ -50,8 +50,9 @@ __device__ __forceinline__ float group16_max(float v) {
 // ---- dropout mask ----------------------------------------------------------------------
 // Stateless counter-based mask shared by every kernel that drops (GEMM epilogues, attention
 // fwd/bwd, softmax, activation backward), so forward and backward regenerate identical masks.
-// Element idx belongs to pair idx >> 1; one 32-bit hash per pair (3 x v_mul_lo_u32, no 64-bit
-// multiplies) yields two 16-bit uniforms: low half -> even idx, high half -> odd idx.
+// Element idx belongs to pair idx >> 1; one 32-bit hash per pair (the keyed counter through the
+// lowbias32 finalizer: 2 x v_mul_lo_u32, no 64-bit multiplies) yields two 16-bit uniforms:
+// low half -> even idx, high half -> odd idx.
 // keep iff u16 >= thresh, thresh = round(p * 65536); kept values scale by 65536 / (65536 - thresh).
 __device__ __forceinline__ uint32_t drop_key(uint64_t seed) {
   uint32_t k = (uint32_t)seed ^ (((uint32_t)(seed >> 32)) * 0x9E3779B1u);
@@ -61,7 +62,7 @@ __device__ __forceinline__ uint32_t drop_key(uint64_t seed) {
   return k;
 }
 __device__ __forceinline__ uint32_t drop_hash(uint32_t key, uint64_t pair) {
-  uint32_t x = ((uint32_t)pair * 0x9E3779B1u) ^ (key + __builtin_rotateleft32((uint32_t)(pair >> 32), 11));
+  uint32_t x = (uint32_t)pair ^ (key + __builtin_rotateleft32((uint32_t)(pair >> 32), 11));
   x ^= x >> 16;
   x *= 0x7feb352du;
   x ^= x >> 15;

@@ -230,8 +230,8 @@ class BlockFn(torch.autograd.Function):
         if flash:
             o = torch.empty(M, D, dtype=c, device=dev)
             lse = torch.empty(B, H, N, dtype=F32, device=dev)
-            ops.attn_fwd(qkv, o, lse, B, N, H, scale, p_attn, seeds[0])
-            P = Pd = None
+            amask = ops.attn_fwd(qkv, o, lse, B, N, H, scale, p_attn, seeds[0])
+            P, Pd = None, amask
         else:
             o, P, Pd = _attn_mat_fwd(qkv, B, N, H, scale, p_attn, seeds[0])
             o = as_dtype(o, c)
@@ -296,7 +296,7 @@ class BlockFn(torch.autograd.Function):
         if flash:
             dqkv = torch.empty(M, 3 * D, dtype=c, device=dev)
             dvec = torch.empty(B, H, N, dtype=F32, device=dev)
-            ops.attn_bwd(qkv, o, do, lse, dvec, dqkv, B, N, H, scale, p_attn, seeds[0])
+            ops.attn_bwd(qkv, o, do, lse, dvec, dqkv, B, N, H, scale, p_attn, seeds[0], mask=Pd)
         else:
             dqkv = as_dtype(_attn_mat_bwd(qkv, P, Pd, do, B, N, H, scale, p_attn, seeds[0]), c)
         del do

@@ -243,27 +243,37 @@ def adamw_ema(p, g, m, v, ema, p_bf16, n_decay, lr, b1, b2, eps, wd, step, grad_
                float(ema_decay), stream())
 
 
-def attn_fwd(qkv, out, lse2, B, N, H, scale, drop_p=0.0, seed=0):
+def attn_dropmask(B, N, H, drop_p, seed, device):
+    """keep-mask bit planes of attention dropout (counter hash of (seed, element)), shared by
+    attn_fwd and attn_bwd of the same step."""
+    mask = torch.empty(lib().query("uva_attn_mask_bytes", B, N, H), dtype=torch.uint8, device=device)
+    lib().call("uva_attn_dropmask", ptr(mask), B, N, H, float(drop_p), int(seed) & 0xFFFFFFFFFFFFFFFF, stream())
+    return mask
+
+
+def attn_fwd(qkv, out, lse2, B, N, H, scale, drop_p=0.0, seed=0, mask=None):
+    """-> the dropout mask planes (None when drop_p == 0); pass them to attn_bwd."""
     assert qkv.dtype == torch.bfloat16 and qkv.is_contiguous() and out.is_contiguous()
     assert N % 64 == 0 and qkv.shape[-1] == 3 * H * 64
+    assert qkv.numel() == B * N * 3 * H * 64 and out.numel() == B * N * H * 64 and lse2.numel() == B * H * N
     with _traced(f"attn_fwd B{B} N{N} H{H}", 4.0 * B * H * N * N * 64):
-        _attn_fwd_call(qkv, out, lse2, B, N, H, scale, drop_p, seed)
+        if drop_p > 0 and mask is None:
+            mask = attn_dropmask(B, N, H, drop_p, seed, qkv.device)
+        lib().call("uva_attn_fwd", ptr(qkv), ptr(out), ptr(lse2), ptr(mask) if drop_p > 0 else None, B, N, H,
+                   float(scale), float(drop_p), stream())
+    return mask if drop_p > 0 else None
 
 
-def _attn_fwd_call(qkv, out, lse2, B, N, H, scale, drop_p, seed):
-    lib().call("uva_attn_fwd", ptr(qkv), ptr(out), ptr(lse2), B, N, H, float(scale), float(drop_p),
-               int(seed) & 0xFFFFFFFFFFFFFFFF, stream())
-
-
-def attn_bwd(qkv, out, dout, lse2, dvec, dqkv, B, N, H, scale, drop_p=0.0, seed=0):
+def attn_bwd(qkv, out, dout, lse2, dvec, dqkv, B, N, H, scale, drop_p=0.0, seed=0, mask=None):
     assert dout.dtype == torch.bfloat16 and dout.is_contiguous() and dqkv.is_contiguous()
+    assert dout.numel() == B * N * H * 64 and dqkv.numel() == B * N * 3 * H * 64 and dvec.numel() == B * H * N
     with _traced(f"attn_bwd B{B} N{N} H{H}", 8.0 * B * H * N * N * 64):
-        _attn_bwd_call(qkv, out, dout, lse2, dvec, dqkv, B, N, H, scale, drop_p, seed)
-
-
-def _attn_bwd_call(qkv, out, dout, lse2, dvec, dqkv, B, N, H, scale, drop_p, seed):
-    lib().call("uva_attn_bwd", ptr(qkv), ptr(out), ptr(dout), ptr(lse2), ptr(dvec), ptr(dqkv), B, N, H,
-               float(scale), float(drop_p), int(seed) & 0xFFFFFFFFFFFFFFFF, stream())
+        if drop_p > 0 and mask is None:
+            mask = attn_dropmask(B, N, H, drop_p, seed, qkv.device)
+        nb = lib().query("uva_attn_bwd_workspace", B, N, H, float(drop_p))
+        ws = torch.empty(nb, dtype=torch.uint8, device=qkv.device) if nb else None
+        lib().call("uva_attn_bwd", ptr(qkv), ptr(out), ptr(dout), ptr(lse2), ptr(mask) if drop_p > 0 else None,
+                   ptr(dvec), ptr(dqkv), ptr(ws), B, N, H, float(scale), float(drop_p), stream())
 
 
 def conv2d(x, w, out, Nimg, Hin, Win, Ci, Co, ks, stride, pad_t, pad_l, Hout, Wout, bias=None, residual=None,
