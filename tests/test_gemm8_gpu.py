@@ -29,7 +29,9 @@ def _stored(op, t_flag):
     return op.t().contiguous() if t_flag else op.contiguous()
 
 
-CASES = [(5376, 3072, 328, 256), (5000, 3000, 136, 256), (6144, 2048, 200, 256)]
+CASES = [(5376, 3072, 328, 256), (5000, 3000, 136, 256), (6144, 2048, 200, 256),
+         # > 256 tiles: persistent blocks walk 3 tiles each, cross-tile K-tile-0 prefetch (ragged M, K tail)
+         (16296, 3072, 328, 256), (16384, 3072, 256, 256)]
 
 
 @pytest.mark.parametrize("odt", [torch.float32, torch.bfloat16])
@@ -62,9 +64,10 @@ def test_gemm8_splitk_dw_accumulate(M, N, K, splits):
     assert rel_err(g, ref) < 1e-4  # exact bf16 products, fp32 partial sums over 8-16k terms
 
 
-def test_gemm8_epilogues():
+@pytest.mark.parametrize("M", [5376, 16384])  # 16384: 768 tiles -> persistent blocks
+def test_gemm8_epilogues(M):
     from unified_video_action_amd.native import ops
-    M, N, K = 5376, 3072, 256
+    N, K = 3072, 256
     assert ops.gemm_plan(M, N, K) == (3, 256, 1)
     x = torch.randn(M, K, device=DEV).to(torch.bfloat16)
     w = (torch.randn(N, K, device=DEV) * 0.1).to(torch.bfloat16)

@@ -18,8 +18,8 @@
 // MFMA kernels, so forward and backward only test bits (v_bfe_i32 + v_and per element):
 //   MQ [bh][key tile kv][q]   u64, bit g*16+kt*4+r  <-> key kv*64 + kt*16 + 4g + r
 //   MK [bh][query tile qb][key] u64, bit g*16+qt*4+r <-> query qb*64 + qt*16 + 4g + r
-// (the 16 bits a lane of quad g needs are the u16 at offset g).  MK comes from MQ's rows by
-// 64 wave ballots (lane L computes the query whose MK bit is L).
+// (the 16 bits a lane of quad g needs are the u16 at offset g).  MK comes from MQ's rows by a
+// 6-stage 64x64 bit transpose across the wave (lane L computes the query whose MK bit is L).
 //
 // Backward (two kernels, FA2 recompute, no atomics -> bitwise reproducible):
 //   attn_bwd_dkdv : block = 128 keys (4 waves x 32), sweeps all 64-query tiles; S and dP with
@@ -32,6 +32,7 @@
 // dO' = dO / (1 - p) is prepared by the pre kernel (with D = rowsum(dO * O)), so the dropout
 // scale costs nothing inside the loops.
 #include "common.h"
+#include <stdlib.h>
 
 #define AT_LD 72
 #define AT_TILE (64 * AT_LD)
@@ -60,14 +61,18 @@ __device__ __forceinline__ f32x4 mfma16(const bf16x8& a, const bf16x8& b, const 
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
 }
 
-// 64 rows x 64 cols of a strided bf16 matrix -> 2 chunks (16 B) per thread
+// 64 rows x 64 cols of a strided bf16 matrix -> 2 chunks (16 B) per thread.  Tiles are always
+// full (N % 64 == 0 is an ABI precondition), so no per-row guard (its exec-mask branches
+// serialised the loads); the uniform tile base is formed once, per-thread offsets are hoisted.
 __device__ __forceinline__ void stage_load(const bf16* __restrict__ g, long long ld, int row0, int nrows,
                                            bf16x8 (&r)[2]) {
+  (void)nrows;
   const int t = threadIdx.x;
+  const bf16* base = g + (long long)row0 * ld;
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
-    int id = t + i * 256, row = id >> 3, c = (id & 7) * 8;
-    r[i] = (row0 + row < nrows) ? *(const bf16x8*)(g + (long long)(row0 + row) * ld + c) : (bf16x8){};
+    const int id = t + i * 256, row = id >> 3, c = (id & 7) * 8;
+    r[i] = *(const bf16x8*)(base + (long long)row * ld + c);
   }
 }
 __device__ __forceinline__ void stage_store(bf16* lds, const bf16x8 (&r)[2]) {
@@ -87,10 +92,15 @@ __device__ __forceinline__ void lds_barrier() {
   asm volatile("" ::: "memory");
 }
 __device__ __forceinline__ float exp2_fast(float x) { return __builtin_amdgcn_exp2f(x); }
-// keep-bit b of a mask word as an all-ones / all-zeros 32-bit mask
+// keep-bit b of a mask word as an all-ones / all-zeros 32-bit mask.  (A v_bfe_i32 in inline asm
+// saves hipcc's v_and + v_cmp + v_cndmask lowering but measured slower in the dK/dV loop: the
+// asm statements constrain its scheduling.)
 __device__ __forceinline__ float keep_and(float v, uint32_t w, int b) {
   return __int_as_float(__float_as_int(v) & __builtin_amdgcn_sbfe(w, b, 1));
 }
+// max of two MFMA outputs without the canonicalising v_max hipcc inserts in front of fmaxf
+// (med3(a, b, +inf) == max(a, b); the compiler fuses chains of it into v_max3_f32)
+__device__ __forceinline__ float fmax_nc(float a, float b) { return __builtin_amdgcn_fmed3f(a, b, INFINITY); }
 // position of element k (0..63) of a 64-wide tile inside an MQ / MK word (an involution)
 __host__ __device__ constexpr int mask_pos(int k) { return ((k >> 2) & 3) * 16 + (k >> 4) * 4 + (k & 3); }
 
@@ -148,12 +158,16 @@ __global__ __launch_bounds__(256) void attn_mask_kernel(uint64_t* __restrict__ M
 // =====================================================================================
 // forward
 // =====================================================================================
-template <bool DROP>
-__global__ __launch_bounds__(256) void attn_fwd_kernel(const bf16* __restrict__ qkv, bf16* __restrict__ out,
+// KT = keys per LDS tile (64 or 128): the longer tile gives each MFMA/softmax round more work to
+// hide the next tile's global loads behind (register-staged, written after the compute).
+template <bool DROP, int KT>
+__global__ __launch_bounds__(256, 2) void attn_fwd_kernel(const bf16* __restrict__ qkv, bf16* __restrict__ out,
                                                        float* __restrict__ lse2, const uint64_t* __restrict__ MQ,
                                                        int N, int H, float c, float dsc) {
-  __shared__ __attribute__((aligned(16))) bf16 sK[2][AT_TILE];
-  __shared__ __attribute__((aligned(16))) bf16 sV[2][AT_TILE];
+  constexpr int NKT = KT / 16;   // 16-key MFMA tiles per LDS tile
+  constexpr int NH = KT / 64;    // 64-key mask words per LDS tile
+  __shared__ __attribute__((aligned(16))) bf16 sK[2][NH * AT_TILE];
+  __shared__ __attribute__((aligned(16))) bf16 sV[2][NH * AT_TILE];
   const int bh = blockIdx.y, b = bh / H, h = bh % H;
   const long long ld = 3LL * H * 64;
   const bf16* Qg = qkv + (long long)b * N * ld + h * 64;
@@ -161,18 +175,22 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const bf16* __restrict__ 
   const bf16* Vg = Qg + 2 * H * 64;
   const int w = threadIdx.x >> 6, l = threadIdx.x & 63, g = l >> 4, li = l & 15;
   const int q0 = blockIdx.x * 128 + w * 32;
-  const int nkv = N / 64;
-  const uint16_t* mq = DROP ? (const uint16_t*)(MQ + (long long)bh * nkv * N) : nullptr;  // [kv][q][4 x u16]
+  const int nkv = N / KT, n64 = N / 64;
+  const uint16_t* mq = DROP ? (const uint16_t*)(MQ + (long long)bh * n64 * N) : nullptr;  // [kv64][q][4 x u16]
 
   bf16x8 qf[2][2];
-  uint32_t mw[2] = {0u, 0u}, mwn[2] = {0u, 0u};
+  uint32_t mw[2][NH], mwn[2][NH];
 #pragma unroll
   for (int qt = 0; qt < 2; ++qt) {
     const int row = q0 + qt * 16 + li;
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks)
       qf[qt][ks] = row < N ? *(const bf16x8*)(Qg + (long long)row * ld + ks * 32 + 8 * g) : (bf16x8){};
-    if (DROP) mw[qt] = row < N ? mq[(long long)row * 4 + g] : 0u;
+#pragma unroll
+    for (int hh = 0; hh < NH; ++hh) {
+      mw[qt][hh] = (DROP && row < N) ? mq[((long long)hh * N + row) * 4 + g] : 0u;
+      mwn[qt][hh] = 0u;
+    }
   }
   float m[2] = {-INFINITY, -INFINITY}, rs[2] = {0.f, 0.f};
   f32x4 o[2][4];
@@ -181,50 +199,63 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const bf16* __restrict__ 
 #pragma unroll
     for (int dt = 0; dt < 4; ++dt) o[qt][dt] = (f32x4){0.f, 0.f, 0.f, 0.f};
 
-  bf16x8 rk[2], rv[2];
-  stage_load(Kg, ld, 0, N, rk);
-  stage_load(Vg, ld, 0, N, rv);
-  stage_store(sK[0], rk);
-  stage_store(sV[0], rv);
+  bf16x8 rk[NH][2], rv[NH][2];
+#pragma unroll
+  for (int hh = 0; hh < NH; ++hh) {
+    stage_load(Kg, ld, hh * 64, N, rk[hh]);
+    stage_load(Vg, ld, hh * 64, N, rv[hh]);
+  }
+#pragma unroll
+  for (int hh = 0; hh < NH; ++hh) {
+    stage_store(sK[0] + hh * AT_TILE, rk[hh]);
+    stage_store(sV[0] + hh * AT_TILE, rv[hh]);
+  }
   __syncthreads();
   int cur = 0;
   for (int kv = 0; kv < nkv; ++kv) {
     const bool more = kv + 1 < nkv;
     if (more) {
-      stage_load(Kg, ld, (kv + 1) * 64, N, rk);
-      stage_load(Vg, ld, (kv + 1) * 64, N, rv);
+#pragma unroll
+      for (int hh = 0; hh < NH; ++hh) {
+        stage_load(Kg, ld, (kv + 1) * KT + hh * 64, N, rk[hh]);
+        stage_load(Vg, ld, (kv + 1) * KT + hh * 64, N, rv[hh]);
+      }
       if (DROP) {
 #pragma unroll
         for (int qt = 0; qt < 2; ++qt) {
           const int row = q0 + qt * 16 + li;
-          mwn[qt] = row < N ? mq[((long long)(kv + 1) * N + row) * 4 + g] : 0u;
+#pragma unroll
+          for (int hh = 0; hh < NH; ++hh)
+            mwn[qt][hh] = row < N ? mq[((long long)((kv + 1) * NH + hh) * N + row) * 4 + g] : 0u;
         }
       }
     }
-    f32x4 s[4][2];
+    const bf16* cK = sK[cur];
+    const bf16* cV = sV[cur];
+    f32x4 s[NKT][2];
 #pragma unroll
-    for (int kt = 0; kt < 4; ++kt)
+    for (int kt = 0; kt < NKT; ++kt)
 #pragma unroll
       for (int qt = 0; qt < 2; ++qt) s[kt][qt] = (f32x4){0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
-      bf16x8 kf[4];
 #pragma unroll
-      for (int kt = 0; kt < 4; ++kt) kf[kt] = lds_row_frag(sK[cur], kt * 16, ks);
+      for (int kt = 0; kt < NKT; ++kt) {
+        const bf16x8 kf = lds_row_frag(cK, kt * 16, ks);
 #pragma unroll
-      for (int kt = 0; kt < 4; ++kt)
-#pragma unroll
-        for (int qt = 0; qt < 2; ++qt) s[kt][qt] = mfma16(kf[kt], qf[qt][ks], s[kt][qt]);
+        for (int qt = 0; qt < 2; ++qt) s[kt][qt] = mfma16(kf, qf[qt][ks], s[kt][qt]);
+      }
     }
-    // row max (lane: 16 keys of its query; the 4 quads of a query meet through two shuffles)
+    // row max (lane: NKT*4 keys of its query; the 4 quads of a query meet through two shuffles)
     float mx[2];
     bool need = false;
 #pragma unroll
     for (int qt = 0; qt < 2; ++qt) {
-      float a = fmaxf(fmaxf(s[0][qt][0], s[0][qt][1]), fmaxf(s[0][qt][2], s[0][qt][3]));
+      float a = fmax_nc(s[0][qt][0], s[0][qt][1]);
 #pragma unroll
-      for (int kt = 1; kt < 4; ++kt)
-        a = fmaxf(a, fmaxf(fmaxf(s[kt][qt][0], s[kt][qt][1]), fmaxf(s[kt][qt][2], s[kt][qt][3])));
+      for (int kt = 0; kt < NKT; ++kt)
+#pragma unroll
+        for (int r = (kt == 0 ? 2 : 0); r < 4; ++r) a = fmax_nc(a, s[kt][qt][r]);
       a = fmaxf(a, __shfl_xor(a, 16, 64));
       a = fmaxf(a, __shfl_xor(a, 32, 64));
       mx[qt] = a * c;
@@ -246,30 +277,38 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const bf16* __restrict__ 
     for (int qt = 0; qt < 2; ++qt) {
       const float nm = -m[qt];
 #pragma unroll
-      for (int kt = 0; kt < 4; ++kt)
+      for (int kt = 0; kt < NKT; ++kt)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const float p = exp2_fast(fmaf(s[kt][qt][r], c, nm));
           rs[qt] += p;
-          s[kt][qt][r] = DROP ? keep_and(p, mw[qt], kt * 4 + r) : p;
+          s[kt][qt][r] = DROP ? keep_and(p, mw[qt][kt >> 2], (kt & 3) * 4 + r) : p;
         }
     }
 #pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
+    for (int ks = 0; ks < KT / 32; ++ks) {
       bf16x8 pf[2];
 #pragma unroll
       for (int qt = 0; qt < 2; ++qt) pf[qt] = pack_pi(s[2 * ks][qt], s[2 * ks + 1][qt]);
 #pragma unroll
       for (int dt = 0; dt < 4; ++dt) {
-        bf16x8 vf = lds_tr_frag(sV[cur], 32 * ks, 32 * ks + 16, dt * 16);
+        const bf16x8 vf = lds_tr_frag(cV, 32 * ks, 32 * ks + 16, dt * 16);
 #pragma unroll
         for (int qt = 0; qt < 2; ++qt) o[qt][dt] = mfma16(vf, pf[qt], o[qt][dt]);
       }
     }
     if (more) {
-      stage_store(sK[cur ^ 1], rk);
-      stage_store(sV[cur ^ 1], rv);
-      if (DROP) { mw[0] = mwn[0]; mw[1] = mwn[1]; }
+#pragma unroll
+      for (int hh = 0; hh < NH; ++hh) {
+        stage_store(sK[cur ^ 1] + hh * AT_TILE, rk[hh]);
+        stage_store(sV[cur ^ 1] + hh * AT_TILE, rv[hh]);
+      }
+      if (DROP) {
+#pragma unroll
+        for (int qt = 0; qt < 2; ++qt)
+#pragma unroll
+          for (int hh = 0; hh < NH; ++hh) mw[qt][hh] = mwn[qt][hh];
+      }
     }
     __syncthreads();
     cur ^= 1;
@@ -649,10 +688,17 @@ extern "C" int uva_attn_fwd(const void* qkv, void* out, float* lse2, const void*
   uva_drop_params(drop_p, &th, &ds);
   dim3 grid((N + 127) / 128, B * H);
   const float c = scale * 1.4426950408889634f;
-  if (drop)
-    attn_fwd_kernel<true><<<grid, 256, 0, s>>>((const bf16*)qkv, (bf16*)out, lse2, (const uint64_t*)mask, N, H, c, ds);
+  static const int kt_env = getenv("UVA_ATTN_FWD_KT") ? atoi(getenv("UVA_ATTN_FWD_KT")) : 128;
+  const bool k128 = kt_env == 128 && N % 128 == 0;
+  const uint64_t* MQ = drop ? (const uint64_t*)mask : nullptr;
+  if (drop && k128)
+    attn_fwd_kernel<true, 128><<<grid, 256, 0, s>>>((const bf16*)qkv, (bf16*)out, lse2, MQ, N, H, c, ds);
+  else if (drop)
+    attn_fwd_kernel<true, 64><<<grid, 256, 0, s>>>((const bf16*)qkv, (bf16*)out, lse2, MQ, N, H, c, ds);
+  else if (k128)
+    attn_fwd_kernel<false, 128><<<grid, 256, 0, s>>>((const bf16*)qkv, (bf16*)out, lse2, nullptr, N, H, c, 1.0f);
   else
-    attn_fwd_kernel<false><<<grid, 256, 0, s>>>((const bf16*)qkv, (bf16*)out, lse2, nullptr, N, H, c, 1.0f);
+    attn_fwd_kernel<false, 64><<<grid, 256, 0, s>>>((const bf16*)qkv, (bf16*)out, lse2, nullptr, N, H, c, 1.0f);
   UVA_LAUNCH_CHECK();
   return 0;
 }

@@ -212,14 +212,16 @@ class BlockFn(torch.autograd.Function):
     x: [B*N, D] fp32 residual stream."""
 
     @staticmethod
-    def forward(ctx, x, shape, p_attn, p_proj, hook, n1w, n1b, qkvw, qkvb, projw, projb, n2w, n2b, fc1w, fc1b,
-                fc2w, fc2b):
+    def forward(ctx, x, shape, p_attn, p_proj, hook, premask, n1w, n1b, qkvw, qkvb, projw, projb, n2w, n2b, fc1w,
+                fc1b, fc2w, fc2b):
         B, N, H = shape
         M, D = x.shape
         dev = x.device
         c = cdt()
         scale = (D // H) ** -0.5
         seeds = [_seed() for _ in range(4)]
+        if premask is not None:  # attention keep-mask planes generated ahead on the side stream
+            seeds[0] = premask[0]
         h1 = torch.empty(M, D, dtype=c, device=dev)
         m1 = torch.empty(M, dtype=F32, device=dev)
         r1 = torch.empty(M, dtype=F32, device=dev)
@@ -230,7 +232,8 @@ class BlockFn(torch.autograd.Function):
         if flash:
             o = torch.empty(M, D, dtype=c, device=dev)
             lse = torch.empty(B, H, N, dtype=F32, device=dev)
-            amask = ops.attn_fwd(qkv, o, lse, B, N, H, scale, p_attn, seeds[0])
+            amask = ops.attn_fwd(qkv, o, lse, B, N, H, scale, p_attn, seeds[0],
+                                 mask=premask[1] if premask is not None else None)
             P, Pd = None, amask
         else:
             o, P, Pd = _attn_mat_fwd(qkv, B, N, H, scale, p_attn, seeds[0])
@@ -310,15 +313,21 @@ class BlockFn(torch.autograd.Function):
                           dx_base=g1)
         if ctx.hook is not None:
             ctx.hook()  # every grad of this block is enqueued: launch its DP bucket all-reduce
-        return (gx,) + (None,) * 16
+        return (gx,) + (None,) * 17
 
 
 def block_forward(blk, x, B, N, p_attn, p_proj):
     """x: [B, N, D] fp32 -> [B, N, D] fp32 through BlockFn."""
     D = x.shape[-1]
     a, m = blk.attn, blk.mlp
+    premask = None
+    if p_attn > 0 and use_flash(N, D // a.num_heads) and x.is_cuda:
+        shape = (B, N, a.num_heads, float(p_attn))
+        premask = RT.take_attn_mask(id(blk), shape)
+        RT.note_attn_shape(id(blk), shape)  # the next step's masks are generated ahead of time
     y = BlockFn.apply(x.reshape(B * N, D).contiguous(), (B, N, a.num_heads), p_attn, p_proj,
-                      getattr(blk, "_uva_bucket_hook", None), blk.norm1.weight, blk.norm1.bias, a.qkv.weight, a.qkv.bias, a.proj.weight, a.proj.bias,
+                      getattr(blk, "_uva_bucket_hook", None), premask, blk.norm1.weight, blk.norm1.bias,
+                      a.qkv.weight, a.qkv.bias, a.proj.weight, a.proj.bias,
                       blk.norm2.weight, blk.norm2.bias, m.fc1.weight, m.fc1.bias, m.fc2.weight, m.fc2.bias)
     return y.reshape(B, N, D)
 

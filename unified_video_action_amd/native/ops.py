@@ -243,10 +243,15 @@ def adamw_ema(p, g, m, v, ema, p_bf16, n_decay, lr, b1, b2, eps, wd, step, grad_
                float(ema_decay), stream())
 
 
-def attn_dropmask(B, N, H, drop_p, seed, device):
+def attn_mask_alloc(B, N, H, device):
+    return torch.empty(lib().query("uva_attn_mask_bytes", B, N, H), dtype=torch.uint8, device=device)
+
+
+def attn_dropmask(B, N, H, drop_p, seed, device, out=None):
     """keep-mask bit planes of attention dropout (counter hash of (seed, element)), shared by
     attn_fwd and attn_bwd of the same step."""
-    mask = torch.empty(lib().query("uva_attn_mask_bytes", B, N, H), dtype=torch.uint8, device=device)
+    mask = attn_mask_alloc(B, N, H, device) if out is None else out
+    assert mask.numel() == lib().query("uva_attn_mask_bytes", B, N, H) and mask.dtype == torch.uint8
     lib().call("uva_attn_dropmask", ptr(mask), B, N, H, float(drop_p), int(seed) & 0xFFFFFFFFFFFFFFFF, stream())
     return mask
 

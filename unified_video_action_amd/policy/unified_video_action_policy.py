@@ -24,6 +24,7 @@ from ..model.autoregressive import mar_con_unified as mar
 from ..model.common.normalizer import LinearNormalizer
 from ..utils.data_utils import (get_trajectory, image_key, select_frame_indices, umi_proprioception,
                                 vae_images)
+from ..runtime import RT
 from ..vae.vaekl import AutoencoderKL
 
 ALL_TASK_MODES = ["video_model", "dynamic_model", "policy_model", "inverse_model", "full_dynamic_model"]
@@ -149,6 +150,8 @@ class UnifiedVideoActionPolicy(nn.Module):
         else:
             sel = select_frame_indices(T, different_history_freq=self.different_history_freq,
                                        rng_choice=rng.get("history_combination"))
+        if self.training and dev.type == "cuda":
+            RT.prefetch_attn_masks(dev)  # attention dropout planes under the VAE encode (side stream)
         x = vae_images(img, sel, self.vae_model.CIN_PAD)
         n_half = B * (len(sel) // 2)
         eps = rng.get("vae_eps_x")

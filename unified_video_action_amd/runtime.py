@@ -11,6 +11,12 @@ class _Runtime:
         self.flash_attention = True           # bf16 fused attention; False -> materialised GEMM+softmax
         self._seed_base = 0x5EED
         self._ctr = itertools.count()
+        # attention dropout masks: per Block the (B, N, H, p) of its last training forward, and the
+        # masks generated ahead of time on a side stream (overlapping the VAE encode)
+        self.attn_prefetch = True
+        self._attn_shapes = {}
+        self._attn_ready = {}
+        self._side = None
 
     def set_precision(self, name):
         name = str(name).lower()
@@ -29,6 +35,43 @@ class _Runtime:
 
     def next_seed(self):
         return (self._seed_base * 0x9E3779B97F4A7C15 + next(self._ctr) * 0xBF58476D1CE4E5B9) & 0xFFFFFFFFFFFFFFFF
+
+
+    # ---- attention dropout-mask prefetch ------------------------------------------------
+    def note_attn_shape(self, key, shape):
+        self._attn_shapes[key] = shape
+
+    def prefetch_attn_masks(self, device):
+        """Generate every known Block's attention keep-mask planes for this step on a side stream,
+        so the VALU-bound mask kernels run under the (MFMA-bound) VAE encode that precedes the MAR.
+        Each Block waits on its own event before its attention forward reads the planes."""
+        if not (self.attn_prefetch and self._attn_shapes and torch.cuda.is_available()):
+            return
+        from .native import ops
+        if self._side is None:
+            self._side = torch.cuda.Stream(device=device)
+        main = torch.cuda.current_stream(device)
+        self._side.wait_stream(main)
+        ready = {}
+        for key, (B, N, H, p) in self._attn_shapes.items():
+            seed = self.next_seed()
+            mask = ops.attn_mask_alloc(B, N, H, device)  # allocated in main-stream order
+            with torch.cuda.stream(self._side):
+                ops.attn_dropmask(B, N, H, p, seed, device, out=mask)
+            ev = torch.cuda.Event()
+            ev.record(self._side)
+            mask.record_stream(self._side)
+            ready[key] = ((B, N, H, p), seed, mask, ev)
+        self._attn_ready = ready
+
+    def take_attn_mask(self, key, shape):
+        """-> (seed, mask) prefetched for this Block and shape (the current stream now waits for
+        it), or None."""
+        hit = self._attn_ready.pop(key, None)
+        if hit is None or hit[0] != shape:
+            return None
+        torch.cuda.current_stream().wait_event(hit[3])
+        return hit[1], hit[2]
 
 
 RT = _Runtime()
