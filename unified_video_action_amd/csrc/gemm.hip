@@ -409,6 +409,13 @@ __device__ __forceinline__ void epi_row8(TC* __restrict__ C, long long cbase, co
 #define EPI_TP 132  // fp32 row pitch of the staged tile (+4 floats: conflict-free column writes)
 #define EPI_LDS_BYTES (128 * EPI_TP * 4 + 4 * 16 * 8 * 2 * 4)
 
+// epilogue barrier that orders LDS only: the chunk's global stores stay in flight across it
+__device__ __forceinline__ void epi_lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
 template <typename TC>
 __device__ __forceinline__ void epilogue_tile(const f32x4 (&acc)[4][4], char* smem, TC* __restrict__ C, int M, int N,
                                               long long ldc, long long coff, const EpiParams& ep, long long roff,
@@ -880,7 +887,10 @@ struct Gemm8Cfg {
 
 // VAR: diagnostic build bits (0 = production): 1 s_memtime stamps per phase segment, 2 no wave-group
 // stagger, 4 no compiler memory fences around barriers, 8 lgkmcnt after the barrier (timing only:
-// breaks the WAR order), 16 no s_setprio
+// breaks the WAR order), 16 no s_setprio, 32 per-tile prologue / K-loop / epilogue stamps,
+// 64 LDS-only epilogue barriers, 128 (with 32) epilogue chunk-0 staging / store split
+// (tools_gemm8_phase.py: the epilogue of a 256x256 bf16 tile is ~29k ticks at K=768, mostly the
+// output stores of all CUs landing at once)
 #define GEMM8_SYNC()                                     \
   do {                                                   \
     if constexpr (!(VAR & 4)) asm volatile("" ::: "memory"); \
@@ -895,6 +905,8 @@ __global__ __launch_bounds__(512, 1) void gemm_8ph(const bf16* __restrict__ A, c
   using G = Gemm8Cfg<BN>;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   bf16* lds = (bf16*)smem;
+  unsigned long long st_entry = 0, st_after_pro = 0, st_after_loop = 0, st_e1 = 0, st_e2 = 0;
+  if constexpr (VAR & 32) asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(st_entry)::"memory");
   const int z = blockIdx.z, zo = z / bs.binner, zi = z % bs.binner;
   A += zo * bs.sAo + zi * bs.sAi;
   B += zo * bs.sBo + zi * bs.sBi;
@@ -986,6 +998,7 @@ __global__ __launch_bounds__(512, 1) void gemm_8ph(const bf16* __restrict__ A, c
   } while (0)
   GEMM8_STAMP(st_loop0);
   st_t0 = st_loop0;
+  if constexpr (VAR & 32) asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(st_after_pro)::"memory");
 
 #define GEMM8_QUAD(AH, BH, FB)                                                                            \
   if constexpr (!(VAR & 16)) __builtin_amdgcn_s_setprio(1);                                               \
@@ -1079,6 +1092,7 @@ __global__ __launch_bounds__(512, 1) void gemm_8ph(const bf16* __restrict__ A, c
     }
   }
 #undef GEMM8_STAMP
+  if constexpr (VAR & 32) asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(st_after_loop)::"memory");
   if (!(VAR & 2) && grp == 0) __builtin_amdgcn_s_barrier();  // re-align barrier counts: every wave is past its last MFMA
   GEMM8_SYNC();
 
@@ -1108,7 +1122,10 @@ __global__ __launch_bounds__(512, 1) void gemm_8ph(const bf16* __restrict__ A, c
           for (int r = 0; r < 4; ++r)
             T[(rbase + i * 16 + (lane >> 4) * 4 + r) * G::TP + wc * G::RWB + j * 16 + (lane & 15)] = acc[i][j][r];
     }
-    __syncthreads();
+    if constexpr (VAR & 64) epi_lds_barrier(); else __syncthreads();
+    if constexpr (VAR & 128) {
+      if (chunk == 0) asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(st_e1)::"memory");
+    }
     for (int it = 0; it < EPI8_ROWS / RPP; ++it) {
       const int rl = it * RPP + rsub;
       const int row = m0 + chunk * EPI8_ROWS + rl;
@@ -1146,6 +1163,9 @@ __global__ __launch_bounds__(512, 1) void gemm_8ph(const bf16* __restrict__ A, c
         }
       }
     }
+    if constexpr (VAR & 128) {
+      if (chunk == 0) asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(st_e2)::"memory");
+    }
     if constexpr (TA == 2) {
       if (gn_part) {
         // per-(128-row chunk, group) sums: lanes sharing c8 inside a wave, then the 8 waves via LDS
@@ -1165,7 +1185,7 @@ __global__ __launch_bounds__(512, 1) void gemm_8ph(const bf16* __restrict__ A, c
             red[((wid * C8 + lane) * 8 + e) * 2 + 1] = gs_q[e];
           }
         }
-        __syncthreads();
+        if constexpr (VAR & 64) epi_lds_barrier(); else __syncthreads();
         const int gsz = N / 32;
         const int ngroups = min(BN, N - n0) / gsz;
         if ((int)threadIdx.x < ngroups && m0 + chunk * EPI8_ROWS < M) {
@@ -1182,7 +1202,21 @@ __global__ __launch_bounds__(512, 1) void gemm_8ph(const bf16* __restrict__ A, c
         }
       }
     }
-    __syncthreads();
+    if constexpr (VAR & 64) epi_lds_barrier(); else __syncthreads();
+  }
+  if constexpr (VAR & 32) {
+    unsigned long long st_end;
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(st_end)::"memory");
+    if ((threadIdx.x & 63) == 0 && blockIdx.x < 16 && blockIdx.y == 0 && blockIdx.z == 0) {
+      unsigned long long* o = g_uva_stamps + (blockIdx.x * 8 + (threadIdx.x >> 6)) * 5;
+      if constexpr (VAR & 128) {  // epilogue split: chunk-0 staging, chunk-0 stores, rest
+        o[0] = st_after_loop - st_entry; o[1] = st_e1 - st_after_loop; o[2] = st_e2 - st_e1; o[3] = st_end - st_e2;
+      } else {
+        o[0] = st_after_pro - st_entry; o[1] = st_after_loop - st_after_pro; o[2] = st_end - st_after_loop;
+        o[3] = st_entry;
+      }
+      o[4] = st_end;
+    }
   }
 }
 
@@ -1317,6 +1351,9 @@ static int launch_8ph(int ta, int tb, const void* A, const void* B, void* C, int
       case 9: G8V(9); break;
       case 16: G8V(16); break;
       case 12: G8V(12); break;
+      case 32: G8V(32); break;
+      case 96: G8V(96); break;
+      case 160: G8V(160); break;
       default: return -(int)hipErrorInvalidValue;
     }
   } else
