@@ -26,6 +26,7 @@
 //     stores, and the deterministic per-(128-pixel half, group) GroupNorm(32) partial sums of
 //     the stored output for the NEXT GroupNorm (uva_groupnorm_finalize_tiles, tile_rows 128).
 #include "common.h"
+#include <stdlib.h>
 
 #define CH_T 16
 #define CH_H 18
@@ -46,12 +47,23 @@ struct ConvHCfg {
   static constexpr int LDS_BYTES = MAIN_BYTES > EPI_BYTES ? MAIN_BYTES : EPI_BYTES;
 };
 
+// workgroup barrier ordering LDS only: the epilogue's global stores stay in flight across it
+// (__syncthreads drains vmcnt, i.e. waits for every store of the half before the next step)
+__device__ __forceinline__ void ch_lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
 __device__ __forceinline__ int ch_xcd_remap(int bid, int nblk) {
   int q = nblk / 8, r = nblk % 8, x = bid % 8;
   return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + bid / 8;
 }
 
-template <int BN, bool GN>
+// VAR (diagnostic builds only, 0 = production): 1 per-tile prologue / main-loop / epilogue s_memtime
+// stamps of the first 16 blocks (uva_debug_conv_stamps)
+__device__ unsigned long long g_uva_conv_stamps[16 * 8 * 4];
+template <int BN, bool GN, int VAR = 0>
 __global__ __launch_bounds__(512, 1) void conv3x3_halo(const bf16* __restrict__ in, const bf16* __restrict__ wt,
                                                        bf16* __restrict__ out, const float* __restrict__ bias,
                                                        const bf16* __restrict__ residual,
@@ -61,6 +73,8 @@ __global__ __launch_bounds__(512, 1) void conv3x3_halo(const bf16* __restrict__ 
                                                        int Co) {
   using G = ConvHCfg<BN>;
   extern __shared__ __attribute__((aligned(16))) char smem[];
+  unsigned long long st0 = 0, st1 = 0, st2 = 0;
+  if constexpr (VAR & 1) asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(st0)::"memory");
   bf16* halo = (bf16*)smem;
   bf16* bimg = halo + 2 * CH_HALO_ELEMS;
   const int tiles_x = W / CH_T, tiles_y = H / CH_T, ncb = Co / BN;
@@ -151,6 +165,7 @@ __global__ __launch_bounds__(512, 1) void conv3x3_halo(const bf16* __restrict__ 
   asm volatile("" ::: "memory");
 
   const int frow = lane & 15, fk = lane >> 4;
+  if constexpr (VAR & 1) asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(st1)::"memory");
   for (int cc = 0; cc < nch; ++cc) {
     const bf16* hcur = halo + (cc & 1) * CH_HALO_ELEMS;
     const bool more = cc + 1 < nch;
@@ -191,15 +206,36 @@ __global__ __launch_bounds__(512, 1) void conv3x3_halo(const bf16* __restrict__ 
     }
   }
 
+  if constexpr (VAR & 1) asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(st2)::"memory");
   // ---- epilogue: two 128-pixel halves (tile rows 0-7, 8-15) staged through LDS as fp32
   float* T = (float*)smem;
   constexpr int C8 = BN / 8, RPP = 512 / C8;
   const int c8 = tid % C8, rsub = tid / C8;
   const int col0 = n0 + c8 * 8;
   float bv[8];
+  if (bias) {
+    const float4 b0 = *(const float4*)(bias + col0), b1 = *(const float4*)(bias + col0 + 4);
+    bv[0] = b0.x; bv[1] = b0.y; bv[2] = b0.z; bv[3] = b0.w; bv[4] = b1.x; bv[5] = b1.y; bv[6] = b1.z; bv[7] = b1.w;
+  } else {
 #pragma unroll
-  for (int e = 0; e < 8; ++e) bv[e] = bias ? bias[col0 + e] : 0.f;
+    for (int e = 0; e < 8; ++e) bv[e] = 0.f;
+  }
   const int tiles_img = tiles_x * tiles_y;
+  // the tile's residual rows (both halves) are loaded up front, so the HBM latency overlaps the
+  // accumulator staging; loaded inside the store loop they serialised (one round trip per
+  // iteration: the stores to `out` kept the compiler from hoisting them) -- 19k ticks per tile
+  constexpr int NIT = 128 / RPP;
+  bf16x8 rres[2][NIT];
+  if (residual) {
+#pragma unroll
+    for (int half = 0; half < 2; ++half)
+#pragma unroll
+      for (int it = 0; it < NIT; ++it) {
+        const int rl = it * RPP + rsub;
+        const int oh = oh0 + half * 8 + (rl >> 4), ow = ow0 + (rl & 15);
+        rres[half][it] = *(const bf16x8*)(residual + (((long long)n * H + oh) * W + ow) * Co + col0);
+      }
+  }
 #pragma unroll
   for (int half = 0; half < 2; ++half) {
     if ((wm * G::FM) / 8 == half) {
@@ -211,11 +247,12 @@ __global__ __launch_bounds__(512, 1) void conv3x3_halo(const bf16* __restrict__ 
           for (int r = 0; r < 4; ++r)
             T[((wm * G::FM + f - half * 8) * 16 + fk * 4 + r) * G::TP + wn * (G::FN * 16) + g * 16 + frow] = acc[f][g][r];
     }
-    __syncthreads();
+    ch_lds_barrier();
     float gs[8], gq[8];
 #pragma unroll
     for (int e = 0; e < 8; ++e) gs[e] = gq[e] = 0.f;
-    for (int it = 0; it < 128 / RPP; ++it) {
+#pragma unroll
+    for (int it = 0; it < NIT; ++it) {
       const int rl = it * RPP + rsub;  // pixel inside the half: row half*8 + rl/16, column rl%16
       const int oh = oh0 + half * 8 + (rl >> 4), ow = ow0 + (rl & 15);
       const long long ob = (((long long)n * H + oh) * W + ow) * Co + col0;
@@ -223,7 +260,7 @@ __global__ __launch_bounds__(512, 1) void conv3x3_halo(const bf16* __restrict__ 
       const float4 b = *(const float4*)(T + rl * G::TP + c8 * 8 + 4);
       float v[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
       if (residual) {
-        const bf16x8 rv = *(const bf16x8*)(residual + ob);
+        const bf16x8 rv = rres[half][it];
 #pragma unroll
         for (int e = 0; e < 8; ++e) v[e] += bv[e], v[e] += (float)rv[e];
       } else {
@@ -259,24 +296,41 @@ __global__ __launch_bounds__(512, 1) void conv3x3_halo(const bf16* __restrict__ 
           red[((wid * C8 + lane) * 8 + e) * 2 + 1] = gq[e];
         }
       }
-      __syncthreads();
+      ch_lds_barrier();
+      // the tile's ngroups groups x (8 waves x gsz channels) partial pairs: 2 per thread, then a
+      // shuffle tree over the group's 512/ngroups consecutive lanes (a serial 32-thread loop over
+      // the 64 LDS values of a group cost ~6k cycles per half)
       const int gsz = Co / 32;
-      const int ngroups = BN / gsz;
-      if (tid < ngroups) {
-        float sum = 0.f, sq = 0.f;
-        for (int c = tid * gsz; c < (tid + 1) * gsz; ++c) {
-          for (int w = 0; w < 8; ++w) {
-            sum += red[((w * C8 + (c >> 3)) * 8 + (c & 7)) * 2 + 0];
-            sq += red[((w * C8 + (c >> 3)) * 8 + (c & 7)) * 2 + 1];
-          }
-        }
-        const int g = n0 / gsz + tid;
+      const int ngroups = BN / gsz;               // 32, 16 or 8 (Co = 128, 256, 512)
+      const int tpg = 512 / ngroups;              // 16, 32 or 64 lanes per group (inside one wave)
+      const int gl = tid / tpg, j = tid % tpg;
+      float sum = 0.f, sq = 0.f;
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const int idx = j * 2 + u, w = idx / gsz, c = gl * gsz + idx % gsz;
+        sum += red[((w * C8 + (c >> 3)) * 8 + (c & 7)) * 2 + 0];
+        sq += red[((w * C8 + (c >> 3)) * 8 + (c & 7)) * 2 + 1];
+      }
+      for (int o = 1; o < tpg; o <<= 1) {
+        sum += __shfl_xor(sum, o, 64);
+        sq += __shfl_xor(sq, o, 64);
+      }
+      if (j == 0) {
+        const int g = n0 / gsz + gl;
         const long long t128 = ((long long)n * tiles_img + (sp % tiles_img)) * 2 + half;
         gn_part[(t128 * 32 + g) * 2 + 0] = sum;
         gn_part[(t128 * 32 + g) * 2 + 1] = sq;
       }
     }
-    __syncthreads();
+    ch_lds_barrier();
+  }
+  if constexpr (VAR & 1) {
+    unsigned long long st3;
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(st3)::"memory");
+    if (lane == 0 && blockIdx.x < 16) {
+      unsigned long long* o = g_uva_conv_stamps + (blockIdx.x * 8 + wid) * 4;
+      o[0] = st1 - st0; o[1] = st2 - st1; o[2] = st3 - st2; o[3] = st3;
+    }
   }
 }
 
@@ -300,20 +354,22 @@ extern "C" int uva_conv3x3_halo(const void* in, const void* w, void* out, const 
   if ((gn_scale == nullptr) != (gn_shift == nullptr)) return (int)hipErrorInvalidValue;
   const long long nblk = (long long)Nimg * (H / CH_T) * (W / CH_T) * (Co / bn);
   if (nblk >= (1ll << 31)) return (int)hipErrorInvalidValue;
-#define CH_LAUNCH(BNV, GNV)                                                                                    \
+#define CH_LAUNCH(BNV, GNV, VARV)                                                                              \
   do {                                                                                                         \
     static bool attr = false;                                                                                  \
     const int lb = ConvHCfg<BNV>::LDS_BYTES;                                                                   \
     if (!attr) {                                                                                               \
-      (void)hipFuncSetAttribute((const void*)conv3x3_halo<BNV, GNV>, hipFuncAttributeMaxDynamicSharedMemorySize, lb); \
+      (void)hipFuncSetAttribute((const void*)conv3x3_halo<BNV, GNV, VARV>, hipFuncAttributeMaxDynamicSharedMemorySize, lb); \
       attr = true;                                                                                             \
     }                                                                                                          \
-    conv3x3_halo<BNV, GNV><<<dim3((unsigned)nblk), 512, lb, stream>>>(                                         \
+    conv3x3_halo<BNV, GNV, VARV><<<dim3((unsigned)nblk), 512, lb, stream>>>(                                   \
         (const bf16*)in, (const bf16*)w, (bf16*)out, bias, (const bf16*)residual, gn_scale, gn_shift, gn_silu, \
         gn_part, Nimg, H, W, Ci, Co);                                                                          \
   } while (0)
-  if (gn_scale) CH_LAUNCH(128, true);
-  else CH_LAUNCH(128, false);
+  static const int var = getenv("UVA_CONV_VAR") ? atoi(getenv("UVA_CONV_VAR")) : 0;
+  if (gn_scale) CH_LAUNCH(128, true, 0);
+  else if (var == 1) CH_LAUNCH(128, false, 1);
+  else CH_LAUNCH(128, false, 0);
 #undef CH_LAUNCH
   UVA_LAUNCH_CHECK();
   return 0;
@@ -450,4 +506,8 @@ extern "C" int uva_conv_in8(const void* in, const void* w, void* out, const floa
                                                            Nimg, H, W);
   UVA_LAUNCH_CHECK();
   return 0;
+}
+
+extern "C" int uva_debug_conv_stamps(unsigned long long* host) {
+  return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_uva_conv_stamps), sizeof(g_uva_conv_stamps));
 }
