@@ -5,7 +5,7 @@
 // (reference vae/vaekl.py:56-113, 246-273) together with the Normalize + nonlinearity that
 // precede them (vaekl.py:9-17, 94-104, 270-271): out = bias + residual + conv(silu(gn(x))).
 //
-// Work decomposition (one 512-thread workgroup per output tile, 1 workgroup / CU):
+// Work decomposition (one workgroup per output tile; TR = 8: 256 threads, 2 workgroups / CU):
 //   * output tile = 16 x 16 pixels x BN output channels (BN = 128 or 256);
 //   * K loop = (64-channel chunk cc) x (9 taps); per chunk the 18 x 18 x 64 input halo is
 //     loaded to registers at tap 0, normalised + SiLU'd (zero padding applied AFTER the
@@ -28,22 +28,29 @@
 #include "common.h"
 #include <stdlib.h>
 
-#define CH_T 16
-#define CH_H 18
+#define CH_T 16   // tile width (pixels)
+#define CH_W 18   // halo width
+#define CH_H 18   // conv_in halo (16 x 16 tile)
 #define CH_HPIX (CH_H * CH_H)
-#define CH_HALO_ELEMS (CH_HPIX * 64)
-#define CH_ROUNDS ((CH_HPIX * 8 + 511) / 512)
 
-template <int BN>
+// TR = tile rows: 16 (512 threads, 1 workgroup / CU) or 8 (256 threads, 2 workgroups / CU: the two
+// co-resident tiles drift apart, so one tile's prologue / epilogue HBM traffic runs under the
+// other's MFMA loop instead of every CU loading and storing in lockstep)
+template <int BN, int TR>
 struct ConvHCfg {
-  static constexpr int WM = BN == 256 ? 2 : 4, WN = 8 / WM;
-  static constexpr int FM = CH_T / WM;          // tile rows (16-pixel fragments) per wave
+  static constexpr int NTH = TR * 32, NW = NTH / 64;
+  static constexpr int WN = 2, WM = NW / WN;    // BN = 128: waves of 64 px x 64 co
+  static constexpr int FM = TR / WM;            // tile rows (16-pixel fragments) per wave
   static constexpr int FN = BN / WN / 16;       // 16-channel fragments per wave
+  static constexpr int HR = TR + 2;             // halo rows
+  static constexpr int HPIX = HR * CH_W;
+  static constexpr int HALO_ELEMS = HPIX * 64;
+  static constexpr int ROUNDS = (HPIX * 8 + NTH - 1) / NTH;
   static constexpr int BT = BN * 64;            // weight tile elements
-  static constexpr int NI = BT / 4096;          // DMA instructions per thread per weight tile
-  static constexpr int MAIN_BYTES = (2 * CH_HALO_ELEMS + 2 * BT) * 2;
+  static constexpr int NI = BT / (NW * 512);    // DMA instructions per thread per weight tile
+  static constexpr int MAIN_BYTES = (2 * HALO_ELEMS + 2 * BT) * 2;
   static constexpr int TP = BN + 4;             // epilogue fp32 pitch
-  static constexpr int EPI_BYTES = 128 * TP * 4 + 8 * (BN / 8) * 8 * 2 * 4;
+  static constexpr int EPI_BYTES = 128 * TP * 4 + NW * (BN / 8) * 8 * 2 * 4;
   static constexpr int LDS_BYTES = MAIN_BYTES > EPI_BYTES ? MAIN_BYTES : EPI_BYTES;
 };
 
@@ -63,27 +70,27 @@ __device__ __forceinline__ int ch_xcd_remap(int bid, int nblk) {
 // VAR (diagnostic builds only, 0 = production): 1 per-tile prologue / main-loop / epilogue s_memtime
 // stamps of the first 16 blocks (uva_debug_conv_stamps)
 __device__ unsigned long long g_uva_conv_stamps[16 * 8 * 4];
-template <int BN, bool GN, int VAR = 0>
-__global__ __launch_bounds__(512, 1) void conv3x3_halo(const bf16* __restrict__ in, const bf16* __restrict__ wt,
+template <int BN, bool GN, int VAR, int TR>
+__global__ __launch_bounds__(TR * 32, 16 / TR) void conv3x3_halo(const bf16* __restrict__ in, const bf16* __restrict__ wt,
                                                        bf16* __restrict__ out, const float* __restrict__ bias,
                                                        const bf16* __restrict__ residual,
                                                        const float* __restrict__ gn_scale,
                                                        const float* __restrict__ gn_shift, int gn_silu,
                                                        float* __restrict__ gn_part, int Nimg, int H, int W, int Ci,
                                                        int Co) {
-  using G = ConvHCfg<BN>;
+  using G = ConvHCfg<BN, TR>;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   unsigned long long st0 = 0, st1 = 0, st2 = 0;
   if constexpr (VAR & 1) asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(st0)::"memory");
   bf16* halo = (bf16*)smem;
-  bf16* bimg = halo + 2 * CH_HALO_ELEMS;
-  const int tiles_x = W / CH_T, tiles_y = H / CH_T, ncb = Co / BN;
+  bf16* bimg = halo + 2 * G::HALO_ELEMS;
+  const int tiles_x = W / CH_T, tiles_y = H / TR, ncb = Co / BN;
   const int nblk = Nimg * tiles_y * tiles_x * ncb;
   const int pid = ch_xcd_remap(blockIdx.x, nblk);
   const int cb = pid % ncb;
   const int sp = pid / ncb;  // spatial tile id, image-major
   const int tx = sp % tiles_x, ty = (sp / tiles_x) % tiles_y, n = sp / (tiles_x * tiles_y);
-  const int oh0 = ty * CH_T, ow0 = tx * CH_T, n0 = cb * BN;
+  const int oh0 = ty * TR, ow0 = tx * CH_T, n0 = cb * BN;
   const int K = 9 * Ci, nch = Ci / 64, S = nch * 9;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -106,15 +113,15 @@ __global__ __launch_bounds__(512, 1) void conv3x3_halo(const bf16* __restrict__ 
     }
   };
 
-  // ---- halo: thread t owns 16-B chunk c = t & 7 of pixels p = (t + 512 i) >> 3
+  // ---- halo: thread t owns 16-B chunk c = t & 7 of pixels p = (t + NTH i) >> 3
   const int hc = tid & 7;
-  bf16x8 hreg[CH_ROUNDS];
+  bf16x8 hreg[G::ROUNDS];
   float gsc[8], gsh[8];
   auto halo_load = [&](int cc) {
 #pragma unroll
-    for (int i = 0; i < CH_ROUNDS; ++i) {
-      const int p = min((tid + i * 512) >> 3, CH_HPIX - 1);
-      const int hy = p / CH_H, hx = p - hy * CH_H;
+    for (int i = 0; i < G::ROUNDS; ++i) {
+      const int p = min((tid + i * G::NTH) >> 3, G::HPIX - 1);
+      const int hy = p / CH_W, hx = p - hy * CH_W;
       const int ih = min(max(oh0 - 1 + hy, 0), H - 1), iw = min(max(ow0 - 1 + hx, 0), W - 1);  // clamped: always in bounds
       hreg[i] = *(const bf16x8*)(in + (((long long)n * H + ih) * W + iw) * Ci + cc * 64 + hc * 8);
     }
@@ -128,12 +135,12 @@ __global__ __launch_bounds__(512, 1) void conv3x3_halo(const bf16* __restrict__ 
     }
   };
   auto halo_store = [&](int hb) {
-    bf16* img = halo + hb * CH_HALO_ELEMS;
+    bf16* img = halo + hb * G::HALO_ELEMS;
 #pragma unroll
-    for (int i = 0; i < CH_ROUNDS; ++i) {
-      const int p = (tid + i * 512) >> 3;
-      if (p < CH_HPIX) {
-        const int hy = p / CH_H, hx = p - hy * CH_H;
+    for (int i = 0; i < G::ROUNDS; ++i) {
+      const int p = (tid + i * G::NTH) >> 3;
+      if (p < G::HPIX) {
+        const int hy = p / CH_W, hx = p - hy * CH_W;
         const int ih = oh0 - 1 + hy, iw = ow0 - 1 + hx;
         bf16x8 v = hreg[i];
         if (ih < 0 || ih >= H || iw < 0 || iw >= W) {
@@ -167,7 +174,7 @@ __global__ __launch_bounds__(512, 1) void conv3x3_halo(const bf16* __restrict__ 
   const int frow = lane & 15, fk = lane >> 4;
   if constexpr (VAR & 1) asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(st1)::"memory");
   for (int cc = 0; cc < nch; ++cc) {
-    const bf16* hcur = halo + (cc & 1) * CH_HALO_ELEMS;
+    const bf16* hcur = halo + (cc & 1) * G::HALO_ELEMS;
     const bool more = cc + 1 < nch;
 #pragma unroll 1
     for (int tap = 0; tap < 9; ++tap) {
@@ -183,7 +190,7 @@ __global__ __launch_bounds__(512, 1) void conv3x3_halo(const bf16* __restrict__ 
         bf16x8 fa[G::FM], fb[G::FN];
 #pragma unroll
         for (int f = 0; f < G::FM; ++f) {
-          const int p = (wm * G::FM + f + kh) * CH_H + frow + kw;
+          const int p = (wm * G::FM + f + kh) * CH_W + frow + kw;
           fa[f] = *(const bf16x8*)(hcur + p * 64 + ((c ^ (p & 7)) << 3));
         }
 #pragma unroll
@@ -207,9 +214,9 @@ __global__ __launch_bounds__(512, 1) void conv3x3_halo(const bf16* __restrict__ 
   }
 
   if constexpr (VAR & 1) asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(st2)::"memory");
-  // ---- epilogue: two 128-pixel halves (tile rows 0-7, 8-15) staged through LDS as fp32
+  // ---- epilogue: 128-pixel halves (tile rows 0-7 [, 8-15]) staged through LDS as fp32
   float* T = (float*)smem;
-  constexpr int C8 = BN / 8, RPP = 512 / C8;
+  constexpr int C8 = BN / 8, RPP = G::NTH / C8, NHALF = TR / 8;
   const int c8 = tid % C8, rsub = tid / C8;
   const int col0 = n0 + c8 * 8;
   float bv[8];
@@ -225,10 +232,10 @@ __global__ __launch_bounds__(512, 1) void conv3x3_halo(const bf16* __restrict__ 
   // accumulator staging; loaded inside the store loop they serialised (one round trip per
   // iteration: the stores to `out` kept the compiler from hoisting them) -- 19k ticks per tile
   constexpr int NIT = 128 / RPP;
-  bf16x8 rres[2][NIT];
+  bf16x8 rres[NHALF][NIT];
   if (residual) {
 #pragma unroll
-    for (int half = 0; half < 2; ++half)
+    for (int half = 0; half < NHALF; ++half)
 #pragma unroll
       for (int it = 0; it < NIT; ++it) {
         const int rl = it * RPP + rsub;
@@ -237,7 +244,7 @@ __global__ __launch_bounds__(512, 1) void conv3x3_halo(const bf16* __restrict__ 
       }
   }
 #pragma unroll
-  for (int half = 0; half < 2; ++half) {
+  for (int half = 0; half < NHALF; ++half) {
     if ((wm * G::FM) / 8 == half) {
 #pragma unroll
       for (int f = 0; f < G::FM; ++f)
@@ -279,7 +286,7 @@ __global__ __launch_bounds__(512, 1) void conv3x3_halo(const bf16* __restrict__ 
       }
     }
     if (gn_part) {
-      // per-column sums over the half's 128 pixels (lanes sharing c8, then the 8 waves via LDS)
+      // per-column sums over the half's 128 pixels (lanes sharing c8, then the NW waves via LDS)
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
 #pragma unroll
@@ -288,7 +295,7 @@ __global__ __launch_bounds__(512, 1) void conv3x3_halo(const bf16* __restrict__ 
           gq[e] += __shfl_xor(gq[e], o, 64);
         }
       }
-      float* red = T + 128 * G::TP;  // [8 waves][C8][8][2]
+      float* red = T + 128 * G::TP;  // [NW waves][C8][8][2]
       if (lane < C8) {
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
@@ -297,12 +304,12 @@ __global__ __launch_bounds__(512, 1) void conv3x3_halo(const bf16* __restrict__ 
         }
       }
       ch_lds_barrier();
-      // the tile's ngroups groups x (8 waves x gsz channels) partial pairs: 2 per thread, then a
-      // shuffle tree over the group's 512/ngroups consecutive lanes (a serial 32-thread loop over
+      // the tile's ngroups groups x (NW waves x gsz channels) partial pairs: 2 per thread, then a
+      // shuffle tree over the group's NTH/ngroups consecutive lanes (a serial 32-thread loop over
       // the 64 LDS values of a group cost ~6k cycles per half)
       const int gsz = Co / 32;
       const int ngroups = BN / gsz;               // 32, 16 or 8 (Co = 128, 256, 512)
-      const int tpg = 512 / ngroups;              // 16, 32 or 64 lanes per group (inside one wave)
+      const int tpg = G::NTH / ngroups;           // lanes per group (inside one wave)
       const int gl = tid / tpg, j = tid % tpg;
       float sum = 0.f, sq = 0.f;
 #pragma unroll
@@ -317,7 +324,7 @@ __global__ __launch_bounds__(512, 1) void conv3x3_halo(const bf16* __restrict__ 
       }
       if (j == 0) {
         const int g = n0 / gsz + gl;
-        const long long t128 = ((long long)n * tiles_img + (sp % tiles_img)) * 2 + half;
+        const long long t128 = ((long long)n * tiles_img + (sp % tiles_img)) * NHALF + half;
         gn_part[(t128 * 32 + g) * 2 + 0] = sum;
         gn_part[(t128 * 32 + g) * 2 + 1] = sq;
       }
@@ -352,24 +359,34 @@ extern "C" int uva_conv3x3_halo(const void* in, const void* w, void* out, const 
   const int bn = halo_bn(Nimg, H, W, Ci, Co);
   if (!bn || (((uintptr_t)in | (uintptr_t)w | (uintptr_t)out | (uintptr_t)residual) % 16)) return (int)hipErrorInvalidValue;
   if ((gn_scale == nullptr) != (gn_shift == nullptr)) return (int)hipErrorInvalidValue;
-  const long long nblk = (long long)Nimg * (H / CH_T) * (W / CH_T) * (Co / bn);
+  // TR = 8 (two co-resident 256-thread workgroups per CU) unless UVA_CONV_TR=16
+  static const int tr_env = getenv("UVA_CONV_TR") ? atoi(getenv("UVA_CONV_TR")) : 8;
+  const int tr = tr_env == 16 ? 16 : 8;
+  const long long nblk = (long long)Nimg * (H / tr) * (W / CH_T) * (Co / bn);
   if (nblk >= (1ll << 31)) return (int)hipErrorInvalidValue;
-#define CH_LAUNCH(BNV, GNV, VARV)                                                                              \
+#define CH_LAUNCH(BNV, GNV, VARV, TRV)                                                                         \
   do {                                                                                                         \
     static bool attr = false;                                                                                  \
-    const int lb = ConvHCfg<BNV>::LDS_BYTES;                                                                   \
+    const int lb = ConvHCfg<BNV, TRV>::LDS_BYTES;                                                              \
     if (!attr) {                                                                                               \
-      (void)hipFuncSetAttribute((const void*)conv3x3_halo<BNV, GNV, VARV>, hipFuncAttributeMaxDynamicSharedMemorySize, lb); \
+      (void)hipFuncSetAttribute((const void*)conv3x3_halo<BNV, GNV, VARV, TRV>,                               \
+                                hipFuncAttributeMaxDynamicSharedMemorySize, lb);                               \
       attr = true;                                                                                             \
     }                                                                                                          \
-    conv3x3_halo<BNV, GNV, VARV><<<dim3((unsigned)nblk), 512, lb, stream>>>(                                   \
+    conv3x3_halo<BNV, GNV, VARV, TRV><<<dim3((unsigned)nblk), TRV * 32, lb, stream>>>(                         \
         (const bf16*)in, (const bf16*)w, (bf16*)out, bias, (const bf16*)residual, gn_scale, gn_shift, gn_silu, \
         gn_part, Nimg, H, W, Ci, Co);                                                                          \
   } while (0)
   static const int var = getenv("UVA_CONV_VAR") ? atoi(getenv("UVA_CONV_VAR")) : 0;
-  if (gn_scale) CH_LAUNCH(128, true, 0);
-  else if (var == 1) CH_LAUNCH(128, false, 1);
-  else CH_LAUNCH(128, false, 0);
+  if (tr == 16) {
+    if (gn_scale) CH_LAUNCH(128, true, 0, 16);
+    else if (var == 1) CH_LAUNCH(128, false, 1, 16);
+    else CH_LAUNCH(128, false, 0, 16);
+  } else {
+    if (gn_scale) CH_LAUNCH(128, true, 0, 8);
+    else if (var == 1) CH_LAUNCH(128, false, 1, 8);
+    else CH_LAUNCH(128, false, 0, 8);
+  }
 #undef CH_LAUNCH
   UVA_LAUNCH_CHECK();
   return 0;

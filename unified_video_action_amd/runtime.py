@@ -1,6 +1,7 @@
 """Process-wide runtime settings of the HIP path: compute precision and the per-call
 dropout seeds (counter-based masks need a distinct seed per op per step)."""
 import itertools
+import os
 
 import torch
 
@@ -9,6 +10,9 @@ class _Runtime:
     def __init__(self):
         self.compute_dtype = torch.bfloat16   # GEMM/attention operand dtype ("bf16" bench mode)
         self.flash_attention = True           # bf16 fused attention; False -> materialised GEMM+softmax
+        # VAE ResnetBlock: GroupNorm+SiLU applied inside the halo conv's input staging (True) or as
+        # a separate apply pass (False); UVA_VAE_GN_IN_CONV=0/1 overrides
+        self.vae_gn_in_conv = os.environ.get("UVA_VAE_GN_IN_CONV", "1") == "1"
         self._seed_base = 0x5EED
         self._ctr = itertools.count()
         # attention dropout masks: per Block the (B, N, H, p) of its last training forward, and the

@@ -22,7 +22,7 @@ import torch
 import torch.nn as nn
 
 from ..native import ops
-from ..runtime import cdt
+from ..runtime import RT, cdt
 
 F32 = torch.float32
 
@@ -144,6 +144,10 @@ class AutoencoderKL(nn.Module):
     def _fused(self):
         return cdt() == torch.bfloat16
 
+    def _gn_in_conv(self, n, H, W, ci, co):
+        return (self._fused() and RT.vae_gn_in_conv and
+                ops.conv_fuses_gn(n, H, W, ci, co, 3, 1, torch.bfloat16))
+
     def _gn(self, x, stats, norm, n, hw, c):
         sc = torch.empty(n, c, dtype=F32, device=x.device)
         sh = torch.empty(n, c, dtype=F32, device=x.device)
@@ -184,12 +188,14 @@ class AutoencoderKL(nn.Module):
 
     def _resblock(self, P, name, blk, x, xs_stats, n, H, W):
         c_in, c_out = blk.in_channels, blk.out_channels
-        # the halo conv kernel can apply GN+SiLU while staging its input (ops.conv_fuses_gn), but that
-        # VALU work is not hidden under its MFMAs (measured: 8.8 ms vs 5.5 + 1.6 ms for the level-0
-        # conv + a separate vectorised apply pass), so the fused path applies GN+SiLU once per element
-        a, g1 = self._norm_act(x, xs_stats, blk.norm1, n, H * W, c_in)
+        # GN+SiLU either inside the halo conv's input staging (in_conv: no separate apply pass; with
+        # two co-resident workgroups per CU that VALU work runs under the other tile's MFMAs) or as
+        # one vectorised apply pass per element (RT.vae_gn_in_conv = False)
+        f1 = self._gn_in_conv(n, H, W, c_in, c_out)
+        a, g1 = self._norm_act(x, xs_stats, blk.norm1, n, H * W, c_in, in_conv=f1)
         h, _, _, hs = self._conv(P, name + ".conv1", a, n, H, W, gn=g1, stats=True)
-        a2, g2 = self._norm_act(h, hs, blk.norm2, n, H * W, c_out)
+        f2 = self._gn_in_conv(n, H, W, c_out, c_out)
+        a2, g2 = self._norm_act(h, hs, blk.norm2, n, H * W, c_out, in_conv=f2)
         xs = self._conv(P, name + ".nin_shortcut", x, n, H, W)[0] if c_in != c_out else x
         out, _, _, os_ = self._conv(P, name + ".conv2", a2, n, H, W, gn=g2, residual=xs, stats=True)
         return out, os_
