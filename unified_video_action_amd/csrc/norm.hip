@@ -240,6 +240,50 @@ __global__ __launch_bounds__(256) void colsum_kernel(const T* __restrict__ in, l
   }
 }
 
+// second stage of the two-level column sums: out[c] (+)= sum_r part[r][c] over a short, wide fp32
+// partial matrix (rows = #row blocks of the first stage).  256 threads = 8 float4 column groups x
+// 32 row lanes per block; grid (cols/32, 2) reduces two matrices (dw, db) in one launch.  (The
+// 64-column scalar form ran 12 blocks for D = 768 with a 128-deep dependent chain each: 34 us.)
+__global__ __launch_bounds__(256) void colsum_partials_kernel(const float* __restrict__ p0, const float* __restrict__ p1,
+                                                              float* __restrict__ o0, float* __restrict__ o1, int rows,
+                                                              int cols, int accum) {
+  const float* in = blockIdx.y ? p1 : p0;
+  float* out = blockIdx.y ? o1 : o0;
+  __shared__ float4 red[32][8];
+  const int cg = threadIdx.x & 7, rl = threadIdx.x >> 3;
+  const int c = blockIdx.x * 32 + cg * 4;
+  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (c < cols) {
+#pragma unroll 4
+    for (int r = rl; r < rows; r += 32) {
+      const float4 v = *(const float4*)(in + (long long)r * cols + c);
+      acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
+    }
+  }
+  red[rl][cg] = acc;
+  __syncthreads();
+  if (rl < 4 && c < cols) {  // 4 x 8 threads: one column each, fixed summation order
+    const int cc = c + rl;
+    float t = 0.f;
+#pragma unroll 8
+    for (int k = 0; k < 32; ++k) {
+      const float4 v = red[k][cg];
+      t += rl == 0 ? v.x : (rl == 1 ? v.y : (rl == 2 ? v.z : v.w));
+    }
+    out[cc] = accum ? out[cc] + t : t;
+  }
+}
+
+static void colsum_partials(const float* p0, const float* p1, float* o0, float* o1, int rows, int cols, int accum,
+                            hipStream_t stream) {
+  if (cols % 4 == 0) {
+    colsum_partials_kernel<<<dim3((cols + 31) / 32, p1 ? 2 : 1), 256, 0, stream>>>(p0, p1, o0, o1, rows, cols, accum);
+  } else {
+    colsum_kernel<float><<<dim3((cols + 63) / 64), 256, 0, stream>>>(p0, cols, o0, rows, cols, accum);
+    if (p1) colsum_kernel<float><<<dim3((cols + 63) / 64), 256, 0, stream>>>(p1, cols, o1, rows, cols, accum);
+  }
+}
+
 // row-partitioned column sum for tall inputs: part[blk][c] = sum over blk's rows
 template <typename T>
 __global__ __launch_bounds__(256) void colsum_part_kernel(const T* __restrict__ in, long long ld,
@@ -367,9 +411,7 @@ extern "C" int uva_layernorm_bwd(int in_dtype, int out_dtype, const void* x, con
     return (int)hipErrorInvalidValue;
   UVA_LAUNCH_CHECK();
   if (dw) {
-    dim3 g2((D + 63) / 64);
-    colsum_kernel<float><<<g2, 256, 0, stream>>>(pw, D, dw, nblk, D, accum_wb);
-    if (db) colsum_kernel<float><<<g2, 256, 0, stream>>>(pb, D, db, nblk, D, accum_wb);
+    colsum_partials(pw, db ? pb : nullptr, dw, db, nblk, D, accum_wb, stream);
     UVA_LAUNCH_CHECK();
   }
   return 0;
@@ -398,7 +440,7 @@ extern "C" int uva_colsum(int dtype, const void* in, long long ld, float* out, i
   if (nb > 1 && workspace) {
     if (dtype == UVA_DT_BF16) colsum_part_kernel<bf16><<<g1, 256, 0, stream>>>((const bf16*)in, ld, workspace, rows, cols, rpb);
     else colsum_part_kernel<float><<<g1, 256, 0, stream>>>((const float*)in, ld, workspace, rows, cols, rpb);
-    colsum_kernel<float><<<dim3((cols + 63) / 64), 256, 0, stream>>>(workspace, cols, out, nb, cols, accum);
+    colsum_partials(workspace, nullptr, out, nullptr, nb, cols, accum, stream);
   } else {
     if (dtype == UVA_DT_BF16) colsum_kernel<bf16><<<dim3((cols + 63) / 64), 256, 0, stream>>>((const bf16*)in, ld, out, rows, cols, accum);
     else colsum_kernel<float><<<dim3((cols + 63) / 64), 256, 0, stream>>>((const float*)in, ld, out, rows, cols, accum);
