@@ -65,6 +65,7 @@ int uva_gemm(int in_dtype, int out_dtype, int ta, int tb, const void* A, const v
  * [16 blocks][8 waves][read+issue, barrier-1, mfma issue, barrier-2, loop total]. */
 int uva_debug_gemm8_stamps(unsigned long long* host);
 int uva_debug_conv_stamps(unsigned long long* host);
+int uva_debug_conv_occupancy(int tr, int gn);
 long long uva_gemm_plan(int in_dtype, int ta, int tb, int M, int N, int K, int batch, int gn_prologue,
                         long long ws_floats);
 int uva_conv2d(int dtype, const void* in, const void* w, void* out, const float* bias, const void* residual, int Nimg,

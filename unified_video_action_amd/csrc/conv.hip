@@ -528,3 +528,20 @@ extern "C" int uva_conv_in8(const void* in, const void* w, void* out, const floa
 extern "C" int uva_debug_conv_stamps(unsigned long long* host) {
   return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_uva_conv_stamps), sizeof(g_uva_conv_stamps));
 }
+
+// resident workgroups per CU of the halo conv variant (tile rows tr, with/without GN prologue)
+extern "C" int uva_debug_conv_occupancy(int tr, int gn) {
+  int nb = -1;
+#define CH_OCC(GNV, TRV)                                                                                       \
+  do {                                                                                                         \
+    const int lb = ConvHCfg<128, TRV>::LDS_BYTES;                                                              \
+    (void)hipFuncSetAttribute((const void*)conv3x3_halo<128, GNV, 0, TRV>,                                     \
+                              hipFuncAttributeMaxDynamicSharedMemorySize, lb);                                 \
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, (const void*)conv3x3_halo<128, GNV, 0, TRV>, TRV * 32, \
+                                                     lb) != hipSuccess) nb = -1;                               \
+  } while (0)
+  if (tr == 16) { if (gn) CH_OCC(true, 16); else CH_OCC(false, 16); }
+  else { if (gn) CH_OCC(true, 8); else CH_OCC(false, 8); }
+#undef CH_OCC
+  return nb;
+}
