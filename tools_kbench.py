@@ -86,10 +86,13 @@ def conv_bench():
         res = torch.randn(n, H, H, Co, device=dev).to(torch.bfloat16)
         bias = torch.randn(Co, device=dev)
         part = torch.empty(n * H * H // 128, 32, 2, device=dev)
+        tg = timeit(lambda: ops.conv2d(x, w, out, n, H, H, Ci, Co, 3, 1, 1, 1, H, H, gn_scale=sc, gn_shift=sh), iters=5)
+        te = timeit(lambda: ops.conv2d(x, w, out, n, H, H, Ci, Co, 3, 1, 1, 1, H, H, bias=bias, residual=res,
+                                       gn_part=part), iters=5)
         t2 = timeit(lambda: ops.conv2d(x, w, out, n, H, H, Ci, Co, 3, 1, 1, 1, H, H, bias=bias, residual=res,
                                        gn_scale=sc, gn_shift=sh, gn_part=part), iters=5)
-        print(f"conv3x3 n{n} {H}x{H} Ci{Ci} Co{Co}: {t:.2f} ms {fl/t/1e9:.0f} TF   "
-              f"+GN/SiLU prologue, bias, residual, GN stats: {t2:.2f} ms {fl/t2/1e9:.0f} TF")
+        print(f"conv3x3 n{n} {H}x{H} Ci{Ci} Co{Co}: plain {t:.2f} ms {fl/t/1e9:.0f} TF | GN/SiLU prologue {tg:.2f} | "
+              f"bias+res+GN-stats epilogue {te:.2f} | all {t2:.2f} ms {fl/t2/1e9:.0f} TF")
 
 
 if __name__ == "__main__" and len(sys.argv) > 1 and sys.argv[1] == "conv":

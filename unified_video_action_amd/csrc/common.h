@@ -107,9 +107,15 @@ __device__ __forceinline__ float gelu_erf_grad(float x) {
   float pdf = 0.39894228040143268f * __expf(-0.5f * x * x);
   return cdf + x * pdf;
 }
-__device__ __forceinline__ float silu(float x) { return x / (1.0f + __expf(-x)); }
+// sigmoid as v_exp_f32 + v_rcp_f32 (1 ulp each): a plain `x / (1 + e)` compiles to the IEEE division
+// sequence (2 x v_div_scale, v_div_fmas, v_div_fixup, v_rcp + 4 FMAs) -- 3x the VALU work of the
+// GroupNorm+SiLU staging in the halo conv
+__device__ __forceinline__ float sigmoid_fast(float x) {
+  return __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(-1.4426950408889634f * x));
+}
+__device__ __forceinline__ float silu(float x) { return x * sigmoid_fast(x); }
 __device__ __forceinline__ float silu_grad(float x) {
-  float s = 1.0f / (1.0f + __expf(-x));
+  const float s = sigmoid_fast(x);
   return s * (1.0f + x * (1.0f - s));
 }
 __device__ __forceinline__ float apply_act(int act, float x) {
