@@ -101,10 +101,25 @@ static inline void uva_drop_params(float p, uint32_t* thresh, float* scale) {
 #define ACT_SILU 2
 #define ACT_RELU 3
 
-__device__ __forceinline__ float gelu_erf(float x) { return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f)); }
+// erf by Abramowitz & Stegun 7.1.26 (|error| <= 1.5e-7, far below the bf16 rounding of every GELU
+// output here): one v_rcp_f32 + one v_exp_f32 + 8 FMA-class ops, branch-free.  The library erff is
+// a branchy polynomial ~3x the VALU work; in the fc1 GEMM epilogue (32768 x 3072 GELUs per block)
+// it cost +85 us over the bias-only epilogue (313 vs 227 us).
+__device__ __forceinline__ float erf_fast(float x) {
+  const float ax = fabsf(x);
+  const float t = __builtin_amdgcn_rcpf(fmaf(0.3275911f, ax, 1.0f));
+  float p = fmaf(1.061405429f, t, -1.453152027f);
+  p = fmaf(p, t, 1.421413741f);
+  p = fmaf(p, t, -0.284496736f);
+  p = fmaf(p, t, 0.254829592f);
+  p *= t;
+  const float e = __builtin_amdgcn_exp2f(-1.4426950408889634f * ax * ax);
+  return copysignf(fmaf(-p, e, 1.0f), x);
+}
+__device__ __forceinline__ float gelu_erf(float x) { return 0.5f * x * (1.0f + erf_fast(x * 0.70710678118654752f)); }
 __device__ __forceinline__ float gelu_erf_grad(float x) {
-  float cdf = 0.5f * (1.0f + erff(x * 0.70710678118654752f));
-  float pdf = 0.39894228040143268f * __expf(-0.5f * x * x);
+  const float cdf = 0.5f * (1.0f + erf_fast(x * 0.70710678118654752f));
+  const float pdf = 0.39894228040143268f * __builtin_amdgcn_exp2f(-0.72134752044448170f * x * x);
   return cdf + x * pdf;
 }
 // sigmoid as v_exp_f32 + v_rcp_f32 (1 ulp each): a plain `x / (1 + e)` compiles to the IEEE division
