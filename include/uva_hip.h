@@ -49,7 +49,19 @@ int uva_gemm(int in_dtype, int out_dtype, int ta, int tb, const void* A, const v
 /* res_dtype: dtype of `residual`; gate (dtype gate_dtype, ld ldg) multiplies the value after
  * dropout and before the residual add (adaLN: x + gate * mlp(h), diffusion_loss.py:163-167). */
 /* workspace (fp32, ws_floats) enables deterministic split-K for few-tile / long-K products
- * (the dW GEMMs, K = tokens); pass NULL/0 to disable. */
+ * (the dW GEMMs, K = tokens); pass NULL/0 to disable.
+ * Epilogue-free bf16 products (no bias / residual / aux / act / dropout / gate, batch 1, alpha 1,
+ * beta 0 or 1: the backward's dX and dW GEMMs) are routed to hipBLASLt when uva_lt_enabled(). */
+
+/* ---- hipBLASLt route for plain bf16 GEMMs (blaslt.hip) ---------------------------------
+ * Same operand convention as uva_gemm (bf16 A/B, fp32 accumulate, out_dtype bf16 or fp32,
+ * C = alpha * op(A) op(B) + beta * C).  Returns 0, -1 when the library has no algorithm for
+ * the shape (uva_gemm then uses its own kernels), or an error code.  uva_lt_mode(0/1) switches
+ * the route off/on (default from UVA_GEMM_LIB, on) and returns the previous mode (-1 = unset). */
+int uva_lt_gemm(int out_dtype, int ta, int tb, const void* A, const void* B, void* C, int M, int N, int K,
+                long long lda, long long ldb, long long ldc, float alpha, float beta, hipStream_t stream);
+int uva_lt_mode(int mode);
+int uva_lt_enabled();
 
 /* ---- convolution as implicit GEMM over NHWC (bf16: MFMA, fp32: VALU) -----------------
  * out[n,oh,ow,co] = bias[co] + residual + sum_{kh,kw,ci} act(in[n,ih,iw,ci]) w[co][kh][kw][ci]

@@ -21,8 +21,10 @@ def rel_err(a, b):
 
 @pytest.fixture(scope="module", autouse=True)
 def _seed():
-    from unified_video_action_amd.native import ops  # noqa: F401 -- fails loudly without the .so
+    from unified_video_action_amd.native import ops  # fails loudly without the .so
     torch.manual_seed(0)
+    with ops.gemm_library("kernels"):  # these tests exercise the hand-written kernels, not hipBLASLt
+        yield
 
 
 def _stored(op, t_flag):

@@ -16,6 +16,11 @@
 //  * gemm_generic    -- fp32 FMA on the VALU, any shape / dtype; the fp32 parity
 //    path and the tiny-K/N projections (K = 2, 4, 10 ...).
 #include "common.h"
+#include "blaslt.h"
+#include <map>
+#include <mutex>
+#include <tuple>
+#include <stdio.h>
 #include <stdlib.h>
 
 struct EpiParams {
@@ -1508,6 +1513,79 @@ static int gemm_dispatch(int in_dtype, int out_dtype, int ta, int tb, const void
   return launch_generic<float, bf16>(ta, tb, A, B, C, M, N, K, lda, ldb, ldc, batch, bs, ep, cp, stream);
 }
 
+extern "C" int uva_lt_enabled();
+
+// Epilogue-free bf16 products: once per shape, time this file's kernel against the hipBLASLt
+// heuristic's first algorithms (blaslt.hip) on a scratch output and keep the fastest (the library
+// wins the dX products by 10-40 %, its first pick loses the long-K dW products by 1.5-3x).
+// Returns 0 when the library ran, -1 when this file's kernels are the choice, or an error code.
+static int plain_gemm_tuned(int out_dtype, int ta, int tb, const void* A, const void* B, void* C, int M, int N,
+                            int K, long long lda, long long ldb, long long ldc, float beta, const BatchStrides& bs,
+                            const EpiParams& ep, float* ws, long long ws_floats, hipStream_t stream) {
+  const LtShape sh{out_dtype, ta, tb, M, N, K, lda, ldb, ldc, beta != 0.f};
+  using Key = std::tuple<int, int, int, int, int, int, long long, long long, long long, int, int, int>;
+  static std::map<Key, int> choice;
+  static std::mutex mu;
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  const Key key{out_dtype, ta, tb, M, N, K, lda, ldb, ldc, beta != 0.f, dev, uva_lt_enabled()};
+  int pick;
+  {
+    std::lock_guard<std::mutex> lock(mu);
+    auto it = choice.find(key);
+    pick = it == choice.end() ? -2 : it->second;
+  }
+  if (pick == -2) {
+    const int n = lt_prepare(sh, 8);
+    pick = -1;
+    if (n > 0 && uva_lt_enabled() == 2) {
+      pick = 0;  // heuristic only
+    } else if (n > 0) {
+      const size_t esz = out_dtype == UVA_DT_BF16 ? 2 : 4;
+      const size_t bytes = (size_t)ldc * M * esz;
+      void* scratch = nullptr;
+      if (hipMalloc(&scratch, bytes) != hipSuccess) return (int)hipErrorOutOfMemory;
+      (void)hipMemsetAsync(scratch, 0, bytes, stream);
+      hipEvent_t e0, e1;
+      (void)hipEventCreate(&e0);
+      (void)hipEventCreate(&e1);
+      auto time_it = [&](auto&& run) -> float {
+        if (run() != 0) return 1e30f;  // warm (first use loads the code object)
+        (void)hipEventRecord(e0, stream);
+        for (int i = 0; i < 3; ++i) run();
+        (void)hipEventRecord(e1, stream);
+        (void)hipEventSynchronize(e1);
+        float ms = 0.f;
+        (void)hipEventElapsedTime(&ms, e0, e1);
+        return ms / 3.f;
+      };
+      ConvParams cp{};
+      float best = time_it([&]() {
+        return gemm_dispatch(UVA_DT_BF16, out_dtype, ta, tb, A, B, scratch, M, N, K, lda, ldb, ldc, 1, bs, ep, cp, 0,
+                             ws, ws_floats, stream);
+      });
+      const float own = best;
+      for (int i = 0; i < n; ++i) {
+        const float t = time_it([&]() { return lt_run(sh, i, A, B, scratch, scratch, 1.f, beta, stream); });
+        if (t < best) {
+          best = t;
+          pick = i;
+        }
+      }
+      (void)hipEventDestroy(e0);
+      (void)hipEventDestroy(e1);
+      (void)hipFree(scratch);
+      if (getenv("UVA_GEMM_TUNE_LOG"))
+        fprintf(stderr, "[uva gemm tune] ta%d tb%d M%d N%d K%d out%d beta%d: own %.1f us, pick %d (%.1f us)\n", ta,
+                tb, M, N, K, out_dtype, beta != 0.f, own * 1e3f, pick, best * 1e3f);
+    }
+    std::lock_guard<std::mutex> lock(mu);
+    choice[key] = pick;
+  }
+  if (pick < 0) return -1;
+  return lt_run(sh, pick, A, B, C, C, 1.f, beta, stream);
+}
+
 extern "C" int uva_gemm(int in_dtype, int out_dtype, int ta, int tb, const void* A, const void* B, void* C, int M,
                         int N, int K, long long lda, long long ldb, long long ldc, int batch, int batch_inner,
                         long long sAo, long long sAi, long long sBo, long long sBi, long long sCo, long long sCi,
@@ -1523,6 +1601,14 @@ extern "C" int uva_gemm(int in_dtype, int out_dtype, int ta, int tb, const void*
   ep.gate = gate;
   ep.ldg = ldg;
   ep.gate_dt = gate_dtype;
+  // epilogue-free bf16 products (the backward's dX / dW): this file's kernel or hipBLASLt, whichever
+  // timed faster for the shape (plain_gemm_tuned)
+  if (in_dtype == UVA_DT_BF16 && batch == 1 && !force_generic && !bias && !residual && !aux && act == 0 &&
+      !(drop_p > 0.f) && !gate && alpha == 1.f && (beta == 0.f || beta == 1.f) && uva_lt_enabled()) {
+    const int r = plain_gemm_tuned(out_dtype, ta, tb, A, B, C, M, N, K, lda, ldb, ldc, beta, bs, ep, workspace,
+                                   ws_floats, stream);
+    if (r >= 0) return r;
+  }
   ConvParams cp{};
   return gemm_dispatch(in_dtype, out_dtype, ta, tb, A, B, C, M, N, K, lda, ldb, ldc, batch, bs, ep, cp, force_generic,
                        workspace, ws_floats, stream);
