@@ -127,26 +127,41 @@ __global__ void posterior_kernel(const void* __restrict__ mom, int mdt, const fl
   }
 }
 
-// finalize fused (conv-epilogue) GroupNorm partials: part[tile][32][2], tiles_per_img tiles per image
-__global__ void gn_finalize_tiles_kernel(const float* __restrict__ part, int tiles_per_img, long long cnt_per_group,
-                                         int C, const float* __restrict__ gamma, const float* __restrict__ beta,
-                                         float eps, float* __restrict__ scale, float* __restrict__ shift, int Nimg) {
-  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= (long long)Nimg * C) return;
-  const int n = i / C, c = i % C, gs = C / 32, g = c / gs;
+// finalize fused (conv-epilogue) GroupNorm partials: part[tile][32][2], tiles_per_img tiles per image.
+// One wave per (image, group): lanes stride over the image's tiles (fp64 sums: E[x^2] - mean^2
+// cancels), a wave reduction, then the group's C/32 channels get scale/shift.  (One thread per
+// channel, each summing all tiles serially, took 40 us per call at the level-0 shape.)
+__global__ __launch_bounds__(256) void gn_finalize_tiles_kernel(const float* __restrict__ part, int tiles_per_img,
+                                                                long long cnt_per_group, int C,
+                                                                const float* __restrict__ gamma,
+                                                                const float* __restrict__ beta, float eps,
+                                                                float* __restrict__ scale, float* __restrict__ shift,
+                                                                int Nimg) {
+  const int w = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (w >= Nimg * 32) return;
+  const int n = w >> 5, g = w & 31, gs = C / 32;
+  const float2* p = (const float2*)part + (long long)n * tiles_per_img * 32 + g;
   double s = 0.0, q = 0.0;
-  const float* p = part + ((long long)n * tiles_per_img * 32 + g) * 2;
-  for (int t = 0; t < tiles_per_img; ++t) {
-    s += p[(long long)t * 64];
-    q += p[(long long)t * 64 + 1];
+  for (int t = lane; t < tiles_per_img; t += 64) {
+    const float2 v = p[(long long)t * 32];
+    s += v.x;
+    q += v.y;
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    s += __shfl_xor(s, o, 64);
+    q += __shfl_xor(q, o, 64);
   }
   const double mean = s / cnt_per_group;
   double var = q / cnt_per_group - mean * mean;
   if (var < 0) var = 0;
   const float rstd = (float)(1.0 / sqrt(var + (double)eps));
-  const float sc = gamma[c] * rstd;
-  scale[i] = sc;
-  shift[i] = beta[c] - (float)mean * sc;
+  for (int j = lane; j < gs; j += 64) {
+    const int c = g * gs + j;
+    const float sc = gamma[c] * rstd;
+    scale[(long long)n * C + c] = sc;
+    shift[(long long)n * C + c] = beta[c] - (float)mean * sc;
+  }
 }
 
 // y = act(x * scale[n][c] + shift[n][c]), NHWC bf16, 8 channels per thread
@@ -218,8 +233,8 @@ extern "C" int uva_groupnorm_finalize_tiles(const float* part, int Nimg, int HW,
                                             const float* gamma, const float* beta, float eps, float* scale,
                                             float* shift, hipStream_t s) {
   if (HW % tile_rows != 0 || C % 32 != 0) return (int)hipErrorInvalidValue;
-  gn_finalize_tiles_kernel<<<gridn((long long)Nimg * C), 256, 0, s>>>(part, HW / tile_rows, (long long)HW * (C / 32), C,
-                                                                       gamma, beta, eps, scale, shift, Nimg);
+  gn_finalize_tiles_kernel<<<dim3((unsigned)((Nimg * 32 + 3) / 4)), 256, 0, s>>>(
+      part, HW / tile_rows, (long long)HW * (C / 32), C, gamma, beta, eps, scale, shift, Nimg);
   UVA_LAUNCH_CHECK();
   return 0;
 }

@@ -204,7 +204,14 @@ class AutoencoderKL(nn.Module):
         C = x.shape[-1]
         L = H * W
         g = self._gn(x, xs_stats, blk.norm, n, L, C)
-        qkv = self._conv(P, name + ".qkv", x, n, H, W, gn=g, gn_silu=False)[0]  # [n, H, W, 3C]; 1x1: prologue once
+        if self._fused():
+            # one GN-apply pass, then the 1x1 conv as a plain LDS-DMA GEMM (a GN prologue forces the
+            # register-staged kernel: 235 TFLOP/s at this shape)
+            xn = torch.empty_like(x)
+            ops.groupnorm_apply(x, g[0], g[1], xn, n, L, C, False)
+            qkv = self._conv(P, name + ".qkv", xn, n, H, W)[0]  # [n, H, W, 3C]
+        else:
+            qkv = self._conv(P, name + ".qkv", x, n, H, W, gn=g, gn_silu=False)[0]
         q = qkv.reshape(n * L, 3 * C)
         S = torch.empty(n, L, L, dtype=x.dtype, device=x.device)
         ops.gemm(q, q[:, C:], S, L, L, C, 3 * C, 3 * C, L, 0, 0, batch=n, sA=(L * 3 * C, 0), sB=(L * 3 * C, 0),
