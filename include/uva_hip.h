@@ -106,9 +106,10 @@ int uva_conv_in8(const void* in, const void* w, void* out, const float* bias, in
 int uva_layernorm_fwd(int in_dtype, int out_dtype, const void* x, const float* w, const float* b, const void* scale,
                       const void* shift, long long ldm, void* y, float* mean, float* rstd, int rows, int D, float eps,
                       hipStream_t stream);
+/* dy: dy_dtype fp32 or bf16 (the consuming GEMM's bf16 dX, autocast semantics) */
 int uva_layernorm_bwd(int in_dtype, int out_dtype, const void* x, const float* w, const float* b, const void* scale,
                       long long ldm,
-                      const float* dy, const float* mean, const float* rstd, const float* dx_base, float* dx,
+                      const void* dy, int dy_dtype, const float* mean, const float* rstd, const float* dx_base, float* dx,
                       int accum, void* dscale,
                       void* dshift, float* dw, float* db, int accum_wb, float* workspace, int rows, int D,
                       hipStream_t stream);

@@ -159,6 +159,13 @@ def test_layernorm_affine_fwd_bwd(D, io):
     assert rel_err(dx - 0.5, xr.grad) < 1e-4
     assert rel_err(dw, wr.grad) < 1e-4
     assert rel_err(db, br.grad) < 1e-4
+    # bf16 dy (the consuming GEMM's bf16 dX) == fp32 dy holding the same bf16-rounded values
+    dyb = dy.to(torch.bfloat16)
+    dx1 = torch.empty(rows, D, device=DEV)
+    dx2 = torch.empty(rows, D, device=DEV)
+    ops.layernorm_bwd(x, w, dyb, mean, rstd, dx1, accum=False)
+    ops.layernorm_bwd(x, w, dyb.float(), mean, rstd, dx2, accum=False)
+    assert torch.equal(dx1, dx2)
 
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])

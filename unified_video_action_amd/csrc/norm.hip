@@ -115,15 +115,16 @@ __global__ __launch_bounds__(256) void ln_fwd(const TI* __restrict__ x, const fl
 }
 
 // ------------------------------------------------------------------------------------
-// backward.  dy fp32.  g = dy*w (affine) or dy*(1+scale) (modulated)
+// backward.  dy fp32 or bf16 (the bf16 dX of the consuming GEMM: autocast semantics, half the
+// bytes of the dominant read).  g = dy*w (affine) or dy*(1+scale) (modulated)
 //   dx (+)= rstd * (g - mean(g) - xhat*mean(g*xhat))           fp32, accumulate if accum
 //   modulated: dscale = dy*xhat, dshift = dy  (TO, ld = ldm)
 //   affine: per-block partial sums dw_part[blk][D] = sum dy*xhat, db_part = sum dy
 // ------------------------------------------------------------------------------------
-template <typename TI, typename TO, int VEC, int NC>
+template <typename TI, typename TO, int VEC, int NC, typename TD>
 __global__ __launch_bounds__(256) void ln_bwd(const TI* __restrict__ x, const float* __restrict__ w,
                                               const float* __restrict__ b, const TO* __restrict__ scale, long long ldm,
-                                              const float* __restrict__ dy, const float* __restrict__ mean_in,
+                                              const TD* __restrict__ dy, const float* __restrict__ mean_in,
                                               const float* __restrict__ rstd_in, const float* dx_base,
                                               float* dx, int accum,
                                               TO* __restrict__ dscale, TO* __restrict__ dshift,
@@ -355,6 +356,17 @@ __global__ __launch_bounds__(256) void softmax_bwd_kernel(const T* __restrict__ 
 // =====================================================================================
 // C ABI
 // =====================================================================================
+#define DISPATCH_LNB(TI, TO, TD, ...)                                                       \
+  do {                                                                                       \
+    if (D % 256 == 0 && D <= 1024) {                                                         \
+      ln_bwd<TI, TO, 4, 4, TD><<<grid, 256, 0, stream>>>(__VA_ARGS__);                       \
+    } else if (D <= 1024) {                                                                  \
+      ln_bwd<TI, TO, 1, 16, TD><<<grid, 256, 0, stream>>>(__VA_ARGS__);                      \
+    } else {                                                                                 \
+      return (int)hipErrorInvalidValue;                                                      \
+    }                                                                                        \
+  } while (0)
+
 #define DISPATCH_LN(KERNEL, TI, TO, ...)                                                    \
   do {                                                                                       \
     if (D % 256 == 0 && D <= 1024) {                                                         \
@@ -388,7 +400,7 @@ extern "C" int uva_layernorm_fwd(int in_dtype, int out_dtype, const void* x, con
 
 extern "C" int uva_layernorm_bwd(int in_dtype, int out_dtype, const void* x, const float* w, const float* b,
                                  const void* scale,
-                                 long long ldm, const float* dy, const float* mean, const float* rstd,
+                                 long long ldm, const void* dy, int dy_dtype, const float* mean, const float* rstd,
                                  const float* dx_base, float* dx, int accum, void* dscale, void* dshift, float* dw, float* db, int accum_wb,
                                  float* workspace, int rows, int D, hipStream_t stream) {
   if (rows <= 0) return 0;
@@ -398,17 +410,24 @@ extern "C" int uva_layernorm_bwd(int in_dtype, int out_dtype, const void* x, con
   dim3 grid(nblk);
   float* pw = dw ? workspace : nullptr;
   float* pb = dw ? workspace + (long long)nblk * D : nullptr;
+#define LNB_DY(TI, TO)                                                                                          \
+  do {                                                                                                          \
+    if (dy_dtype == UVA_DT_BF16)                                                                                \
+      DISPATCH_LNB(TI, TO, bf16, (const TI*)x, w, b, (const TO*)scale, ldm, (const bf16*)dy, mean, rstd, dx_base, \
+                   dx, accum, (TO*)dscale, (TO*)dshift, pw, pb, rows, D, rpb);                                  \
+    else                                                                                                        \
+      DISPATCH_LNB(TI, TO, float, (const TI*)x, w, b, (const TO*)scale, ldm, (const float*)dy, mean, rstd,        \
+                   dx_base, dx, accum, (TO*)dscale, (TO*)dshift, pw, pb, rows, D, rpb);                         \
+  } while (0)
   if (in_dtype == UVA_DT_F32 && out_dtype == UVA_DT_F32)
-    DISPATCH_LN(ln_bwd, float, float, (const float*)x, w, b, (const float*)scale, ldm, dy, mean, rstd, dx_base, dx, accum,
-                (float*)dscale, (float*)dshift, pw, pb, rows, D, rpb);
+    LNB_DY(float, float);
   else if (in_dtype == UVA_DT_F32 && out_dtype == UVA_DT_BF16)
-    DISPATCH_LN(ln_bwd, float, bf16, (const float*)x, w, b, (const bf16*)scale, ldm, dy, mean, rstd, dx_base, dx, accum,
-                (bf16*)dscale, (bf16*)dshift, pw, pb, rows, D, rpb);
+    LNB_DY(float, bf16);
   else if (in_dtype == UVA_DT_BF16 && out_dtype == UVA_DT_BF16)
-    DISPATCH_LN(ln_bwd, bf16, bf16, (const bf16*)x, w, b, (const bf16*)scale, ldm, dy, mean, rstd, dx_base, dx, accum,
-                (bf16*)dscale, (bf16*)dshift, pw, pb, rows, D, rpb);
+    LNB_DY(bf16, bf16);
   else
     return (int)hipErrorInvalidValue;
+#undef LNB_DY
   UVA_LAUNCH_CHECK();
   if (dw) {
     colsum_partials(pw, db ? pb : nullptr, dw, db, nblk, D, accum_wb, stream);

@@ -282,7 +282,9 @@ class BlockFn(torch.autograd.Function):
         ops.act_bwd_bias(pre1, da, dpre1, grad_buf(fc1b), "gelu", drop_p=p_proj, seed=seeds[2])
         del da
         ops.linear_dw(dpre1, h2, grad_buf(fc1w))
-        dh2 = torch.empty(M, D, dtype=F32, device=dev)
+        # dX of the LN-fed GEMMs in the compute dtype (autocast: the matmul's input grad is half
+        # precision before the cast back to the fp32 LayerNorm output); LN backward reads it as is
+        dh2 = torch.empty(M, D, dtype=c if RT.ln_dy_lowp else F32, device=dev)
         ops.linear_dx(dpre1, compute_weight(fc1w), dh2)
         del dpre1
         g1 = torch.empty(M, D, dtype=F32, device=dev)
@@ -305,7 +307,7 @@ class BlockFn(torch.autograd.Function):
         del do
         ops.linear_dw(dqkv, h1, grad_buf(qkvw))
         ops.colsum(dqkv, grad_buf(qkvb))
-        dh1 = torch.empty(M, D, dtype=F32, device=dev)
+        dh1 = torch.empty(M, D, dtype=c if RT.ln_dy_lowp else F32, device=dev)
         ops.linear_dx(dqkv, compute_weight(qkvw), dh1)
         del dqkv
         gx = torch.empty(M, D, dtype=F32, device=dev)

@@ -161,12 +161,13 @@ def layernorm_bwd(x, w, dy, mean, rstd, dx, accum, dw=None, db=None, scale=None,
     """dx (= dx_base +) LN backward.  With `scale` (adaLN modulation) the affine (w, b) output is
     modulated: h = (xhat*w + b)*(1+scale) + shift; b is needed for d(scale)."""
     rows, D = x.shape
-    assert dy.dtype == torch.float32 and dx.dtype == torch.float32
+    assert dy.dtype in (torch.float32, torch.bfloat16) and dx.dtype == torch.float32
     odt = out_dtype if out_dtype is not None else (dt(scale) if scale is not None else dt(x))
     ws = None
     if dw is not None:
         ws = workspace(lib().query("uva_layernorm_bwd_workspace", rows, D), x.device)
-    lib().call("uva_layernorm_bwd", dt(x), odt, ptr(x), ptr(w), ptr(b), ptr(scale), ldm, ptr(dy), ptr(mean), ptr(rstd),
+    lib().call("uva_layernorm_bwd", dt(x), odt, ptr(x), ptr(w), ptr(b), ptr(scale), ldm, ptr(dy), dt(dy), ptr(mean),
+               ptr(rstd),
                ptr(dx_base), ptr(dx), int(accum), ptr(dscale), ptr(dshift), ptr(dw), ptr(db), int(accum_wb), ptr(ws), rows, D,
                stream())
 

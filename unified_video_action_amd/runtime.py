@@ -13,6 +13,8 @@ class _Runtime:
         # VAE ResnetBlock: GroupNorm+SiLU applied inside the halo conv's input staging (True) or as
         # a separate apply pass (False); UVA_VAE_GN_IN_CONV=0/1 overrides
         self.vae_gn_in_conv = os.environ.get("UVA_VAE_GN_IN_CONV", "1") == "1"
+        # dX of the LayerNorm-fed GEMMs in the compute dtype (autocast semantics) instead of fp32
+        self.ln_dy_lowp = os.environ.get("UVA_LN_DY_LOWP", "1") == "1"
         self._seed_base = 0x5EED
         self._ctr = itertools.count()
         # attention dropout masks: per Block the (B, N, H, p) of its last training forward, and the
