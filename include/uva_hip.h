@@ -132,6 +132,12 @@ int uva_softmax_bwd(int dtype, const void* P, const void* dPd, void* dS, long lo
 int uva_cast(int sdt, const void* src, long long lds, int ddt, void* dst, long long ldd, long long rows, int cols,
              hipStream_t stream);
 int uva_act_fwd(int xdt, const void* x, int ydt, void* y, long long n, int act, hipStream_t stream);
+/* y = residual + dropout(act(x)) over n contiguous elements (n % 8 == 0, 16-B aligned), dropout
+ * index = flat element index (the GEMM epilogue's / uva_act_bwd's mask).  timm Mlp forward
+ * (mar_con_unified.py:201-249: fc1 -> GELU -> drop, fc2 -> drop -> + residual) when fc1 / fc2 run
+ * as bias-only GEMMs.  (xdt, ydt, rdt) in {(bf16, bf16, bf16), (bf16, f32, f32), (f32, f32, f32)}. */
+int uva_act_drop_fwd(int xdt, const void* x, int ydt, void* y, int rdt, const void* residual, long long n, int act,
+                     float drop_p, unsigned long long seed, hipStream_t stream);
 int uva_act_bwd(int pdt, const void* pre, int gdt, const void* dy, long long ld_dy, int xdt, void* dx,
                 long long ld_dx, long long rows, int cols, int act, float drop_p, unsigned long long seed, int accum,
                 hipStream_t stream);

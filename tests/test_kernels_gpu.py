@@ -328,3 +328,29 @@ def test_adamw_ema_matches_torch():
         assert rel_err(p, torch.cat([pa, pb]).detach()) < 1e-6
     assert rel_err(ema, ema_ref) < 1e-6
     assert torch.equal(pbf, p.to(torch.bfloat16))
+
+
+@pytest.mark.parametrize("rows,cols", [(64, 3072), (1000, 768)])
+def test_act_drop_fwd_matches_backward_mask_and_torch(rows, cols):
+    """uva_act_drop_fwd (timm Mlp forward after bias-only GEMMs): GELU against torch's exact GELU, the
+    dropout keep pattern identical to the one act_bwd regenerates (flat element index), residual add."""
+    from unified_video_action_amd.native import ops
+    torch.manual_seed(rows + cols)
+    x = (torch.randn(rows, cols, device=DEV) * 2).to(torch.bfloat16)
+    y = torch.empty_like(x)
+    ops.act_drop_fwd(x, y, "gelu")
+    ref = torch.nn.functional.gelu(x.float())
+    assert rel_err(y.float(), ref) < 1e-2
+    ones = torch.ones(rows, cols, device=DEV).to(torch.bfloat16)
+    yd = torch.empty(rows, cols, device=DEV).to(torch.bfloat16)
+    ops.act_drop_fwd(ones, yd, "none", drop_p=0.1, seed=77)
+    g = torch.empty(rows, cols, device=DEV)
+    ops.act_bwd(None, torch.ones(rows, cols, device=DEV), g, "none", drop_p=0.1, seed=77)
+    assert torch.equal(yd.float() != 0, g != 0)
+    assert abs((g != 0).float().mean().item() - 0.9) < 0.02
+    res = torch.randn(rows, cols, device=DEV)
+    out = torch.empty(rows, cols, device=DEV)
+    ops.act_drop_fwd(x, out, "none", drop_p=0.1, seed=78, residual=res)
+    keep = torch.empty(rows, cols, device=DEV)
+    ops.act_bwd(None, torch.ones(rows, cols, device=DEV), keep, "none", drop_p=0.1, seed=78)
+    assert torch.allclose(out, res + x.float() * keep, rtol=1e-6, atol=1e-6)

@@ -3,7 +3,9 @@
 // timm Block / nn.Linear autograd, models/mar.py Block stack).  Every GEMM with a fused epilogue
 // (bias, GELU + pre-activation copy, dropout, residual, adaLN gate, GroupNorm-prologue convs)
 // stays on the hand-written kernels of gemm.hip / conv.hip; this file only routes the products
-// the library does at its peak (bf16 in, fp32 accumulate, bf16 or fp32 out, beta in {0, 1}).
+// the library does at its peak (bf16 in, fp32 accumulate, bf16 or fp32 out, beta in {0, 1}, an
+// optional fp32 bias: the forward's bias-only products -- qkv, and fc1 / fc2 whose GELU + dropout
+// and dropout + residual then run as one elementwise pass, uva_act_drop_fwd).
 //
 // Row-major C[M][N] = op(A)[M][K] . op(B)[K][N] (gemm.hip operand convention: ta = 0 -> A stored
 // [M][K], ta = 1 -> [K][M]; tb = 0 -> B stored [N][K], tb = 1 -> [K][N]) is the column-major
@@ -29,7 +31,7 @@ struct LtPlan {
   std::vector<size_t> ws;
 };
 
-using LtKey = std::tuple<int, int, int, int, int, int, long long, long long, long long, int>;
+using LtKey = std::tuple<int, int, int, int, int, int, long long, long long, long long, int, int>;
 
 struct LtState {
   hipblasLtHandle_t handle = nullptr;
@@ -49,7 +51,7 @@ constexpr size_t kLtWorkspace = 64ull << 20;
 int g_lt_mode = -1;  // -1: from UVA_GEMM_LIB (default 1)
 
 LtKey key_of(const LtShape& s) {
-  return LtKey{s.out_dtype, s.ta, s.tb, s.M, s.N, s.K, s.lda, s.ldb, s.ldc, s.beta_nonzero};
+  return LtKey{s.out_dtype, s.ta, s.tb, s.M, s.N, s.K, s.lda, s.ldb, s.ldc, s.beta_nonzero, s.bias};
 }
 
 // plan (descriptors + up to max_algos heuristic algorithms) for the shape, created on first use
@@ -70,6 +72,14 @@ LtPlan* plan_for(LtState& st, const LtShape& s, int max_algos) {
                      HIPBLAS_STATUS_SUCCESS;
   good = good && hipblasLtMatmulDescSetAttribute(p.desc, HIPBLASLT_MATMUL_DESC_TRANSB, &opB, sizeof(opB)) ==
                      HIPBLAS_STATUS_SUCCESS;
+  if (s.bias) {  // bias[N] = per row of the column-major D (N x M); fp32 vector
+    const hipblasLtEpilogue_t epi = HIPBLASLT_EPILOGUE_BIAS;
+    const hipDataType bt = HIP_R_32F;
+    good = good && hipblasLtMatmulDescSetAttribute(p.desc, HIPBLASLT_MATMUL_DESC_EPILOGUE, &epi, sizeof(epi)) ==
+                       HIPBLAS_STATUS_SUCCESS;
+    good = good && hipblasLtMatmulDescSetAttribute(p.desc, HIPBLASLT_MATMUL_DESC_BIAS_DATA_TYPE, &bt, sizeof(bt)) ==
+                       HIPBLAS_STATUS_SUCCESS;
+  }
   // stored shapes (column-major rows x cols, ld)
   good = good && hipblasLtMatrixLayoutCreate(&p.la, HIP_R_16BF, s.tb == 0 ? s.K : s.N, s.tb == 0 ? s.N : s.K,
                                              s.ldb) == HIPBLAS_STATUS_SUCCESS;
@@ -109,13 +119,19 @@ int lt_prepare(const LtShape& s, int max_algos) {
 }
 
 int lt_run(const LtShape& s, int idx, const void* A, const void* B, const void* C, void* D, float alpha, float beta,
-           hipStream_t stream) {
+           const float* bias, hipStream_t stream) {
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess) return (int)hipErrorInvalidDevice;
   LtState& st = lt_state(dev);
   std::lock_guard<std::mutex> lock(st.mu);
   LtPlan* p = plan_for(st, s, 8);
   if (!p || idx < 0 || idx >= (int)p->algos.size()) return -1;
+  if (s.bias) {
+    const void* bp = bias;
+    if (hipblasLtMatmulDescSetAttribute(p->desc, HIPBLASLT_MATMUL_DESC_BIAS_POINTER, &bp, sizeof(bp)) !=
+        HIPBLAS_STATUS_SUCCESS)
+      return -1;
+  }
   const hipblasStatus_t r = hipblasLtMatmul(st.handle, p->desc, &alpha, B, p->la, A, p->lb, &beta, C, p->lc, D,
                                             p->lc, &p->algos[idx], st.ws, p->ws[idx], stream);
   return r == HIPBLAS_STATUS_SUCCESS ? 0 : 1000 + (int)r;
@@ -140,7 +156,7 @@ extern "C" int uva_lt_enabled() {
 extern "C" int uva_lt_gemm(int out_dtype, int ta, int tb, const void* A, const void* B, void* C, int M, int N,
                            int K, long long lda, long long ldb, long long ldc, float alpha, float beta,
                            hipStream_t stream) {
-  const LtShape s{out_dtype, ta, tb, M, N, K, lda, ldb, ldc, beta != 0.f};
+  const LtShape s{out_dtype, ta, tb, M, N, K, lda, ldb, ldc, beta != 0.f, 0};
   if (lt_prepare(s, 8) <= 0) return -1;
-  return lt_run(s, 0, A, B, C, C, alpha, beta, stream);
+  return lt_run(s, 0, A, B, C, C, alpha, beta, nullptr, stream);
 }

@@ -292,6 +292,68 @@ extern "C" int uva_cast(int sdt, const void* src, long long lds, int ddt, void* 
   return 0;
 }
 
+// y = residual + drop(act(x)), 8 consecutive elements per thread (16-B bf16 / 2 x 16-B fp32
+// accesses), dropout index = flat element index (= row * cols + col of a contiguous [rows][cols]:
+// the GEMM epilogue's and act_bwd's mask).  The forward of timm Mlp when its GEMMs run bias-only
+// on the library: fc1 -> a = drop(GELU(pre)), fc2 -> x2 = x1 + drop(fc2 out).
+template <typename TX, typename TY, typename TR>
+__global__ __launch_bounds__(256) void act_drop_fwd_kernel(const TX* __restrict__ x, TY* __restrict__ y,
+                                                           const TR* __restrict__ res, long long n8, int act,
+                                                           uint32_t thresh, float dscale, uint64_t seed) {
+  GRID_STRIDE(i, n8) {
+    float v[8], r[8];
+    ld8<TX>(x + i * 8, v);
+    if (res) ld8<TR>(res + i * 8, r);
+    switch (act) {
+      case ACT_GELU:
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] = gelu_erf(v[e]);
+        break;
+      case ACT_SILU:
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] = silu(v[e]);
+        break;
+      case ACT_RELU:
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] = v[e] > 0.f ? v[e] : 0.f;
+        break;
+      default:
+        break;
+    }
+    if (thresh) {
+      bool keep[8];
+#pragma unroll
+      for (int e = 0; e < 8; e += 2) dropout_keep2(seed, (uint64_t)(i * 8 + e), thresh, keep[e], keep[e + 1]);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = keep[e] ? v[e] * dscale : 0.f;
+    }
+    if (res) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] += r[e];
+    }
+    st8<TY>(y + i * 8, v);
+  }
+}
+
+extern "C" int uva_act_drop_fwd(int xdt, const void* x, int ydt, void* y, int rdt, const void* residual, long long n,
+                                int act, float drop_p, unsigned long long seed, hipStream_t s) {
+  if (n <= 0) return 0;
+  if (n % 8 || (((uintptr_t)x | (uintptr_t)y | (uintptr_t)residual) % 16)) return (int)hipErrorInvalidValue;
+  uint32_t th;
+  float ds;
+  uva_drop_params(drop_p, &th, &ds);
+  const long long n8 = n / 8;
+#define ADF(TX, TY, TR) \
+  act_drop_fwd_kernel<TX, TY, TR><<<ew_grid(n8), 256, 0, s>>>((const TX*)x, (TY*)y, (const TR*)residual, n8, act, th, ds, seed)
+  if (xdt == UVA_DT_BF16 && ydt == UVA_DT_BF16 && (!residual || rdt == UVA_DT_BF16)) ADF(bf16, bf16, bf16);
+  else if (xdt == UVA_DT_BF16 && ydt == UVA_DT_F32 && (!residual || rdt == UVA_DT_F32)) ADF(bf16, float, float);
+  else if (xdt == UVA_DT_F32 && ydt == UVA_DT_F32 && (!residual || rdt == UVA_DT_F32)) ADF(float, float, float);
+  else return (int)hipErrorInvalidValue;
+#undef ADF
+  UVA_LAUNCH_CHECK();
+  return 0;
+}
+
 extern "C" int uva_act_fwd(int xdt, const void* x, int ydt, void* y, long long n, int act, hipStream_t s) {
   if (n <= 0) return 0;
   act_fwd_kernel<<<ew_grid(n), 256, 0, s>>>(x, xdt, y, ydt, n, act);

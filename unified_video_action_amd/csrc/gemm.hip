@@ -1522,13 +1522,13 @@ extern "C" int uva_lt_enabled();
 static int plain_gemm_tuned(int out_dtype, int ta, int tb, const void* A, const void* B, void* C, int M, int N,
                             int K, long long lda, long long ldb, long long ldc, float beta, const BatchStrides& bs,
                             const EpiParams& ep, float* ws, long long ws_floats, hipStream_t stream) {
-  const LtShape sh{out_dtype, ta, tb, M, N, K, lda, ldb, ldc, beta != 0.f};
-  using Key = std::tuple<int, int, int, int, int, int, long long, long long, long long, int, int, int>;
+  const LtShape sh{out_dtype, ta, tb, M, N, K, lda, ldb, ldc, beta != 0.f, ep.bias != nullptr};
+  using Key = std::tuple<int, int, int, int, int, int, long long, long long, long long, int, int, int, int>;
   static std::map<Key, int> choice;
   static std::mutex mu;
   int dev = 0;
   (void)hipGetDevice(&dev);
-  const Key key{out_dtype, ta, tb, M, N, K, lda, ldb, ldc, beta != 0.f, dev, uva_lt_enabled()};
+  const Key key{out_dtype, ta, tb, M, N, K, lda, ldb, ldc, beta != 0.f, dev, uva_lt_enabled(), ep.bias != nullptr};
   int pick;
   {
     std::lock_guard<std::mutex> lock(mu);
@@ -1566,7 +1566,7 @@ static int plain_gemm_tuned(int out_dtype, int ta, int tb, const void* A, const 
       });
       const float own = best;
       for (int i = 0; i < n; ++i) {
-        const float t = time_it([&]() { return lt_run(sh, i, A, B, scratch, scratch, 1.f, beta, stream); });
+        const float t = time_it([&]() { return lt_run(sh, i, A, B, scratch, scratch, 1.f, beta, ep.bias, stream); });
         if (t < best) {
           best = t;
           pick = i;
@@ -1583,7 +1583,7 @@ static int plain_gemm_tuned(int out_dtype, int ta, int tb, const void* A, const 
     choice[key] = pick;
   }
   if (pick < 0) return -1;
-  return lt_run(sh, pick, A, B, C, C, 1.f, beta, stream);
+  return lt_run(sh, pick, A, B, C, C, 1.f, beta, ep.bias, stream);
 }
 
 extern "C" int uva_gemm(int in_dtype, int out_dtype, int ta, int tb, const void* A, const void* B, void* C, int M,
@@ -1601,10 +1601,10 @@ extern "C" int uva_gemm(int in_dtype, int out_dtype, int ta, int tb, const void*
   ep.gate = gate;
   ep.ldg = ldg;
   ep.gate_dt = gate_dtype;
-  // epilogue-free bf16 products (the backward's dX / dW): this file's kernel or hipBLASLt, whichever
-  // timed faster for the shape (plain_gemm_tuned)
-  if (in_dtype == UVA_DT_BF16 && batch == 1 && !force_generic && !bias && !residual && !aux && act == 0 &&
-      !(drop_p > 0.f) && !gate && alpha == 1.f && (beta == 0.f || beta == 1.f) && uva_lt_enabled()) {
+  // epilogue-free (or bias-only) bf16 products -- the backward's dX / dW, the forward's qkv / fc1 /
+  // fc2: this file's kernel or hipBLASLt, whichever timed faster for the shape (plain_gemm_tuned)
+  if (in_dtype == UVA_DT_BF16 && batch == 1 && !force_generic && !residual && !aux && act == 0 &&
+      !(drop_p > 0.f) && !gate && alpha == 1.f && (beta == 0.f || (beta == 1.f && !bias)) && uva_lt_enabled()) {
     const int r = plain_gemm_tuned(out_dtype, ta, tb, A, B, C, M, N, K, lda, ldb, ldc, beta, bs, ep, workspace,
                                    ws_floats, stream);
     if (r >= 0) return r;

@@ -249,10 +249,20 @@ class BlockFn(torch.autograd.Function):
         Hd = fc1w.shape[0]
         a = torch.empty(M, Hd, dtype=c, device=dev)
         pre1 = torch.empty(M, Hd, dtype=c, device=dev)
-        ops.linear(h2, compute_weight(fc1w), a, bias=fc1b.detach(), act="gelu", aux=pre1, drop_p=p_proj,
-                   seed=seeds[2])
         x2 = torch.empty(M, D, dtype=F32, device=dev)
-        ops.linear(a, compute_weight(fc2w), x2, bias=fc2b.detach(), residual=x1, drop_p=p_proj, seed=seeds[3])
+        if c == torch.bfloat16 and RT.mlp_split_epilogue:
+            # bias-only GEMMs (autocast: fc1 / fc2 outputs are bf16 before GELU / dropout / the fp32
+            # residual add) + one elementwise pass each; same dropout masks (flat element index)
+            ops.linear(h2, compute_weight(fc1w), pre1, bias=fc1b.detach())
+            ops.act_drop_fwd(pre1, a, "gelu", drop_p=p_proj, seed=seeds[2])
+            t2 = torch.empty(M, D, dtype=c, device=dev)
+            ops.linear(a, compute_weight(fc2w), t2, bias=fc2b.detach())
+            ops.act_drop_fwd(t2, x2, "none", drop_p=p_proj, seed=seeds[3], residual=x1)
+            del t2
+        else:
+            ops.linear(h2, compute_weight(fc1w), a, bias=fc1b.detach(), act="gelu", aux=pre1, drop_p=p_proj,
+                       seed=seeds[2])
+            ops.linear(a, compute_weight(fc2w), x2, bias=fc2b.detach(), residual=x1, drop_p=p_proj, seed=seeds[3])
         ctx.save_for_backward(x, h1, m1, r1, qkv, o, lse, P, Pd, x1, h2, m2, r2, pre1, a,
                               n1w, n1b, qkvw, qkvb, projw, projb, n2w, n2b, fc1w, fc1b, fc2w, fc2b)
         ctx.cfg = (B, N, H, p_attn, p_proj, seeds, flash)

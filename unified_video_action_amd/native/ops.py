@@ -63,8 +63,9 @@ def gemm(A, B, C, M, N, K, lda, ldb, ldc, ta=0, tb=0, batch=1, inner=1, sA=(0, 0
         assert bias.dtype == torch.float32 and bias.is_contiguous()
     if aux is not None:
         assert aux.dtype == C.dtype
-    plain = (dt(A) == 1 and batch == 1 and not force_generic and bias is None and residual is None and aux is None
-             and act in ("none", 0) and not drop_p > 0 and gate is None and alpha == 1.0 and beta in (0.0, 1.0))
+    plain = (dt(A) == 1 and batch == 1 and not force_generic and residual is None and aux is None
+             and act in ("none", 0) and not drop_p > 0 and gate is None and alpha == 1.0
+             and (beta == 0.0 or (beta == 1.0 and bias is None)))
     route = " hipBLASLt" if plain and lib().query("uva_lt_enabled") else ""
     with _traced(f"gemm[{'NT'[ta]}{'NT'[tb]}] {'bf16' if dt(A) else 'f32'} M{M} N{N} K{K} b{batch}{route}",
                  2.0 * M * N * K * batch):
@@ -196,6 +197,15 @@ def cast(src, dst):
 
 def act_fwd(x, y, act):
     lib().call("uva_act_fwd", dt(x), ptr(x), dt(y), ptr(y), x.numel(), ACT[act], stream())
+
+
+def act_drop_fwd(x, y, act="none", drop_p=0.0, seed=0, residual=None):
+    """y = residual + dropout(act(x)); contiguous, same element count (mask = flat index)."""
+    assert x.is_contiguous() and y.is_contiguous() and x.numel() == y.numel()
+    if residual is not None:
+        assert residual.is_contiguous() and residual.numel() == x.numel()
+    lib().call("uva_act_drop_fwd", dt(x), ptr(x), dt(y), ptr(y), dt(residual) if residual is not None else 0,
+               ptr(residual), x.numel(), ACT[act], float(drop_p), int(seed) & 0xFFFFFFFFFFFFFFFF, stream())
 
 
 def act_bwd(pre, dy, dx, act, drop_p=0.0, seed=0, accum=False):

@@ -15,6 +15,9 @@ class _Runtime:
         self.vae_gn_in_conv = os.environ.get("UVA_VAE_GN_IN_CONV", "1") == "1"
         # dX of the LayerNorm-fed GEMMs in the compute dtype (autocast semantics) instead of fp32
         self.ln_dy_lowp = os.environ.get("UVA_LN_DY_LOWP", "1") == "1"
+        # timm Mlp forward (bf16): fc1 / fc2 as bias-only GEMMs (tuned: library or own kernel) + one
+        # elementwise GELU/dropout(/residual) pass each, instead of the fused-epilogue GEMMs
+        self.mlp_split_epilogue = os.environ.get("UVA_MLP_SPLIT_EPI", "1") == "1"
         self._seed_base = 0x5EED
         self._ctr = itertools.count()
         # attention dropout masks: per Block the (B, N, H, p) of its last training forward, and the
