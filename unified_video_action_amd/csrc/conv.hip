@@ -403,114 +403,131 @@ extern "C" int uva_conv3x3_halo(const void* in, const void* w, void* out, const 
 //   * per 16-pixel row: 24 MFMAs, bias, bf16, GN partial sums, then the 16 px x 128 ch tile goes
 //     through a per-wave LDS slab so the global stores are 4 fully contiguous 1-KiB wave stores.
 // =====================================================================================
+// weights and bias staged in LDS once per workgroup, which then walks CI_TPW consecutive 16x16
+// tiles; padded LDS pitches (weights 224 B, output slab 272 B) keep every fragment read and slab
+// write conflict-free or 2-way.  The first form (weights in 96 VGPRs, unpadded slab: 16-way
+// conflicts on every slab write, 600M conflict cycles per launch) took 1.78 ms at the level-0 shape,
+// this one 1.38 ms.  Taps 9..13 of the padded weight row are zero, so every read is unconditional.
+#define CI_WK 112  // weight row pitch (elements): 12 taps x 8 + 16 pad -> conflict-free ds_read_b128 (224 B)
+#define CI_SP 136  // slab pixel pitch (elements): 128 + 8 pad (unpadded, the 16 lanes of a b64 write
+                   // hit one bank: 16-way conflicts, 600M conflict cycles per launch)
+#define CI_TPW 4   // tiles per workgroup
 __global__ __launch_bounds__(256) void conv_in_kernel(const bf16* __restrict__ in, const bf16* __restrict__ wt,
                                                       const float* __restrict__ bias, bf16* __restrict__ out,
                                                       float* __restrict__ gn_part, int Nimg, int H, int W) {
   __shared__ __attribute__((aligned(16))) bf16 sx[CH_HPIX * 8];
-  __shared__ __attribute__((aligned(16))) bf16 slab[4][16 * 128];
+  __shared__ __attribute__((aligned(16))) bf16 sw[128 * CI_WK];
+  __shared__ __attribute__((aligned(16))) bf16 slab[4][16 * CI_SP];
+  __shared__ float sb[128];
   __shared__ float red[4][32][2];
   const int tiles_x = W / CH_T, tiles_y = H / CH_T;
-  const int sp = blockIdx.x;
-  const int tx = sp % tiles_x, ty = (sp / tiles_x) % tiles_y, n = sp / (tiles_x * tiles_y);
-  const int oh0 = ty * CH_T, ow0 = tx * CH_T;
+  const int ntiles = Nimg * tiles_x * tiles_y;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int frow = lane & 15, fk = lane >> 4;
-  // halo: 324 pixels x 16 B
-  for (int p = tid; p < CH_HPIX; p += 256) {
-    const int hy = p / CH_H, hx = p - hy * CH_H;
-    const int ih = oh0 - 1 + hy, iw = ow0 - 1 + hx;
+  // weights [128][72] -> LDS [128][CI_WK] (16-B chunks; chunks 9..13 of each row zero)
+  for (int i = tid; i < 128 * 14; i += 256) {
+    const int r = i / 14, c = i - r * 14;
     bf16x8 v = (bf16x8){};
-    if (ih >= 0 && ih < H && iw >= 0 && iw < W) v = *(const bf16x8*)(in + (((long long)n * H + ih) * W + iw) * 8);
-    *(bf16x8*)(sx + p * 8) = v;
+    if (c < 9) v = *(const bf16x8*)(wt + r * 72 + c * 8);
+    *(bf16x8*)(sw + r * CI_WK + c * 8) = v;
   }
-  // weights [128][72] -> A fragments (row = channel f*16 + frow, k-group = tap ks*4 + fk)
-  bf16x8 wf[8][3];
-#pragma unroll
-  for (int f = 0; f < 8; ++f)
-#pragma unroll
-    for (int ks = 0; ks < 3; ++ks) {
-      const int tap = ks * 4 + fk;
-      wf[f][ks] = tap < 9 ? *(const bf16x8*)(wt + (f * 16 + frow) * 72 + tap * 8) : (bf16x8){};
-    }
-  float bv[8][4];
-#pragma unroll
-  for (int f = 0; f < 8; ++f)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) bv[f][r] = bias ? bias[f * 16 + fk * 4 + r] : 0.f;
-  __syncthreads();
-  float gs[8], gq[8];
-#pragma unroll
-  for (int f = 0; f < 8; ++f) gs[f] = gq[f] = 0.f;
+  if (tid < 128) sb[tid] = bias ? bias[tid] : 0.f;
   bf16* myslab = slab[wid];
 #pragma unroll 1
-  for (int rr = 0; rr < 4; ++rr) {
-    const int row = wid * 4 + rr;  // tile row
-    bf16x8 xf[3];
-#pragma unroll
-    for (int ks = 0; ks < 3; ++ks) {
-      const int tap = ks * 4 + fk;
-      const int kh = tap / 3, kw = tap % 3;
-      xf[ks] = tap < 9 ? *(const bf16x8*)(sx + ((row + kh) * CH_H + frow + kw) * 8) : (bf16x8){};
-    }
-    f32x4 acc[8];
-#pragma unroll
-    for (int f = 0; f < 8; ++f) {
-      acc[f] = (f32x4){0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int ks = 0; ks < 3; ++ks) acc[f] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[f][ks], xf[ks], acc[f], 0, 0, 0);
-    }
-    // acc[f][r] = out[pixel frow][channel f*16 + fk*4 + r]
-#pragma unroll
-    for (int f = 0; f < 8; ++f) {
-      bf16x4 o;
-      float s = 0.f, q = 0.f;
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        o[r] = (bf16)(acc[f][r] + bv[f][r]);
-        const float v = (float)o[r];
-        s += v;
-        q += v * v;
-      }
-      gs[f] += s;
-      gq[f] += q;
-      *(bf16x4*)(myslab + frow * 128 + f * 16 + fk * 4) = o;
-    }
-    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): slab writes done (wave-private slab)
-    __builtin_amdgcn_wave_barrier();
-    const long long ob = (((long long)n * H + oh0 + row) * W + ow0) * 128;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int e = (i * 64 + lane) * 8;  // 16 px x 128 ch contiguous in NHWC
-      *(bf16x8*)(out + ob + e) = *(const bf16x8*)(myslab + e);
-    }
-    __builtin_amdgcn_wave_barrier();
-  }
-  if (gn_part) {
-    // group g = f*4 + fk: reduce over the 16 pixel lanes sharing fk
-#pragma unroll
-    for (int f = 0; f < 8; ++f) {
-#pragma unroll
-      for (int o = 1; o < 16; o <<= 1) {
-        gs[f] += __shfl_xor(gs[f], o, 64);
-        gq[f] += __shfl_xor(gq[f], o, 64);
-      }
-    }
-    if (frow == 0) {
-#pragma unroll
-      for (int f = 0; f < 8; ++f) {
-        red[wid][f * 4 + fk][0] = gs[f];
-        red[wid][f * 4 + fk][1] = gq[f];
-      }
+  for (int sp = blockIdx.x * CI_TPW; sp < min(ntiles, (int)(blockIdx.x + 1) * CI_TPW); ++sp) {
+    const int tx = sp % tiles_x, ty = (sp / tiles_x) % tiles_y, n = sp / (tiles_x * tiles_y);
+    const int oh0 = ty * CH_T, ow0 = tx * CH_T;
+    // halo: 324 pixels x 16 B (the previous tile's readers passed the barrier ending its iteration)
+    for (int p = tid; p < CH_HPIX; p += 256) {
+      const int hy = p / CH_H, hx = p - hy * CH_H;
+      const int ih = oh0 - 1 + hy, iw = ow0 - 1 + hx;
+      bf16x8 v = (bf16x8){};
+      if (ih >= 0 && ih < H && iw >= 0 && iw < W) v = *(const bf16x8*)(in + (((long long)n * H + ih) * W + iw) * 8);
+      *(bf16x8*)(sx + p * 8) = v;
     }
     __syncthreads();
-    if (tid < 64) {
-      const int half = tid >> 5, g = tid & 31;  // half 0 = waves 0,1 (tile rows 0-7)
-      const float s = red[half * 2][g][0] + red[half * 2 + 1][g][0];
-      const float q = red[half * 2][g][1] + red[half * 2 + 1][g][1];
-      const long long t128 = ((long long)n * tiles_x * tiles_y + (sp % (tiles_x * tiles_y))) * 2 + half;
-      gn_part[(t128 * 32 + g) * 2 + 0] = s;
-      gn_part[(t128 * 32 + g) * 2 + 1] = q;
+    float gs[8], gq[8];
+#pragma unroll
+    for (int f = 0; f < 8; ++f) gs[f] = gq[f] = 0.f;
+#pragma unroll 1
+    for (int rr = 0; rr < 4; ++rr) {
+      const int row = wid * 4 + rr;  // tile row
+      bf16x8 xf[3];
+#pragma unroll
+      for (int ks = 0; ks < 3; ++ks) {
+        const int tap = ks * 4 + fk;
+        const int kh = tap / 3, kw = tap % 3;
+        xf[ks] = tap < 9 ? *(const bf16x8*)(sx + ((row + kh) * CH_H + frow + kw) * 8) : (bf16x8){};
+      }
+      // acc[f][r] = out[pixel frow][channel f*16 + fk*4 + r]   (A = weights: row = channel f*16 + frow).
+      // k-step-major issue: 8 independent accumulators between dependent MFMAs (f-major, the three
+      // chained MFMAs of each f stalled on one another and on the accumulator read-back)
+      f32x4 acc[8];
+#pragma unroll
+      for (int f = 0; f < 8; ++f) acc[f] = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ks = 0; ks < 3; ++ks) {
+        bf16x8 wf[8];
+#pragma unroll
+        for (int f = 0; f < 8; ++f) wf[f] = *(const bf16x8*)(sw + (f * 16 + frow) * CI_WK + (ks * 4 + fk) * 8);
+#pragma unroll
+        for (int f = 0; f < 8; ++f) acc[f] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[f], xf[ks], acc[f], 0, 0, 0);
+      }
+#pragma unroll
+      for (int f = 0; f < 8; ++f) {
+        const float4 b4 = *(const float4*)(sb + f * 16 + fk * 4);
+        const float bb[4] = {b4.x, b4.y, b4.z, b4.w};
+        bf16x4 o;
+        float s = 0.f, q = 0.f;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          o[r] = (bf16)(acc[f][r] + bb[r]);
+          const float v = (float)o[r];
+          s += v;
+          q += v * v;
+        }
+        gs[f] += s;
+        gq[f] += q;
+        *(bf16x4*)(myslab + frow * CI_SP + f * 16 + fk * 4) = o;
+      }
+      __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): slab writes done (wave-private slab)
+      __builtin_amdgcn_wave_barrier();
+      const long long ob = (((long long)n * H + oh0 + row) * W + ow0) * 128;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int e = (i * 64 + lane) * 8;  // 16 px x 128 ch contiguous in NHWC
+        *(bf16x8*)(out + ob + e) = *(const bf16x8*)(myslab + (e >> 7) * CI_SP + (e & 127));
+      }
+      __builtin_amdgcn_wave_barrier();
     }
+    if (gn_part) {
+      // group g = f*4 + fk: reduce over the 16 pixel lanes sharing fk
+#pragma unroll
+      for (int f = 0; f < 8; ++f) {
+#pragma unroll
+        for (int o = 1; o < 16; o <<= 1) {
+          gs[f] += __shfl_xor(gs[f], o, 64);
+          gq[f] += __shfl_xor(gq[f], o, 64);
+        }
+      }
+      if (frow == 0) {
+#pragma unroll
+        for (int f = 0; f < 8; ++f) {
+          red[wid][f * 4 + fk][0] = gs[f];
+          red[wid][f * 4 + fk][1] = gq[f];
+        }
+      }
+      __syncthreads();
+      if (tid < 64) {
+        const int half = tid >> 5, g = tid & 31;  // half 0 = waves 0,1 (tile rows 0-7)
+        const float s = red[half * 2][g][0] + red[half * 2 + 1][g][0];
+        const float q = red[half * 2][g][1] + red[half * 2 + 1][g][1];
+        const long long t128 = ((long long)n * tiles_x * tiles_y + (sp % (tiles_x * tiles_y))) * 2 + half;
+        gn_part[(t128 * 32 + g) * 2 + 0] = s;
+        gn_part[(t128 * 32 + g) * 2 + 1] = q;
+      }
+    }
+    __syncthreads();  // sx / red reused by the next tile
   }
 }
 
@@ -518,7 +535,7 @@ extern "C" int uva_conv_in8(const void* in, const void* w, void* out, const floa
                             float* gn_part, hipStream_t stream) {
   if (Nimg <= 0) return 0;
   if (H % CH_T || W % CH_T || (((uintptr_t)in | (uintptr_t)w | (uintptr_t)out) % 16)) return (int)hipErrorInvalidValue;
-  const long long nblk = (long long)Nimg * (H / CH_T) * (W / CH_T);
+  const long long nblk = ((long long)Nimg * (H / CH_T) * (W / CH_T) + CI_TPW - 1) / CI_TPW;
   conv_in_kernel<<<dim3((unsigned)nblk), 256, 0, stream>>>((const bf16*)in, (const bf16*)w, bias, (bf16*)out, gn_part,
                                                            Nimg, H, W);
   UVA_LAUNCH_CHECK();
