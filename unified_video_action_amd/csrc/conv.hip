@@ -146,10 +146,18 @@ __global__ __launch_bounds__(TR * 32, 16 / TR) void conv3x3_halo(const bf16* __r
         if (ih < 0 || ih >= H || iw < 0 || iw >= W) {
           v = (bf16x8){};
         } else if constexpr (GN) {
+          // packed pairs: v_pk_fma / v_pk_mul / v_pk_add for everything but the two transcendentals
 #pragma unroll
-          for (int j = 0; j < 8; ++j) {
-            const float u = (float)v[j] * gsc[j] + gsh[j];
-            v[j] = (bf16)(gn_silu ? silu(u) : u);
+          for (int j = 0; j < 8; j += 2) {
+            const f32x2 x = {(float)v[j], (float)v[j + 1]};
+            f32x2 u = x * (f32x2){gsc[j], gsc[j + 1]} + (f32x2){gsh[j], gsh[j + 1]};
+            if (gn_silu) {
+              const f32x2 t = u * (f32x2){-1.4426950408889634f, -1.4426950408889634f};
+              const f32x2 d = (f32x2){__builtin_amdgcn_exp2f(t.x), __builtin_amdgcn_exp2f(t.y)} + (f32x2){1.f, 1.f};
+              u = u * (f32x2){__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y)};
+            }
+            v[j] = (bf16)u.x;
+            v[j + 1] = (bf16)u.y;
           }
         }
         *(bf16x8*)(img + p * 64 + ((hc ^ (p & 7)) << 3)) = v;
