@@ -62,6 +62,19 @@ __device__ __forceinline__ void ch_lds_barrier() {
   asm volatile("" ::: "memory");
 }
 
+// v + v[lane ^ o]: o = 16 / 32 by v_permlane16/32_swap (VALU; ds_bpermute for the rest)
+__device__ __forceinline__ float xor_lane_sum(float v, int o) {
+  if (o == 16) {
+    const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+    return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+  }
+  if (o == 32) {
+    const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+    return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+  }
+  return v + __shfl_xor(v, o, 64);
+}
+
 __device__ __forceinline__ int ch_xcd_remap(int bid, int nblk) {
   int q = nblk / 8, r = nblk % 8, x = bid % 8;
   return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + bid / 8;
@@ -180,6 +193,25 @@ __global__ __launch_bounds__(TR * 32, 16 / TR) void conv3x3_halo(const bf16* __r
   asm volatile("" ::: "memory");
 
   const int frow = lane & 15, fk = lane >> 4;
+  // epilogue geometry.  The first ROUNDS of the tile's residual row chunks are loaded at tap 0 of
+  // the LAST chunk into hreg (free there: no next halo), so the step barriers cover their HBM
+  // latency (loaded at the epilogue's start, ~1.5-3k cycles stayed exposed per tile, +0.7 ms at
+  // the level-0 shape); a separate register array for them spilled the GN variant
+  constexpr int C8 = BN / 8, RPP = G::NTH / C8, NHALF = TR / 8;
+  const int c8 = tid % C8, rsub = tid / C8;
+  const int col0 = n0 + c8 * 8;
+  constexpr int NIT = 128 / RPP;
+  constexpr int NPRE = G::ROUNDS < NHALF * NIT ? G::ROUNDS : NHALF * NIT;
+  auto res_ptr = [&](int idx) {
+    const int half = idx / NIT, it = idx % NIT;
+    const int rl = it * RPP + rsub;
+    const int oh = oh0 + half * 8 + (rl >> 4), ow = ow0 + (rl & 15);
+    return (const bf16x8*)(residual + (((long long)n * H + oh) * W + ow) * Co + col0);
+  };
+  auto res_load = [&]() {
+#pragma unroll
+    for (int i = 0; i < NPRE; ++i) hreg[i] = *res_ptr(i);
+  };
   if constexpr (VAR & 1) asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(st1)::"memory");
   for (int cc = 0; cc < nch; ++cc) {
     const bf16* hcur = halo + (cc & 1) * G::HALO_ELEMS;
@@ -190,6 +222,7 @@ __global__ __launch_bounds__(TR * 32, 16 / TR) void conv3x3_halo(const bf16* __r
       // ring slot (s+1)&1 was last read in step s-1; every wave passed the barrier that ended it
       if (s + 1 < S) dma_w(s + 1, (s + 1) & 1);
       if (tap == 0 && more) halo_load(cc + 1);
+      if (tap == 0 && !more && residual) res_load();
       const bf16* bcur = bimg + (s & 1) * G::BT;
       const int kh = tap / 3, kw = tap % 3;
 #pragma unroll
@@ -224,9 +257,6 @@ __global__ __launch_bounds__(TR * 32, 16 / TR) void conv3x3_halo(const bf16* __r
   if constexpr (VAR & 1) asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(st2)::"memory");
   // ---- epilogue: 128-pixel halves (tile rows 0-7 [, 8-15]) staged through LDS as fp32
   float* T = (float*)smem;
-  constexpr int C8 = BN / 8, RPP = G::NTH / C8, NHALF = TR / 8;
-  const int c8 = tid % C8, rsub = tid / C8;
-  const int col0 = n0 + c8 * 8;
   float bv[8];
   if (bias) {
     const float4 b0 = *(const float4*)(bias + col0), b1 = *(const float4*)(bias + col0 + 4);
@@ -236,20 +266,10 @@ __global__ __launch_bounds__(TR * 32, 16 / TR) void conv3x3_halo(const bf16* __r
     for (int e = 0; e < 8; ++e) bv[e] = 0.f;
   }
   const int tiles_img = tiles_x * tiles_y;
-  // the tile's residual rows (both halves) are loaded up front, so the HBM latency overlaps the
-  // accumulator staging; loaded inside the store loop they serialised (one round trip per
-  // iteration: the stores to `out` kept the compiler from hoisting them) -- 19k ticks per tile
-  constexpr int NIT = 128 / RPP;
   bf16x8 rres[NHALF][NIT];
   if (residual) {
 #pragma unroll
-    for (int half = 0; half < NHALF; ++half)
-#pragma unroll
-      for (int it = 0; it < NIT; ++it) {
-        const int rl = it * RPP + rsub;
-        const int oh = oh0 + half * 8 + (rl >> 4), ow = ow0 + (rl & 15);
-        rres[half][it] = *(const bf16x8*)(residual + (((long long)n * H + oh) * W + ow) * Co + col0);
-      }
+    for (int i = 0; i < NHALF * NIT; ++i) rres[i / NIT][i % NIT] = i < NPRE ? hreg[i] : *res_ptr(i);
   }
 #pragma unroll
   for (int half = 0; half < NHALF; ++half) {
@@ -299,8 +319,8 @@ __global__ __launch_bounds__(TR * 32, 16 / TR) void conv3x3_halo(const bf16* __r
       for (int e = 0; e < 8; ++e) {
 #pragma unroll
         for (int o = C8; o < 64; o <<= 1) {
-          gs[e] += __shfl_xor(gs[e], o, 64);
-          gq[e] += __shfl_xor(gq[e], o, 64);
+          gs[e] = xor_lane_sum(gs[e], o);
+          gq[e] = xor_lane_sum(gq[e], o);
         }
       }
       float* red = T + 128 * G::TP;  // [NW waves][C8][8][2]
