@@ -7,7 +7,8 @@ import re
 
 _PKG = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 _ROOT = os.path.dirname(_PKG)
-LIB_PATH = os.path.join(_PKG, "libuva_hip.so")
+# UVA_LIB_PATH: an alternative build of this library (same-box A/B of two builds, tools_ab.sh)
+LIB_PATH = os.environ.get("UVA_LIB_PATH") or os.path.join(_PKG, "libuva_hip.so")
 HEADER = os.path.join(_ROOT, "include", "uva_hip.h")
 
 _CTYPE = {
