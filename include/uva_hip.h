@@ -168,6 +168,15 @@ int uva_weighted_mean(const float* l, const float* w, int n, float* res, hipStre
 int uva_loss_grad(const float* dl, const float* w, const float* wsum, const float* g_up, int ddt, void* dout,
                   long long ld, int rows, int C2, hipStream_t stream);
 
+/* ---- diffusion sampler step (gaussian_diffusion.py:260-346,395-440; respace.py:65-130;
+ *      diffusion_action_loss.py:168-232 DiffActLoss.sample) --------------------------------
+ * out: net output [rows, ld_out] (eps | var_values, 2C columns), x/noise/x_new: fp32 [rows, C]
+ * (x_new may alias x), coef: HOST array of 8 floats {sqrt_recip_ac, sqrt_recipm1_ac, coef1,
+ * coef2, min_log (posterior_log_variance_clipped), max_log (log beta), nonzero (t != 0),
+ * temperature} of the step's spaced timestep; x_net (nullable): x_new in dtype xdt. */
+int uva_p_sample_step(int odt, const void* out, long long ld_out, const float* x, const float* noise,
+                      const float* coef, float* x_new, int xdt, void* x_net, int rows, int C, hipStream_t stream);
+
 /* ---- optimizer + EMA (policy:343-360 torch AdamW; ema_model.py:57-89) ----------------- */
 int uva_adamw_ema(float* p, const float* g, float* m, float* v, float* ema, void* p_bf16, long long n,
                   long long n_decay, float lr, float b1, float b2, float eps, float wd, int step, float grad_scale,

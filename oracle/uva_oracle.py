@@ -28,15 +28,20 @@ LATENT_SCALE = 0.2325  # data_utils.py:396
 class DiffusionTables:
     """float64 tables of the cosine schedule, spaced over all T steps like SpacedDiffusion."""
 
-    def __init__(self, T=1000):
+    def __init__(self, T=1000, use_timesteps=None):
         abar = lambda s: math.cos((s + 0.008) / 1.008 * math.pi / 2) ** 2
         b0 = np.array([min(1 - abar((i + 1) / T) / abar(i / T), 0.999) for i in range(T)])
         ac0 = np.cumprod(1.0 - b0)
-        # respacing with every step kept: betas re-derived from consecutive alpha-bars
-        prev, nb = 1.0, []
-        for a in ac0:
-            nb.append(1.0 - a / prev)
-            prev = a
+        # respacing (respace.py:65-90): betas re-derived from consecutive retained alpha-bars
+        keep = set(range(T)) if use_timesteps is None else set(use_timesteps)
+        prev, nb, tmap = 1.0, [], []
+        for i, a in enumerate(ac0):
+            if i in keep:
+                nb.append(1.0 - a / prev)
+                prev = a
+                tmap.append(i)
+        self.timestep_map = np.array(tmap, np.int64)
+        T = len(nb)
         betas = np.array(nb, dtype=np.float64)
         ac = np.cumprod(1.0 - betas)
         ac_prev = np.concatenate([[1.0], ac[:-1]])
@@ -56,6 +61,41 @@ class DiffusionTables:
     def gather(self, name, t):
         """float64 table lookup then cast to fp32 (gaussian_diffusion.py:892-904)."""
         return torch.from_numpy(getattr(self, name))[t].float()[:, None]
+
+
+def space_timesteps(num_timesteps, section_counts):
+    """respace.py:14-56 for comma-separated section counts (e.g. "100")."""
+    counts = [int(x) for x in str(section_counts).split(",")]
+    size_per, extra = num_timesteps // len(counts), num_timesteps % len(counts)
+    start, steps = 0, set()
+    for i, n in enumerate(counts):
+        size = size_per + (1 if i < extra else 0)
+        stride = 1 if n <= 1 else (size - 1) / (n - 1)
+        cur = 0.0
+        for _ in range(n):
+            steps.add(start + round(cur))
+            cur += stride
+        start += size
+    return steps
+
+
+def p_sample_loop(tb, model_fn, noise, step_noise, temperature=1.0):
+    """gaussian_diffusion.py:260-346 (p_mean_variance, learned-range variance, eps model,
+    clip_denoised) + :395-492 (p_sample / p_sample_loop_progressive); the wrapped model gets
+    the base timestep (respace.py:118-130).  step_noise[k] is the k-th randn_like draw."""
+    x = noise
+    C = x.shape[1]
+    for k, i in enumerate(reversed(range(tb.T))):
+        t = torch.full((x.shape[0],), i, dtype=torch.long)
+        out = model_fn(x, torch.from_numpy(tb.timestep_map)[t])
+        eps, v = out[:, :C], out[:, C:]
+        frac = (v + 1) / 2
+        log_var = frac * tb.gather("log_betas", t) + (1 - frac) * tb.gather("plvc", t)
+        x0 = (tb.gather("sqrt_recip_ac", t) * x - tb.gather("sqrt_recipm1_ac", t) * eps).clamp(-1, 1)
+        mean = tb.gather("coef1", t) * x0 + tb.gather("coef2", t) * x
+        nonzero = (t != 0).float()[:, None]
+        x = mean + nonzero * torch.exp(0.5 * log_var) * step_noise[k] * temperature
+    return x
 
 
 def _approx_cdf(x):
@@ -256,6 +296,14 @@ class DiffActLoss(nn.Module):
                                              target.reshape(B * S, -1), t, noise)
         return loss.reshape(B, S).mean()
 
+    def sample(self, z, noise, step_noise, temperature=1.0, respacing="100"):
+        """diffusion_action_loss.py:168-232 with cfg = 1.0 -> [B, 16, C]."""
+        B = z.shape[0]
+        c = self.trunk(z).reshape(B * 16, -1)
+        tb = DiffusionTables(1000, space_timesteps(1000, respacing))
+        x = p_sample_loop(tb, lambda xt, tt: self.net(xt, tt, c), noise, step_noise, temperature)
+        return x.reshape(B, 16, -1)
+
 
 # --------------------------------------------------------------------------------------
 # MAR (mar_con_unified.py:28-943), training forward only
@@ -379,6 +427,18 @@ class MAR(nn.Module):
         if self.clip:
             h = h[:, 64:]
         return h + self._pos(self.diffusion_temporal_embed, self.diffusion_spatial_embed)
+
+    @torch.no_grad()
+    def sample_policy(self, c, text_latents, noise, step_noise, temperature=1.0, prop=None):
+        """sample_tokens, task_mode="policy_model" (mar_con_unified.py:945-1041): one pass over
+        the fully masked grid, eval mode (no text drop), then the action head's sampler."""
+        B = c.shape[0]
+        cond = self.patchify(c.reshape(B * 4, *c.shape[2:])).reshape(B, 4, 256, -1)
+        x = torch.zeros_like(cond)
+        text = self.text_proj_cond(text_latents) if self.clip else None
+        mask = torch.ones(B, 4 * 256)
+        h = self.encode(x, cond, mask, None, text, "policy_model", prop, torch.ones(B))
+        return self.diffactloss.sample(self.decode(h), noise, step_noise, temperature)
 
     def forward(self, z, c, nactions, text_latents, mode, rng, prop=None):
         """Training forward -> (loss, video_loss, act_loss) with injected draws `rng`."""
@@ -535,10 +595,15 @@ def train_frame_indices(T=32, k=4):
     return torch.arange(0, T, T // (2 * k)) + k - 1
 
 
-def vae_input(img):
+def eval_frame_indices(T=32, k=4):
+    """[3, 11, 19, 27] for T=32 (select_frames eval=True, data_utils.py:141-142)."""
+    return torch.arange(0, T, T // k) + k - 1
+
+
+def vae_input(img, eval=False):
     """x*255 -> frame select -> /127.5-1 -> b c t h w (data_utils.py:206-226)."""
     x = img * 255.0
-    x = x[:, train_frame_indices(img.shape[1])]
+    x = x[:, (eval_frame_indices if eval else train_frame_indices)(img.shape[1])]
     return (x / 127.5 - 1).permute(0, 2, 1, 3, 4)
 
 
@@ -575,6 +640,20 @@ class PolicyOracle(nn.Module):
         for p in self.model.parameters():  # policy:421-423 (adds exact zeros)
             loss = loss + 0 * p.sum()
         return loss, (lv, la)
+
+    @torch.no_grad()
+    def predict_action(self, image, rng, temperature=0.95, n_action_steps=8):
+        """predict_action (policy:221-320), PushT: resize_image_eval -> eval frame select ->
+        VAE posterior sample (eps in (b t) order) -> sample_tokens(policy_model) -> unnormalize."""
+        B = image.shape[0]
+        x = vae_input(resize_256(image), eval=True)
+        f = x.permute(0, 2, 1, 3, 4).reshape(-1, 3, 256, 256)
+        c = self.vae_model.sample(f, torch.as_tensor(rng["vae_eps"]))
+        c = c.reshape(B, 4, *c.shape[1:])
+        act = self.model.sample_policy(c, None, torch.as_tensor(rng["noise"]), torch.as_tensor(rng["step_noise"]),
+                                       temperature)
+        pred = (act[..., :self.a_scale.numel()] - self.a_offset) / self.a_scale
+        return pred[:, :n_action_steps], pred
 
 
 # --------------------------------------------------------------------------------------

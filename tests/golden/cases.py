@@ -144,3 +144,37 @@ def policy_rng(mode, B=POLICY_B):
     r["vae_eps_x"] = hash_normal(tag + "/eps_x", (B * 4, 16, 16, 16))
     r["vae_eps_c"] = hash_normal(tag + "/eps_c", (B * 4, 16, 16, 16))
     return r
+
+
+SAMPLE_STEPS = 100  # act_diff_testing_steps="100"
+SAMPLE_TEMPERATURE = 0.95  # config/model/uva.yaml:45
+
+
+def sample_rng(variant, B=B_MAR):
+    """Injected draws of one sample_tokens(policy_model) call, in the reference's order:
+    orders (:994), x_T (diffusion_action_loss.py:212), then one randn_like per p_sample step
+    (gaussian_diffusion.py:431)."""
+    v = VARIANTS[variant]
+    tag = f"sample/{variant}"
+    rows = B * 16
+    return {
+        "orders": np.stack([np.random.default_rng(i).permutation(256) for i in range(B)]).astype(np.int64),
+        "noise": hash_normal(f"{tag}/xT", (rows, v["Da"])),
+        "step_noise": hash_normal(f"{tag}/steps", (SAMPLE_STEPS, rows, v["Da"])),
+    }
+
+
+def predict_rng(B=POLICY_B):
+    """predict_action draws: posterior eps of the 4 eval frames ((b t) order, vaekl.py:414),
+    then the sampler's x_T and per-step noise (sample_rng semantics)."""
+    r = sample_rng("pusht", B)
+    r["noise"] = hash_normal("predict/xT", (B * 16, 2))
+    r["step_noise"] = hash_normal("predict/steps", (SAMPLE_STEPS, B * 16, 2))
+    r["vae_eps"] = hash_normal("predict/eps", (B * 4, 16, 16, 16))
+    return r
+
+
+POLICY_AMP_KEYS = ("img_size", "vae_stride", "patch_size", "vae_embed_dim", "mask_ratio_min", "label_drop_prob",
+                   "attn_dropout", "proj_dropout", "diffloss_d", "diffloss_w", "diffloss_act_d", "diffloss_act_w",
+                   "num_sampling_steps", "diffusion_batch_mul", "grad_checkpointing", "predict_video",
+                   "act_diff_training_steps", "act_diff_testing_steps")

@@ -262,6 +262,27 @@ def gen_ema():
     print("ema done")
 
 
+def _ref_policy(cls, AD, amp):
+    from unified_video_action.model.common.normalizer import LinearNormalizer
+    pol = cls(
+        vae_model_params=AD(autoencoder_path=None, ddconfig=AD(vae_embed_dim=16, ch_mult=[1, 1, 2, 2, 4])),
+        autoregressive_model_params=AD(amp),
+        action_model_params=AD(predict_action=True, act_model_type="conv_fc"),
+        shape_meta=AD(action=AD(shape=[2])), n_action_steps=8, shift_action=True,
+        language_emb_model=None, task_name="pusht", task_modes=[],
+        normalizer_type="all", selected_training_mode=None, use_history_action=False,
+        use_proprioception=False, action_mask_ratio=0.5, different_history_freq=False,
+        predict_wrist_img=False, predict_proprioception=False, debug=False)
+    hash_init_(pol.vae_model, "vae.")
+    hash_init_(pol.model, "mar.")
+    norm = LinearNormalizer()
+    lim = torch.zeros(2, 2)
+    lim[1] = 512.0
+    norm.fit({"action": lim, "agent_pos": lim})
+    pol.set_normalizer(norm)
+    return pol
+
+
 def gen_policy():
     from unified_video_action.policy.unified_video_action_policy import UnifiedVideoActionPolicy
     from unified_video_action.model.common.normalizer import LinearNormalizer
@@ -274,32 +295,12 @@ def gen_policy():
     ref_mar.mar_golden = lambda **kw: ref_mar.MAR(
         norm_layer=partial(nn.LayerNorm, eps=1e-6), **cases.MAR_GOLDEN, **kw)
     amp = dict(pretrained_model_path=None, model_size="mar_golden")
-    for k in ("img_size", "vae_stride", "patch_size", "vae_embed_dim", "mask_ratio_min",
-              "label_drop_prob", "attn_dropout", "proj_dropout", "diffloss_d", "diffloss_w",
-              "diffloss_act_d", "diffloss_act_w", "num_sampling_steps", "diffusion_batch_mul",
-              "grad_checkpointing", "predict_video", "act_diff_training_steps",
-              "act_diff_testing_steps"):
+    for k in cases.POLICY_AMP_KEYS:
         amp[k] = cases.MAR_KW[k]
     out = {}
     for mode in cases.POLICY_MODES:
-        pol = UnifiedVideoActionPolicy(
-            vae_model_params=AD(autoencoder_path=None,
-                                ddconfig=AD(vae_embed_dim=16, ch_mult=[1, 1, 2, 2, 4])),
-            autoregressive_model_params=AD(amp),
-            action_model_params=AD(predict_action=True, act_model_type="conv_fc"),
-            shape_meta=AD(action=AD(shape=[2])), n_action_steps=8, shift_action=True,
-            language_emb_model=None, task_name="pusht", task_modes=[],
-            normalizer_type="all", selected_training_mode=None, use_history_action=False,
-            use_proprioception=False, action_mask_ratio=0.5, different_history_freq=False,
-            predict_wrist_img=False, predict_proprioception=False, debug=False)
-        hash_init_(pol.vae_model, "vae.")
-        hash_init_(pol.model, "mar.")
+        pol = _ref_policy(UnifiedVideoActionPolicy, AD, amp)
         pol.train()
-        norm = LinearNormalizer()
-        lim = torch.zeros(2, 2)
-        lim[1] = 512.0
-        norm.fit({"action": lim, "agent_pos": lim})
-        pol.set_normalizer(norm)
         b = cases.policy_batch()
         batch = {"obs": {"image": torch.from_numpy(b["image"]),
                          "agent_pos": torch.from_numpy(b["agent_pos"])},
@@ -328,8 +329,89 @@ def gen_policy():
     np.savez(os.path.join(OUT, "g2_policy_pusht.npz"), **out)
 
 
+def gen_sample():
+    """sample_tokens(task_mode="policy_model") of the reference on every variant (eval mode),
+    with the sampler's randn draws injected (cases.sample_rng)."""
+    out = {}
+    for variant, v in cases.VARIANTS.items():
+        m = build_mar(variant)
+        m.eval()
+        inp = {k: torch.from_numpy(x) for k, x in cases.mar_inputs(variant).items()}
+        rng = cases.sample_rng(variant)
+        q = [torch.from_numpy(a) for a in rng["step_noise"]]
+        saved = (torch.randn, torch.randn_like, torch.Tensor.cuda, ref_mar.MAR.sample_orders)
+
+        def fake_randn(*shape, **k):
+            assert tuple(shape) == rng["noise"].shape, shape
+            return torch.from_numpy(rng["noise"])
+
+        def fake_randn_like(x, *a, **k):
+            return q.pop(0).to(x.dtype)
+
+        torch.randn, torch.randn_like = fake_randn, fake_randn_like
+        torch.Tensor.cuda = lambda self, *a, **k: self
+        ref_mar.MAR.sample_orders = lambda self, bsz: torch.from_numpy(rng["orders"])
+        try:
+            prop = {k: inp[k] for k in inp if k.startswith("robot0_") and not k.endswith("_pred")}
+            _, act = m.sample_tokens(bsz=cases.B_MAR, cond=inp["c"], text_latents=inp.get("text_latents"),
+                                     num_iter=1, cfg=1.0, temperature=cases.SAMPLE_TEMPERATURE,
+                                     proprioception_input=prop, task_mode="policy_model")
+        finally:
+            torch.randn, torch.randn_like, torch.Tensor.cuda, ref_mar.MAR.sample_orders = saved
+        assert not q, "unconsumed step noise"
+        out[f"{variant}_act"] = act.detach().double().numpy()
+        print(f"sample {variant}: act sum={act.sum().item():.6f} absmax={act.abs().max().item():.4f}")
+    np.savez(os.path.join(OUT, "g5_sample.npz"), **out)
+
+
+def gen_predict():
+    """UnifiedVideoActionPolicy.predict_action (policy:221-320) of the reference, eval mode, on the
+    golden PushT policy (full KL-VAE, reduced MAR), draws injected (cases.predict_rng)."""
+    from unified_video_action.policy.unified_video_action_policy import UnifiedVideoActionPolicy
+
+    class AD(dict):
+        def __getattr__(self, k):
+            v = self[k]
+            return AD(v) if isinstance(v, dict) else v
+
+    ref_mar.mar_golden = lambda **kw: ref_mar.MAR(
+        norm_layer=partial(nn.LayerNorm, eps=1e-6), **cases.MAR_GOLDEN, **kw)
+    amp = dict(pretrained_model_path=None, model_size="mar_golden", num_iter=1, cfg=1,
+               cfg_schedule="linear", temperature=cases.SAMPLE_TEMPERATURE)
+    for k in cases.POLICY_AMP_KEYS:
+        amp[k] = cases.MAR_KW[k]
+    pol = _ref_policy(UnifiedVideoActionPolicy, AD, amp)
+    pol.eval()
+    b = cases.policy_batch()
+    rng = cases.predict_rng()
+    q_randn = [torch.from_numpy(rng["vae_eps"]), torch.from_numpy(rng["noise"])]
+    q = [torch.from_numpy(a) for a in rng["step_noise"]]
+    saved = (torch.randn, torch.randn_like, torch.Tensor.cuda, ref_mar.MAR.sample_orders)
+
+    def fake_randn(*shape, **k):
+        v = q_randn.pop(0)
+        shp = shape[0] if len(shape) == 1 and not isinstance(shape[0], int) else shape
+        assert tuple(shp) == tuple(v.shape), (shp, v.shape)
+        return v
+
+    torch.randn = fake_randn
+    torch.randn_like = lambda x, *a, **k: q.pop(0).to(x.dtype)
+    torch.Tensor.cuda = lambda self, *a, **k: self
+    ref_mar.MAR.sample_orders = lambda self, bsz: torch.from_numpy(rng["orders"])
+    try:
+        with torch.no_grad():
+            res = pol.predict_action({"image": torch.from_numpy(b["image"]),
+                                      "agent_pos": torch.from_numpy(b["agent_pos"])})
+    finally:
+        torch.randn, torch.randn_like, torch.Tensor.cuda, ref_mar.MAR.sample_orders = saved
+    assert not q and not q_randn, "unconsumed draws"
+    np.savez(os.path.join(OUT, "g5_predict_pusht.npz"), action=res["action"].double().numpy(),
+             action_pred=res["action_pred"].double().numpy())
+    print("predict pusht: action_pred", tuple(res["action_pred"].shape), res["action_pred"][0, :3].tolist())
+
+
 if __name__ == "__main__":
     which = sys.argv[1:] or ["indexing", "mar", "block", "mlp", "diffusion_math", "vae",
-                             "resize", "ema", "policy"]
+                             "resize", "ema", "policy", "sample", "predict"]
     for w in which:
         globals()[f"gen_{w}"]()

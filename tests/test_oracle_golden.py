@@ -156,3 +156,47 @@ def test_policy_compute_loss_end_to_end():
         assert max(errs.values()) < 1e-3, max(errs.items(), key=lambda kv: kv[1])
     decay, _ = O.weight_decay_split(mar.named_parameters())
     assert decay == [str(n) for n in g["decay_names"]]
+
+
+@pytest.mark.parametrize("variant", list(cases.VARIANTS))
+def test_sample_tokens_policy_oracle(variant):
+    """sample_tokens(policy_model): encoder/decoder pass + 100-step spaced reverse diffusion of the
+    action head (mar_con_unified.py:945-1041, diffusion_action_loss.py:168-232), vs the reference."""
+    g = replay.load("g5_sample.npz")
+    mar = O.MAR(**replay.mar_ctor_kwargs(variant))
+    hash_init_(mar, "mar.")
+    mar.eval()
+    inp = {k: torch.from_numpy(x) for k, x in cases.mar_inputs(variant).items()}
+    rng = cases.sample_rng(variant)
+    prop = {k: inp[k] for k in inp if k.startswith("robot0_") and not k.endswith("_pred")}
+    act = mar.sample_policy(inp["c"], inp.get("text_latents"), torch.from_numpy(rng["noise"]),
+                            torch.from_numpy(rng["step_noise"]), cases.SAMPLE_TEMPERATURE, prop)
+    np.testing.assert_allclose(act.double().numpy(), g[f"{variant}_act"], rtol=0, atol=1e-5)
+
+
+def test_spaced_schedule_matches_oracle():
+    """product schedule (respace.py:14-90 restated in diffusion.py) == oracle tables, per step."""
+    from unified_video_action_amd.model.autoregressive.diffusion import SamplingSchedule, space_timesteps
+    assert space_timesteps(1000, "100") == sorted(O.space_timesteps(1000, "100"))
+    tb = O.DiffusionTables(1000, O.space_timesteps(1000, "100"))
+    ss = SamplingSchedule(1000, "100")
+    assert [s[1] for s in ss.steps] == list(tb.timestep_map[::-1])
+    for t, base, coef in ss.steps:
+        tt = torch.tensor([t])
+        want = [tb.gather(n, tt).item() for n in ("sqrt_recip_ac", "sqrt_recipm1_ac", "coef1", "coef2",
+                                                  "plvc", "log_betas")] + [float(t != 0)]
+        assert coef == want, (t, coef, want)
+
+
+def test_predict_action_end_to_end_oracle():
+    """predict_action (policy:221-320): eval resize/select -> full VAE -> sample_tokens -> unnormalize."""
+    g = replay.load("g5_predict_pusht.npz")
+    mar = O.MAR(**replay.mar_ctor_kwargs("pusht"))
+    hash_init_(mar, "mar.")
+    vae = O.AutoencoderKLEncoder()
+    hash_init_(vae, "vae.")
+    pol = O.PolicyOracle(mar, vae, [2 / 512, 2 / 512], [-1.0, -1.0]).eval()
+    b = cases.policy_batch()
+    action, pred = pol.predict_action(torch.from_numpy(b["image"]), cases.predict_rng(), cases.SAMPLE_TEMPERATURE)
+    np.testing.assert_allclose(pred.double().numpy(), g["action_pred"], rtol=0, atol=2e-3)
+    np.testing.assert_allclose(action.double().numpy(), g["action"], rtol=0, atol=2e-3)

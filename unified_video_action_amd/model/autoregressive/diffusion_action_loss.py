@@ -4,6 +4,7 @@
 Trunk: z [B, 4*256, D] -> per-frame NHWC 16x16 -> conv3x3+ReLU (implicit-GEMM HIP conv,
 fused ReLU epilogue) -> AdaptiveAvgPool(4,4) -> fc(ReLU) -> fc -> Linear(4->16 frames)
 -> refine MLP -> SimpleMLPAdaLN diffusion loss over B*16 rows (plain mean).
+sample(): the same trunk, then the spaced reverse-diffusion loop (sampler.ActionSampler).
 """
 import torch
 import torch.nn as nn
@@ -13,6 +14,7 @@ from ...native import ops
 from ...runtime import cdt
 from .diffusion_loss import SimpleMLPAdaLN, diffusion_head_loss, schedule
 from .functional import F32, as_dtype, grad_buf, linear
+from .sampler import ActionSampler
 
 
 class Conv3x3ReluFn(torch.autograd.Function):
@@ -69,6 +71,8 @@ class DiffActLoss(nn.Module):
         self.refine = nn.Sequential(nn.Linear(z_channels, z_channels), nn.ReLU(), nn.Linear(z_channels, z_channels))
         self.net = SimpleMLPAdaLN(target_channels, width, target_channels * 2, z_channels, depth, grad_checkpointing)
         self.num_timesteps = act_diff_training_steps
+        self.act_diff_testing_steps = act_diff_testing_steps
+        self._sampler = None
 
     def trunk(self, z):
         B, N, D = z.shape
@@ -87,3 +91,27 @@ class DiffActLoss(nn.Module):
         c = self.trunk(z).reshape(bsz * seq_len, -1)
         return diffusion_head_loss(self.net, schedule(self.num_timesteps, target.device),
                                    target.reshape(bsz * seq_len, -1), c, None, t, noise)
+
+    @torch.no_grad()
+    def sample(self, z, temperature=1.0, cfg=1.0, text_latents=None, noise=None, step_noise=None):
+        """z [B, 4*256, D] decoder tokens -> sampled action latents [B, 16, C]
+        (diffusion_action_loss.py:168-232).  noise [B*16, C] (x_T) and step_noise [S, B*16, C]
+        (the per-step randn_like of p_sample, gaussian_diffusion.py:431) may be injected."""
+        if cfg != 1.0:
+            # forward_with_cfg needs a doubled (cond, uncond) batch; the policy/inverse paths
+            # always sample the action head with act_cfg = 1.0 (mar_con_unified.py:1031-1036).
+            raise NotImplementedError("classifier-free guidance on the action head is not on the policy path")
+        c = self.trunk(z)
+        bsz, seq_len, _ = c.shape
+        rows = bsz * seq_len
+        if self._sampler is None:
+            self._sampler = ActionSampler(self.net, self.act_diff_testing_steps)
+        S = self._sampler.sched.S
+        dev = z.device
+        if noise is None:
+            noise = torch.randn(rows, self.in_channels, device=dev)
+        if step_noise is None:
+            step_noise = torch.randn(S, rows, self.in_channels, device=dev)
+        x = self._sampler(c.reshape(rows, -1).float().contiguous(), noise.to(dev, F32).reshape(rows, -1),
+                          step_noise.to(dev, F32).reshape(S, rows, -1), temperature)
+        return x.reshape(bsz, seq_len, -1)

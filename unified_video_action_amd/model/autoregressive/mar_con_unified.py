@@ -293,6 +293,42 @@ class MAR(nn.Module):
         return self.forward_loss(z, gt, mask, nactions, task_mode, proprioception_input, draws)
 
 
+    # ---- inference (:945-1047), policy / inverse paths ---------------------------------
+    @torch.no_grad()
+    def sample_tokens(self, bsz, cond, text_latents=None, num_iter=64, cfg=1.0, cfg_schedule="linear",
+                      temperature=1.0, progress=False, history_nactions=None, nactions=None,
+                      proprioception_input={}, task_mode=None, vae_model=None, x=None, rng=None):
+        """policy_model / inverse_model: one encoder+decoder pass over the (fully masked) token
+        grid, then the action head's reverse diffusion (act_cfg = 1.0) -> (None, actions
+        [B, 16, Da]).  The reference returns on the first MaskGIT iteration for these modes
+        (:1040-1041); the video-generation loop (:1043-1100) is not on this path.  `rng` may
+        inject {"noise": x_T, "step_noise": [S, B*16, Da]} (the sampler's randn draws)."""
+        if task_mode not in ("policy_model", "inverse_model"):
+            raise NotImplementedError(f"sample_tokens task_mode={task_mode}: video generation loop not built")
+        if not self.predict_action:
+            raise NotImplementedError("sample_tokens without an action head returns nothing on this path")
+        rng = rng or {}
+        dev = cond.device
+        cnd = self.to_tokens(cond).to(F32)
+        B = cnd.shape[0]
+        if text_latents is not None and self.clip:
+            text_latents = linear(text_latents.to(dev).float(), self.text_proj_cond, out_dtype=F32)
+        if task_mode == "inverse_model":
+            tokens = self.to_tokens(x).to(F32)
+            mask = torch.zeros(B, self.n_frames * self.seq_len, device=dev)
+        else:
+            tokens = torch.zeros(B, self.n_frames, self.seq_len, self.token_embed_dim, device=dev)
+            mask = torch.ones(B, self.n_frames * self.seq_len, device=dev)
+        if "orders" not in rng:
+            self.sample_orders(bsz)  # drawn but unused on these paths (:994), kept for RNG parity
+        h = self.forward_mae_encoder(tokens, mask, cnd, text_latents, nactions, task_mode, proprioception_input,
+                                     torch.ones(B))
+        z = self.forward_mae_decoder(h)
+        act = self.diffactloss.sample(z, temperature, cfg=1.0, text_latents=text_latents,
+                                      noise=rng.get("noise"), step_noise=rng.get("step_noise"))
+        return None, act
+
+
 def _mar(D, depth, heads, **kwargs):
     return MAR(encoder_embed_dim=D, encoder_depth=depth, encoder_num_heads=heads, decoder_embed_dim=D,
                decoder_depth=depth, decoder_num_heads=heads, mlp_ratio=4,

@@ -1,0 +1,168 @@
+"""Reverse-diffusion sampler of the action head (inference path).
+
+Reference: DiffActLoss.sample (diffusion_action_loss.py:168-232) ->
+gen_diffusion.p_sample_loop (gaussian_diffusion.py:395-492) over the spaced cosine
+schedule (create_diffusion(timestep_respacing=act_diff_testing_steps), respace.py:65-130),
+with the SimpleMLPAdaLN net (diffusion_loss.py:192-283) as the eps / variance model.
+
+MI355X layout of one sampling call over R = B*16 action rows and S spaced steps:
+  * everything that depends only on (cond, t) is hoisted out of the step loop: the
+    cond embedding once, the S timestep embeddings once, and the adaLN modulation of
+    every res block and the final layer for ALL steps as ONE [S*R, W] x [W, (3d+2)W]
+    GEMM (the sampler's dominant FLOPs; per step it would be S launches at M=R);
+  * the step loop is what is left: input_proj, d x (adaLN-LN, fc1+SiLU, fc2+gate+residual),
+    final LN-modulate, final linear, and the fused p_sample update kernel
+    (uva_p_sample_step) -- replayed from a captured HIP graph after one eager step
+    (which also settles the per-shape GEMM route choices before capture).
+No autograd and no backward residues (the training trunk's aux tensors) are produced.
+"""
+import torch
+
+from ...native import ops
+from ...runtime import cdt
+from .diffusion import SamplingSchedule, timestep_freqs
+from .functional import F32, compute_weight
+
+_SCHED = {}
+
+
+def sampling_schedule(respacing, T=1000):
+    key = (T, str(respacing))
+    if key not in _SCHED:
+        _SCHED[key] = SamplingSchedule(T, str(respacing))
+    return _SCHED[key]
+
+
+class ActionSampler:
+    """One p_sample_loop over the SimpleMLPAdaLN `net` conditioned on c [R, z] (fp32)."""
+
+    MOD_BYTES_CAP = 16 << 30  # all-step modulation table above this is computed per step
+
+    def __init__(self, net, respacing="100", use_graph=True):
+        self.net = net
+        self.sched = sampling_schedule(respacing)
+        self.use_graph = use_graph
+
+    # ---- hoisted conditioning -------------------------------------------------------------
+    def _weights(self):
+        net = self.net
+        blocks = [b.trunk_params() for b in net.res_blocks]
+        fl = net.final_layer.trunk_params()
+        wcat = torch.cat([compute_weight(b[0]) for b in blocks] + [compute_weight(fl[0])], 0).contiguous()
+        bcat = torch.cat([b[1].detach() for b in blocks] + [fl[1].detach()], 0).float().contiguous()
+        return blocks, fl, wcat, bcat
+
+    def _time_embed(self, dev):
+        te = self.net.time_embed
+        tmap = torch.tensor([s[1] for s in self.sched.steps], dtype=torch.int64, device=dev)
+        f = torch.empty(tmap.numel(), te.frequency_embedding_size, dtype=cdt(), device=dev)
+        ops.timestep_features(tmap, timestep_freqs(dev), f)
+        h = torch.empty(tmap.numel(), te.mlp[0].weight.shape[0], dtype=cdt(), device=dev)
+        ops.linear(f, compute_weight(te.mlp[0].weight), h, bias=te.mlp[0].bias.detach(), act="silu")
+        out = torch.empty(tmap.numel(), te.mlp[2].weight.shape[0], dtype=F32, device=dev)
+        ops.linear(h, compute_weight(te.mlp[2].weight), out, bias=te.mlp[2].bias.detach())
+        return out  # [S, W], row k = step k of the loop
+
+    def _modulation(self, c, st):
+        """sy_k = SiLU(cond_embed(c) + t_emb_k);  mod[k] = sy_k @ wcat^T + bcat -> st["mod"] [S, R, (3d+2)W]
+        (or st["sy"] only, when the all-step table is over MOD_BYTES_CAP)."""
+        net = self.net
+        R = c.shape[0]
+        W = net.model_channels
+        dev = c.device
+        yc = torch.empty(R, W, dtype=F32, device=dev)
+        ops.linear(c.to(cdt()).contiguous(), compute_weight(net.cond_embed.weight), yc,
+                   bias=net.cond_embed.bias.detach())
+        te = self._time_embed(dev)
+        S = te.shape[0]
+        y = yc[None] + te[:, None]  # [S, R, W] fp32 (t + c, diffusion_loss.py:276-278)
+        ops.act_fwd(y, st["sy"], "silu")
+        del y
+        if st["mod"] is not None:
+            ncol = st["wcat"].shape[0]
+            ops.linear(st["sy"].reshape(S * R, W), st["wcat"], st["mod"].reshape(S * R, ncol), bias=st["bcat"])
+
+    # ---- one reverse step (captured) --------------------------------------------------------
+    def _step(self, k, st):
+        net = self.net
+        R, C, W = st["R"], st["C"], net.model_channels
+        blocks, fl, mod_all = st["blocks"], st["fl"], st["mod"]
+        if mod_all is None:
+            mod = st["mod_buf"]
+            ops.linear(st["sy"][k], st["wcat"], mod, bias=st["bcat"])
+        else:
+            mod = mod_all[k]
+        ncol = mod.shape[1]
+        x = st["h0"]
+        ops.linear(st["x_net"], compute_weight(net.input_proj.weight), x, bias=net.input_proj.bias.detach())
+        for i, (modw, modb, w1, b1, w2, b2, lnw, lnb) in enumerate(blocks):
+            m = mod[:, 3 * W * i:3 * W * (i + 1)]
+            ops.layernorm_fwd(x, lnw.detach(), lnb.detach(), st["h"], st["mean"], st["rstd"],
+                              scale=m[:, W:2 * W], shift=m[:, :W], ldm=ncol)
+            ops.linear(st["h"], compute_weight(w1), st["a"], bias=b1.detach(), act="silu")
+            xn = st["h1"] if x is st["h0"] else st["h0"]
+            ops.linear(st["a"], compute_weight(w2), xn, bias=b2.detach(), gate=m[:, 2 * W:3 * W], residual=x)
+            x = xn
+        fm = mod[:, 3 * W * len(blocks):]
+        ops.layernorm_fwd(x, None, None, st["h"], st["mean"], st["rstd"], scale=fm[:, W:2 * W], shift=fm[:, :W],
+                          ldm=ncol)
+        ops.linear(st["h"], compute_weight(fl[2]), st["out"], bias=fl[3].detach())
+        coef = list(self.sched.steps[k][2]) + [st["temperature"]]
+        ops.p_sample_step(st["out"], st["x"], st["noise"][k], coef, st["x"], st["x_net"])
+
+    def _state(self, R, C, dev, temperature):
+        """Persistent step buffers (+ captured graph) per (rows, channels, dtype, weights)."""
+        net = self.net
+        cd = cdt()
+        sig = (R, C, str(cd), float(temperature), str(dev),
+               tuple((p.data_ptr(), p._version) for p in net.parameters()))
+        cache = getattr(self, "_cache", None)
+        if cache is not None and cache["sig"] == sig:
+            return cache
+        W = net.model_channels
+        S = self.sched.S
+        blocks, fl, wcat, bcat = self._weights()
+        ncol = wcat.shape[0]
+        per_step = S * R * ncol * (torch.finfo(cd).bits // 8) > self.MOD_BYTES_CAP
+        st = dict(sig=sig, R=R, C=C, blocks=blocks, fl=fl, wcat=wcat, bcat=bcat, temperature=float(temperature),
+                  sy=torch.empty(S, R, W, dtype=cd, device=dev),
+                  mod=None if per_step else torch.empty(S, R, ncol, dtype=cd, device=dev),
+                  mod_buf=torch.empty(R, ncol, dtype=cd, device=dev) if per_step else None,
+                  x=torch.empty(R, C, dtype=F32, device=dev), noise=torch.empty(S, R, C, dtype=F32, device=dev),
+                  x_net=torch.empty(R, C, dtype=cd, device=dev),
+                  h0=torch.empty(R, W, dtype=F32, device=dev), h1=torch.empty(R, W, dtype=F32, device=dev),
+                  h=torch.empty(R, W, dtype=cd, device=dev), a=torch.empty(R, W, dtype=cd, device=dev),
+                  mean=torch.empty(R, dtype=F32, device=dev), rstd=torch.empty(R, dtype=F32, device=dev),
+                  out=torch.empty(R, 2 * C, dtype=F32, device=dev), graph=None)
+        self._cache = st
+        return st
+
+    @torch.no_grad()
+    def __call__(self, c, noise, step_noise, temperature=1.0):
+        """c [R, z] fp32 cond, noise [R, C] x_T, step_noise [S, R, C] -> x_0 [R, C] fp32."""
+        dev = c.device
+        R, C = noise.shape
+        S = self.sched.S
+        if step_noise.shape != (S, R, C):
+            raise ValueError(f"step_noise {tuple(step_noise.shape)} != {(S, R, C)}")
+        if c.shape[0] != R:
+            raise ValueError(f"cond rows {c.shape[0]} != noise rows {R}")
+        st = self._state(R, C, dev, temperature)
+        self._modulation(c, st)
+        st["x"].copy_(noise)
+        st["x_net"].copy_(noise)
+        st["noise"].copy_(step_noise)
+        self._step(0, st)  # eager: settles GEMM routes and workspaces before capture
+        if S > 1 and self.use_graph and dev.type == "cuda":
+            if st["graph"] is None:
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g):
+                    for k in range(1, S):
+                        self._step(k, st)
+                st["graph"] = g
+                # capture records without executing: run the captured steps once now
+            st["graph"].replay()
+        else:
+            for k in range(1, S):
+                self._step(k, st)
+        return st["x"].clone()

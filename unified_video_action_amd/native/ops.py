@@ -259,6 +259,22 @@ def diffusion_loss(x0, noise, t, out, tables, loss_row, dl):
                ctypes.cast(arr, ctypes.c_void_p), ptr(loss_row), ptr(dl), rows, C, stream())
 
 
+def p_sample_step(out, x, noise, coef, x_new, x_net=None):
+    """One reverse diffusion step (uva_p_sample_step); coef = 8 python floats of the step."""
+    rows, C = x.shape
+    if out.shape[0] != rows or out.shape[1] != 2 * C or out.stride(1) != 1:
+        raise ValueError(f"p_sample_step: out {tuple(out.shape)} vs x {tuple(x.shape)}")
+    for t in (x, noise, x_new):
+        if t.dtype != torch.float32 or not t.is_contiguous() or t.shape != x.shape:
+            raise ValueError("p_sample_step: x / noise / x_new must be contiguous fp32 [rows, C]")
+    if x_net is not None and (not x_net.is_contiguous() or x_net.shape != x.shape):
+        raise ValueError("p_sample_step: x_net must be contiguous [rows, C]")
+    k = (ctypes.c_float * 8)(*coef)
+    lib().call("uva_p_sample_step", dt(out), ptr(out), out.stride(0), ptr(x), ptr(noise),
+               ctypes.cast(k, ctypes.c_void_p), ptr(x_new), dt(x_net) if x_net is not None else 0,
+               ptr(x_net), rows, C, stream())
+
+
 def weighted_mean(l, w, res):
     lib().call("uva_weighted_mean", ptr(l), ptr(w), l.numel(), ptr(res), stream())
 

@@ -7,8 +7,9 @@ shape_meta, n_action_steps, shift_action, language_emb_model, task_name, task_mo
 same training surface: forward(batch) -> (loss, (video_loss, action_loss)),
 compute_loss, get_optimizer(weight_decay, learning_rate, betas), set_normalizer,
 add_weight_decay.  The step runs on libuva_hip.so end to end (frame select+resize,
-VAE encoder, MAR, diffusion heads, backward); inference (`predict_action`) is the §8f
-"next" row and raises.
+VAE encoder, MAR, diffusion heads, backward).  Inference: predict_action(obs_dict) ->
+{"action", "action_pred"} on the same kernels plus the HIP-graph reverse-diffusion sampler
+(policy:221-320).
 
 Differences that do not change results: frames are selected before the bilinear resize
 (per-frame op), and the "loss += 0*p.sum()" DDP workaround (policy:421-423) is replaced
@@ -72,6 +73,9 @@ class UnifiedVideoActionPolicy(nn.Module):
             p.requires_grad = False
 
         ap = autoregressive_model_params
+        self.sample_params = dict(num_iter=_get(ap, "num_iter", 1), cfg=_get(ap, "cfg", 1.0),
+                                  cfg_schedule=_get(ap, "cfg_schedule", "linear"),
+                                  temperature=_get(ap, "temperature", 0.95))
         self.model = getattr(mar, _get(ap, "model_size", "mar_base"))(
             img_size=_get(ap, "img_size", 256), vae_stride=_get(ap, "vae_stride", 16),
             patch_size=_get(ap, "patch_size", 1), vae_embed_dim=_get(ap, "vae_embed_dim", 16),
@@ -171,5 +175,58 @@ class UnifiedVideoActionPolicy(nn.Module):
     def forward(self, batch, **kwargs):
         return self.compute_loss(batch, **kwargs)
 
-    def predict_action(self, obs_dict, language_goal=None):
-        raise NotImplementedError("inference sampler (MAR.sample_tokens + DiffActLoss.sample) is SURVEY §8f next")
+    _EVAL_IMAGE_KEYS = (("libero", "agentview_image"), ("toolhang", "sideview_image"), ("umi", "camera0_rgb"))
+
+    @torch.no_grad()
+    def predict_action(self, obs_dict, language_goal=None, rng=None):
+        """obs_dict: {"image" (or the task's camera key): [B,T,3,H,W] in [0,1], low-dim keys}
+        -> {"action": [B, n_action_steps, Da], "action_pred": [B, 16, Da]}  (policy:221-320).
+        language_goal: precomputed text latents [B, 512] (CLIP needs network weights).
+        rng injects {"vae_eps": [B*4,16,16,16] (posterior.sample, reference (b t) order),
+        "noise", "step_noise"} for parity runs."""
+        rng = rng or {}
+        obs = dict(obs_dict)
+        for task, key in self._EVAL_IMAGE_KEYS:  # resize_image_eval key mapping (data_utils.py:86-104)
+            if task in self.task_name and key in obs:
+                obs["image"] = obs.pop(key)
+        img = obs["image"]
+        B, T = img.shape[:2]
+        dev = img.device
+        text_latents = None
+        if self.language_emb_model == "clip":
+            if not torch.is_tensor(language_goal):
+                raise NotImplementedError("CLIP text encoding needs network weights; pass text latents [B, 512]")
+            text_latents = language_goal.to(dev).float()
+        if self.normalizer_type == "all":  # normalize_obs: every non-image key (data_utils.py:185-203)
+            for k in list(obs):
+                if "image" not in k and k in self.normalizer:
+                    obs[k] = self.normalizer[k].normalize(obs[k])
+        prop = {}
+        if "umi" in self.task_name:
+            sel = np.arange(T)
+            if self.use_proprioception:
+                idx = obs["img_indices"].int().squeeze(2) if "img_indices" in obs else None
+                prop = umi_proprioception(obs, idx, self.different_history_freq, train=False)
+        else:
+            sel = select_frame_indices(T, eval=True)
+        if len(sel) % 2:
+            raise ValueError(f"eval frame selection {sel.tolist()} must hold an even number of frames")
+        x = vae_images(img, sel, self.vae_model.CIN_PAD)  # [sel[h:] per sample | sel[:h] per sample]
+        h = len(sel) // 2
+        eps = rng.get("vae_eps")
+        if eps is not None:
+            e = torch.as_tensor(eps).to(dev).reshape(B, 2, h, *eps.shape[1:])
+            eps = torch.cat([e[:, 1].reshape(B * h, *eps.shape[1:]), e[:, 0].reshape(B * h, *eps.shape[1:])])
+        else:
+            eps = torch.randn(B * len(sel), self.vae_model.embed_dim, 16, 16, device=dev)
+        tok = self.vae_model.encode_tokens(x, eps).reshape(2, B, h, 256, -1)
+        c = torch.cat([tok[1], tok[0]], dim=1)  # [B, len(sel), 256, 16] in selection order
+        sp = self.sample_params
+        _, act = self.model.sample_tokens(bsz=B, cond=c, text_latents=text_latents, num_iter=sp["num_iter"],
+                                          cfg=sp["cfg"], cfg_schedule=sp["cfg_schedule"],
+                                          temperature=sp["temperature"], proprioception_input=prop,
+                                          task_mode="policy_model", vae_model=self.vae_model, rng=rng)
+        action_pred = act[..., :self.action_dim]
+        if self.normalizer_type == "all":
+            action_pred = self.normalizer["action"].unnormalize(action_pred)
+        return {"action": action_pred[:, :self.n_action_steps], "action_pred": action_pred}
