@@ -1394,9 +1394,10 @@ static int launch_mfma(int ta, int tb, const void* A, const void* B, void* C, in
   const int nblk = ((M + MB_M - 1) / MB_M) * ((N + MB_N - 1) / MB_N);
   // split-K when the output tiling cannot fill the chip (dW GEMMs: few tiles, K = tokens)
   int splits = 1;
-  if (batch == 1 && ws && nblk < 256 && K >= 4 * MB_K) {
+  static const int minks = env_int("UVA_SPLITK_MIN_KSTEPS", 4);  // K steps (x MB_K) per split, at least (sampler: 4 > 2)
+  if (batch == 1 && ws && nblk < 256 && K >= 2 * minks * MB_K) {
     splits = (512 + nblk - 1) / nblk;
-    int kmax = K / (2 * MB_K);
+    int kmax = K / (minks * MB_K);
     if (splits > kmax) splits = kmax;
     if (splits > 16) splits = 16;
     while (splits > 1 && (long long)splits * M * N > ws_floats) --splits;
