@@ -177,6 +177,18 @@ int uva_loss_grad(const float* dl, const float* w, const float* wsum, const floa
 int uva_p_sample_step(int odt, const void* out, long long ld_out, const float* x, const float* noise,
                       const float* coef, float* x_new, int xdt, void* x_net, int rows, int C, hipStream_t stream);
 
+/* ---- few-row fused linear of the action sampler (inference, bf16; diffusion_loss.py:142-189)
+ * out[R,N] = epi(A' W^T + bias), W bf16 [N,K] (K in {256, 512, 1024}), R any.
+ * ln = 1: A = fp32 residual rows x [R, lda]; A' = (LN(x)[*lnw + lnb]) * (1 + scale) + shift
+ *         (lnw/lnb nullable; shift/scale bf16 columns of the adaLN modulation, row stride ldm).
+ * ln = 0: A' = A bf16 [R, lda].  act: 0 or 2 (SiLU).  gate/res (both or neither, fp32 out):
+ * out = res + gate * v.  Supported: (ln, SiLU, bf16 out), (ln, none, fp32 out),
+ * (plain, gate, fp32 out), (plain, SiLU, bf16 out). */
+int uva_sampler_linear(int ln, const void* A, long long lda, const float* lnw, const float* lnb, const void* shift,
+                       const void* scale, long long ldm, float eps, const void* W, const float* bias, int act,
+                       const void* gate, long long ldg, const float* res, long long ldr, int odt, void* out,
+                       long long ldo, int R, int N, int K, hipStream_t stream);
+
 /* ---- optimizer + EMA (policy:343-360 torch AdamW; ema_model.py:57-89) ----------------- */
 int uva_adamw_ema(float* p, const float* g, float* m, float* v, float* ema, void* p_bf16, long long n,
                   long long n_decay, float lr, float b1, float b2, float eps, float wd, int step, float grad_scale,

@@ -429,15 +429,21 @@ class MAR(nn.Module):
         return h + self._pos(self.diffusion_temporal_embed, self.diffusion_spatial_embed)
 
     @torch.no_grad()
-    def sample_policy(self, c, text_latents, noise, step_noise, temperature=1.0, prop=None):
-        """sample_tokens, task_mode="policy_model" (mar_con_unified.py:945-1041): one pass over
-        the fully masked grid, eval mode (no text drop), then the action head's sampler."""
+    def sample_policy(self, c, text_latents, noise, step_noise, temperature=1.0, prop=None, mode="policy_model",
+                      x=None):
+        """sample_tokens, task_mode policy_model / inverse_model (mar_con_unified.py:945-1041): one
+        pass over the fully masked (policy) or fully visible (inverse, tokens = x) grid, eval mode
+        (no text drop), then the action head's sampler."""
         B = c.shape[0]
         cond = self.patchify(c.reshape(B * 4, *c.shape[2:])).reshape(B, 4, 256, -1)
-        x = torch.zeros_like(cond)
+        if mode == "inverse_model":
+            x = self.patchify(x.reshape(B * 4, *x.shape[2:])).reshape(B, 4, 256, -1)
+            mask = torch.zeros(B, 4 * 256)
+        else:
+            x = torch.zeros_like(cond)
+            mask = torch.ones(B, 4 * 256)
         text = self.text_proj_cond(text_latents) if self.clip else None
-        mask = torch.ones(B, 4 * 256)
-        h = self.encode(x, cond, mask, None, text, "policy_model", prop, torch.ones(B))
+        h = self.encode(x, cond, mask, None, text, mode, prop, torch.ones(B))
         return self.diffactloss.sample(self.decode(h), noise, step_noise, temperature)
 
     def forward(self, z, c, nactions, text_latents, mode, rng, prop=None):

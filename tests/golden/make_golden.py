@@ -356,11 +356,17 @@ def gen_sample():
             _, act = m.sample_tokens(bsz=cases.B_MAR, cond=inp["c"], text_latents=inp.get("text_latents"),
                                      num_iter=1, cfg=1.0, temperature=cases.SAMPLE_TEMPERATURE,
                                      proprioception_input=prop, task_mode="policy_model")
+            assert not q, "unconsumed step noise"
+            q = [torch.from_numpy(a) for a in rng["step_noise"]]
+            _, inv = m.sample_tokens(bsz=cases.B_MAR, cond=inp["c"], text_latents=inp.get("text_latents"),
+                                     num_iter=1, cfg=1.0, temperature=cases.SAMPLE_TEMPERATURE,
+                                     proprioception_input=prop, task_mode="inverse_model", x=inp["z"])
         finally:
             torch.randn, torch.randn_like, torch.Tensor.cuda, ref_mar.MAR.sample_orders = saved
         assert not q, "unconsumed step noise"
         out[f"{variant}_act"] = act.detach().double().numpy()
-        print(f"sample {variant}: act sum={act.sum().item():.6f} absmax={act.abs().max().item():.4f}")
+        out[f"{variant}_inverse_act"] = inv.detach().double().numpy()
+        print(f"sample {variant}: act sum={act.sum().item():.6f} inverse sum={inv.sum().item():.6f}")
     np.savez(os.path.join(OUT, "g5_sample.npz"), **out)
 
 

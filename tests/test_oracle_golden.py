@@ -172,6 +172,10 @@ def test_sample_tokens_policy_oracle(variant):
     act = mar.sample_policy(inp["c"], inp.get("text_latents"), torch.from_numpy(rng["noise"]),
                             torch.from_numpy(rng["step_noise"]), cases.SAMPLE_TEMPERATURE, prop)
     np.testing.assert_allclose(act.double().numpy(), g[f"{variant}_act"], rtol=0, atol=1e-5)
+    inv = mar.sample_policy(inp["c"], inp.get("text_latents"), torch.from_numpy(rng["noise"]),
+                            torch.from_numpy(rng["step_noise"]), cases.SAMPLE_TEMPERATURE, prop,
+                            mode="inverse_model", x=inp["z"])
+    np.testing.assert_allclose(inv.double().numpy(), g[f"{variant}_inverse_act"], rtol=0, atol=1e-5)
 
 
 def test_spaced_schedule_matches_oracle():

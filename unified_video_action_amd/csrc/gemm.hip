@@ -1394,7 +1394,10 @@ static int launch_mfma(int ta, int tb, const void* A, const void* B, void* C, in
   const int nblk = ((M + MB_M - 1) / MB_M) * ((N + MB_N - 1) / MB_N);
   // split-K when the output tiling cannot fill the chip (dW GEMMs: few tiles, K = tokens)
   int splits = 1;
-  static const int minks = env_int("UVA_SPLITK_MIN_KSTEPS", 4);  // K steps (x MB_K) per split, at least (sampler: 4 > 2)
+  // K steps (x MB_K) per split, at least: 2 for the long-K training products; 4 for few-row GEMMs
+  // (M <= 1024: the inference sampler's 1024x1024 layers, 41 -> 34 ms per 100-step loop at B=32)
+  static const int minks_env = env_int("UVA_SPLITK_MIN_KSTEPS", 0);
+  const int minks = minks_env > 0 ? minks_env : (M <= 1024 ? 4 : 2);
   if (batch == 1 && ws && nblk < 256 && K >= 2 * minks * MB_K) {
     splits = (512 + nblk - 1) / nblk;
     int kmax = K / (minks * MB_K);

@@ -10,12 +10,16 @@ MI355X layout of one sampling call over R = B*16 action rows and S spaced steps:
     cond embedding once, the S timestep embeddings once, and the adaLN modulation of
     every res block and the final layer for ALL steps as ONE [S*R, W] x [W, (3d+2)W]
     GEMM (the sampler's dominant FLOPs; per step it would be S launches at M=R);
-  * the step loop is what is left: input_proj, d x (adaLN-LN, fc1+SiLU, fc2+gate+residual),
-    final LN-modulate, final linear, and the fused p_sample update kernel
-    (uva_p_sample_step) -- replayed from a captured HIP graph after one eager step
+  * the step loop is what is left: input_proj, d x (adaLN-LN, fc1 + SiLU, fc2 + gate +
+    residual) and LN-modulate + final linear, the linears as few-row fused kernels
+    (uva_sampler_linear: 32x64 tiles over the full K, weights preloaded into registers,
+    optional LayerNorm in the A staging -- used for the final layer),
+    and the fused p_sample update kernel (uva_p_sample_step) -- replayed from a captured HIP graph after one eager step
     (which also settles the per-shape GEMM route choices before capture).
 No autograd and no backward residues (the training trunk's aux tensors) are produced.
 """
+import os
+
 import torch
 
 from ...native import ops
@@ -38,10 +42,14 @@ class ActionSampler:
 
     MOD_BYTES_CAP = 16 << 30  # all-step modulation table above this is computed per step
 
-    def __init__(self, net, respacing="100", use_graph=True):
+    def __init__(self, net, respacing="100", use_graph=True, use_fused=True):
         self.net = net
         self.sched = sampling_schedule(respacing)
         self.use_graph = use_graph
+        self.use_fused = use_fused  # few-row fused LN+linear kernels (bf16 compute, width <= 1024)
+        # LN inside fc1's A staging: every 64-column block re-normalises its 32 rows (16x redundant
+        # at width 1024), measured slower than the separate LN kernel (B=32: 27.8 vs 26.0 ms / loop)
+        self.fuse_ln = os.environ.get("UVA_SAMPLER_FUSE_LN", "0") == "1"
 
     # ---- hoisted conditioning -------------------------------------------------------------
     def _weights(self):
@@ -92,9 +100,34 @@ class ActionSampler:
             ops.linear(st["sy"][k], st["wcat"], mod, bias=st["bcat"])
         else:
             mod = mod_all[k]
-        ncol = mod.shape[1]
         x = st["h0"]
         ops.linear(st["x_net"], compute_weight(net.input_proj.weight), x, bias=net.input_proj.bias.detach())
+        if st["fused"]:
+            for i, (modw, modb, w1, b1, w2, b2, lnw, lnb) in enumerate(blocks):
+                m = mod[:, 3 * W * i:3 * W * (i + 1)]
+                if self.fuse_ln:
+                    ops.sampler_linear(x, compute_weight(w1), st["a"], bias=b1.detach(), act="silu", ln=True,
+                                       lnw=lnw.detach(), lnb=lnb.detach(), shift=m[:, :W], scale=m[:, W:2 * W])
+                else:
+                    ops.layernorm_fwd(x, lnw.detach(), lnb.detach(), st["h"], st["mean"], st["rstd"],
+                                      scale=m[:, W:2 * W], shift=m[:, :W], ldm=mod.shape[1])
+                    ops.sampler_linear(st["h"], compute_weight(w1), st["a"], bias=b1.detach(), act="silu")
+                xn = st["h1"] if x is st["h0"] else st["h0"]
+                ops.sampler_linear(st["a"], compute_weight(w2), xn, bias=b2.detach(), gate=m[:, 2 * W:3 * W],
+                                   residual=x)
+                x = xn
+            fm = mod[:, 3 * W * len(blocks):]
+            ops.sampler_linear(x, compute_weight(fl[2]), st["out"], bias=fl[3].detach(), ln=True,
+                               shift=fm[:, :W], scale=fm[:, W:2 * W])
+        else:
+            self._step_unfused(x, mod, st)
+        coef = list(self.sched.steps[k][2]) + [st["temperature"]]
+        ops.p_sample_step(st["out"], st["x"], st["noise"][k], coef, st["x"], st["x_net"])
+
+    def _step_unfused(self, x, mod, st):
+        """general-route step body (fp32 parity mode, or widths over the fused kernel's K limit)."""
+        W = self.net.model_channels
+        blocks, fl, ncol = st["blocks"], st["fl"], mod.shape[1]
         for i, (modw, modb, w1, b1, w2, b2, lnw, lnb) in enumerate(blocks):
             m = mod[:, 3 * W * i:3 * W * (i + 1)]
             ops.layernorm_fwd(x, lnw.detach(), lnb.detach(), st["h"], st["mean"], st["rstd"],
@@ -107,14 +140,12 @@ class ActionSampler:
         ops.layernorm_fwd(x, None, None, st["h"], st["mean"], st["rstd"], scale=fm[:, W:2 * W], shift=fm[:, :W],
                           ldm=ncol)
         ops.linear(st["h"], compute_weight(fl[2]), st["out"], bias=fl[3].detach())
-        coef = list(self.sched.steps[k][2]) + [st["temperature"]]
-        ops.p_sample_step(st["out"], st["x"], st["noise"][k], coef, st["x"], st["x_net"])
 
     def _state(self, R, C, dev, temperature):
         """Persistent step buffers (+ captured graph) per (rows, channels, dtype, weights)."""
         net = self.net
         cd = cdt()
-        sig = (R, C, str(cd), float(temperature), str(dev),
+        sig = (R, C, str(cd), float(temperature), str(dev), self.use_fused,
                tuple((p.data_ptr(), p._version) for p in net.parameters()))
         cache = getattr(self, "_cache", None)
         if cache is not None and cache["sig"] == sig:
@@ -133,7 +164,8 @@ class ActionSampler:
                   h0=torch.empty(R, W, dtype=F32, device=dev), h1=torch.empty(R, W, dtype=F32, device=dev),
                   h=torch.empty(R, W, dtype=cd, device=dev), a=torch.empty(R, W, dtype=cd, device=dev),
                   mean=torch.empty(R, dtype=F32, device=dev), rstd=torch.empty(R, dtype=F32, device=dev),
-                  out=torch.empty(R, 2 * C, dtype=F32, device=dev), graph=None)
+                  out=torch.empty(R, 2 * C, dtype=F32, device=dev), graph=None,
+                  fused=self.use_fused and cd == torch.bfloat16 and W in (256, 512, 1024))
         self._cache = st
         return st
 

@@ -275,6 +275,30 @@ def p_sample_step(out, x, noise, coef, x_new, x_net=None):
                ptr(x_net), rows, C, stream())
 
 
+def sampler_linear(A, W, out, bias=None, act="none", ln=False, lnw=None, lnb=None, shift=None, scale=None,
+                   eps=1e-6, gate=None, residual=None):
+    """Few-row fused linear (uva_sampler_linear): out = epi(A' @ W^T + bias), A' = A (bf16) or the
+    adaLN-modulated LayerNorm of fp32 rows A (ln=True)."""
+    R, K = A.shape
+    N = W.shape[0]
+    if W.shape[1] != K or W.dtype != torch.bfloat16 or W.stride(1) != 1 or W.stride(0) != K:
+        raise ValueError(f"sampler_linear: W {tuple(W.shape)} must be contiguous bf16 [N, {K}]")
+    if out.shape != (R, N) or out.stride(1) != 1:
+        raise ValueError(f"sampler_linear: out {tuple(out.shape)} != {(R, N)}")
+    if A.stride(1) != 1 or A.dtype != (torch.float32 if ln else torch.bfloat16):
+        raise ValueError("sampler_linear: A must be row-major fp32 (ln) or bf16")
+    ldm = 0
+    if ln:
+        if shift is None or scale is None or shift.stride(0) != scale.stride(0) or shift.dtype != torch.bfloat16:
+            raise ValueError("sampler_linear: ln needs bf16 shift/scale views with one row stride")
+        ldm = shift.stride(0)
+    ldg = gate.stride(0) if gate is not None else 0
+    ldr = residual.stride(0) if residual is not None else 0
+    lib().call("uva_sampler_linear", int(ln), ptr(A), A.stride(0), ptr(lnw), ptr(lnb), ptr(shift), ptr(scale), ldm,
+               float(eps), ptr(W), ptr(bias), ACT[act], ptr(gate), ldg, ptr(residual), ldr, dt(out), ptr(out),
+               out.stride(0), R, N, K, stream())
+
+
 def weighted_mean(l, w, res):
     lib().call("uva_weighted_mean", ptr(l), ptr(w), l.numel(), ptr(res), stream())
 
