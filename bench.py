@@ -40,7 +40,7 @@ def parse():
     ap.add_argument("--no-trace", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--trace-out", default="", help="write every traced kernel row (tag, launches, avg ms) here")
-    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r01.json"))
+    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r01f.json"))
     return ap.parse_args()
 
 

@@ -228,6 +228,9 @@ int uva_groupnorm_finalize_tiles(const float* part, int Nimg, int HW, int C, int
 /* y = [SiLU](x*scale + shift) over NHWC bf16 (GroupNorm apply, once per element) */
 int uva_groupnorm_apply(const void* x, const float* scale, const float* shift, void* y, int Nimg, int HW, int C,
                         int do_silu, hipStream_t stream);
+/* y [n, 2H, 2W, C] = nearest x2 upsample of NHWC x [n, H, W, C] (decoder Upsample,
+ * vaekl.py:20-33); C * sizeof(dtype) % 16 == 0. */
+int uva_upsample_nearest2x(int dtype, const void* x, void* y, int n, int H, int W, int C, hipStream_t stream);
 int uva_posterior_sample(int mdt, const void* moments, const float* eps, float* z, int Nimg, float scale,
                          hipStream_t stream);
 

@@ -566,6 +566,65 @@ class Encoder(nn.Module):
         return self.conv_out(F.silu(self.norm_out(h)))
 
 
+class _Up(nn.Module):
+    """Upsample (vaekl.py:20-33): nearest x2 then conv3x3."""
+
+    def __init__(self, c):
+        super().__init__()
+        self.conv = nn.Conv2d(c, c, 3, padding=1)
+
+    def forward(self, x):
+        return self.conv(F.interpolate(x, scale_factor=2.0, mode="nearest"))
+
+
+class Decoder(nn.Module):
+    """vaekl.py:276-397 with attn_resolutions=() (AutoencoderKL's construction)."""
+
+    def __init__(self, ch=128, out_ch=3, ch_mult=(1, 1, 2, 2, 4), num_res_blocks=2, z_channels=16):
+        super().__init__()
+        block_in = ch * ch_mult[-1]
+        self.conv_in = nn.Conv2d(z_channels, block_in, 3, padding=1)
+        self.mid = nn.Module()
+        self.mid.block_1 = _ResnetBlock(block_in, block_in)
+        self.mid.attn_1 = _AttnBlock(block_in)
+        self.mid.block_2 = _ResnetBlock(block_in, block_in)
+        ups = []
+        for lvl in reversed(range(len(ch_mult))):
+            u = nn.Module()
+            u.block = nn.ModuleList()
+            for _ in range(num_res_blocks + 1):
+                u.block.append(_ResnetBlock(block_in, ch * ch_mult[lvl]))
+                block_in = ch * ch_mult[lvl]
+            if lvl != 0:
+                u.upsample = _Up(block_in)
+            ups.insert(0, u)
+        self.up = nn.ModuleList(ups)
+        self.norm_out = _gn(block_in)
+        self.conv_out = nn.Conv2d(block_in, out_ch, 3, padding=1)
+
+    def forward(self, z):
+        h = self.conv_in(z)
+        h = self.mid.block_2(self.mid.attn_1(self.mid.block_1(h)))
+        for lvl in reversed(range(len(self.up))):
+            for blk in self.up[lvl].block:
+                h = blk(h)
+            if hasattr(self.up[lvl], "upsample"):
+                h = self.up[lvl].upsample(h)
+        return self.conv_out(F.silu(self.norm_out(h)))
+
+
+class AutoencoderKLDecoder(nn.Module):
+    """AutoencoderKL.decode (vaekl.py:56-58): post_quant_conv -> Decoder."""
+
+    def __init__(self, embed_dim=16, ch_mult=(1, 1, 2, 2, 4)):
+        super().__init__()
+        self.decoder = Decoder(ch_mult=ch_mult, z_channels=embed_dim)
+        self.post_quant_conv = nn.Conv2d(embed_dim, embed_dim, 1)
+
+    def decode(self, z):
+        return self.decoder(self.post_quant_conv(z))
+
+
 class AutoencoderKLEncoder(nn.Module):
     """Encoder half of AutoencoderKL (vaekl.py:449-493); the decoder is out of scope."""
 

@@ -242,6 +242,22 @@ def gen_vae():
     print("vae done")
 
 
+def gen_vae_decode():
+    """AutoencoderKL.decode of the reference (vaekl.py:56-58, Decoder :276-397) on hash weights."""
+    class DD:
+        vae_embed_dim = 16
+        ch_mult = (1, 1, 2, 2, 4)
+
+    ae = vaekl.AutoencoderKL(autoencoder_path=None, ddconfig=DD())
+    hash_init_(ae, "vae.")
+    z = torch.from_numpy(hash_normal("vae/dec_z", (1, 16, 16, 16)))
+    with torch.no_grad():
+        img = ae.decode(z)
+    np.savez(os.path.join(OUT, "g3_vae_decode.npz"), sub=img[:, :, ::8, ::8].numpy(),
+             checksum=checksum(img), shape=np.array(img.shape))
+    print("vae decode", tuple(img.shape), checksum(img))
+
+
 def gen_resize():
     import torch.nn.functional as F
     d = {}
@@ -418,6 +434,6 @@ def gen_predict():
 
 if __name__ == "__main__":
     which = sys.argv[1:] or ["indexing", "mar", "block", "mlp", "diffusion_math", "vae",
-                             "resize", "ema", "policy", "sample", "predict"]
+                             "resize", "ema", "policy", "sample", "predict", "vae_decode"]
     for w in which:
         globals()[f"gen_{w}"]()

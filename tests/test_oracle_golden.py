@@ -204,3 +204,15 @@ def test_predict_action_end_to_end_oracle():
     action, pred = pol.predict_action(torch.from_numpy(b["image"]), cases.predict_rng(), cases.SAMPLE_TEMPERATURE)
     np.testing.assert_allclose(pred.double().numpy(), g["action_pred"], rtol=0, atol=2e-3)
     np.testing.assert_allclose(action.double().numpy(), g["action"], rtol=0, atol=2e-3)
+
+
+def test_vae_decode_oracle():
+    """AutoencoderKL.decode (vaekl.py:56-58, Decoder :276-397) restatement vs the reference."""
+    g = replay.load("g3_vae_decode.npz")
+    dec = O.AutoencoderKLDecoder()
+    hash_init_(dec, "vae.")
+    z = torch.from_numpy(hash_normal("vae/dec_z", (1, 16, 16, 16)))
+    with torch.no_grad():
+        img = dec.decode(z)
+    np.testing.assert_allclose(img[:, :, ::8, ::8].numpy(), g["sub"], rtol=0, atol=1e-4)
+    np.testing.assert_allclose(replay.checksum(img), g["checksum"], rtol=1e-5)

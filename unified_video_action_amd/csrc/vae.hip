@@ -247,3 +247,37 @@ extern "C" int uva_groupnorm_apply(const void* x, const float* scale, const floa
   UVA_LAUNCH_CHECK();
   return 0;
 }
+
+// Nearest x2 upsampling of NHWC maps (Upsample, vae/vaekl.py:20-33: F.interpolate(scale_factor=2,
+// mode="nearest")): one 16-byte channel chunk per thread, read once, written to the 4 children.
+__global__ void upsample2x_kernel(const uint4* __restrict__ x, uint4* __restrict__ y, int n, int H, int W, int chunks) {
+  const long long total = (long long)n * H * W * chunks;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += (long long)gridDim.x * blockDim.x) {
+    const int c = (int)(i % chunks);
+    long long p = i / chunks;
+    const int w = (int)(p % W);
+    p /= W;
+    const int h = (int)(p % H);
+    const long long img = p / H;
+    const uint4 v = x[i];
+    const long long W2 = 2LL * W;
+    const long long base = ((img * 2 * H + 2 * h) * W2 + 2 * w) * chunks + c;
+    y[base] = v;
+    y[base + chunks] = v;
+    y[base + W2 * chunks] = v;
+    y[base + W2 * chunks + chunks] = v;
+  }
+}
+
+extern "C" int uva_upsample_nearest2x(int dtype, const void* x, void* y, int n, int H, int W, int C, hipStream_t s) {
+  const int esz = dtype == UVA_DT_BF16 ? 2 : 4;
+  if (n <= 0 || H <= 0 || W <= 0 || (C * esz) % 16) return (int)hipErrorInvalidValue;
+  const int chunks = C * esz / 16;
+  const long long total = (long long)n * H * W * chunks;
+  long long blocks = (total + 255) / 256;
+  if (blocks > 16384) blocks = 16384;
+  upsample2x_kernel<<<dim3((unsigned)blocks), 256, 0, s>>>((const uint4*)x, (uint4*)y, n, H, W, chunks);
+  UVA_LAUNCH_CHECK();
+  return 0;
+}

@@ -403,3 +403,11 @@ def resize_select(img, sel, out, Cpad):
 
 def posterior_sample(moments, eps, z, Nimg, scale=0.2325):
     lib().call("uva_posterior_sample", dt(moments), ptr(moments), ptr(eps), ptr(z), Nimg, float(scale), stream())
+
+
+def upsample_nearest2x(x, y):
+    """NHWC nearest x2 (uva_upsample_nearest2x)."""
+    n, H, W, C = x.shape
+    if not (x.is_contiguous() and y.is_contiguous() and y.shape == (n, 2 * H, 2 * W, C) and y.dtype == x.dtype):
+        raise ValueError(f"upsample_nearest2x: {tuple(x.shape)} -> {tuple(y.shape)}")
+    lib().call("uva_upsample_nearest2x", dt(x), ptr(x), ptr(y), n, H, W, C, stream())

@@ -3,8 +3,11 @@
 Parameters keep the reference module tree (encoder.conv_in, encoder.down.{i}.block.{j}.
 {norm1,conv1,norm2,conv2,nin_shortcut}, encoder.down.{i}.attn.{j}.{norm,q,k,v,proj_out},
 encoder.down.{i}.downsample.conv, encoder.mid.*, encoder.norm_out, encoder.conv_out,
-quant_conv) so reference checkpoints (kl16.ckpt "model" dict) load unchanged.  The decoder
-is used only by the epoch-end FVD eval and is out of scope.
+quant_conv, post_quant_conv, decoder.conv_in, decoder.mid.*, decoder.up.{i}.block.{j},
+decoder.up.{i}.upsample.conv, decoder.norm_out, decoder.conv_out) so reference checkpoints
+(kl16.ckpt "model" dict) load unchanged.  decode() (vaekl.py:56-58, Decoder :276-397; the
+consumer of generated latents: video sampling and the FVD eval) reuses the encoder's
+resblock / attention / conv pieces plus a nearest-x2 upsample kernel.
 
 Forward runs entirely in NHWC on libuva_hip.so:
   * every conv = implicit-GEMM MFMA kernel with the residual add in its epilogue; the
@@ -59,6 +62,41 @@ class Downsample(nn.Module):
         self.conv = nn.Conv2d(c, c, 3, 2, 0)
 
 
+class Upsample(nn.Module):
+    def __init__(self, c):
+        super().__init__()
+        self.conv = nn.Conv2d(c, c, 3, 1, 1)
+
+
+class Decoder(nn.Module):
+    """vaekl.py:276-397 (attn_resolutions=(), as AutoencoderKL builds it)."""
+
+    def __init__(self, ch=128, out_ch=3, ch_mult=(1, 1, 2, 2, 4), num_res_blocks=2, resolution=256, z_channels=16,
+                 **ignore):
+        super().__init__()
+        self.num_resolutions = len(ch_mult)
+        self.num_res_blocks = num_res_blocks
+        block_in = ch * ch_mult[-1]
+        self.conv_in = nn.Conv2d(z_channels, block_in, 3, 1, 1)
+        self.mid = nn.Module()
+        self.mid.block_1 = ResnetBlock(block_in, block_in)
+        self.mid.attn_1 = AttnBlock(block_in)
+        self.mid.block_2 = ResnetBlock(block_in, block_in)
+        ups = []
+        for lvl in reversed(range(self.num_resolutions)):
+            u = nn.Module()
+            u.block, u.attn = nn.ModuleList(), nn.ModuleList()
+            for _ in range(num_res_blocks + 1):
+                u.block.append(ResnetBlock(block_in, ch * ch_mult[lvl]))
+                block_in = ch * ch_mult[lvl]
+            if lvl != 0:
+                u.upsample = Upsample(block_in)
+            ups.insert(0, u)
+        self.up = nn.ModuleList(ups)
+        self.norm_out = _gn(block_in)
+        self.conv_out = nn.Conv2d(block_in, out_ch, 3, 1, 1)
+
+
 class Encoder(nn.Module):
     def __init__(self, ch=128, ch_mult=(1, 1, 2, 2, 4), num_res_blocks=2, attn_resolutions=(16,), in_channels=3,
                  resolution=256, z_channels=16, double_z=True, **ignore):
@@ -99,10 +137,14 @@ class _Prepared:
         for name, m in vae.named_modules():
             if isinstance(m, nn.Conv2d):
                 w = m.weight.detach().to(device)
+                b = m.bias.detach().to(device, F32)
                 if name.endswith("conv_in") and w.shape[1] < cin_pad:
                     w = torch.nn.functional.pad(w, (0, 0, 0, 0, 0, cin_pad - w.shape[1]))
+                if w.shape[0] < cin_pad:  # decoder.conv_out: 3 output channels padded to 8 (sliced after)
+                    w = torch.nn.functional.pad(w, (0, 0, 0, 0, 0, 0, 0, cin_pad - w.shape[0]))
+                    b = torch.nn.functional.pad(b, (0, cin_pad - b.shape[0]))
                 self.w[name] = w.permute(0, 2, 3, 1).contiguous().to(dtype)
-                self.b[name] = m.bias.detach().to(device, F32).contiguous()
+                self.b[name] = b.contiguous()
         for name, m in vae.named_modules():
             if isinstance(m, AttnBlock):
                 self.w[name + ".qkv"] = torch.cat([self.w[name + ".q"], self.w[name + ".k"], self.w[name + ".v"]])
@@ -120,6 +162,8 @@ class AutoencoderKL(nn.Module):
         self.encoder = Encoder(ch_mult=ch_mult, z_channels=embed_dim)
         self.use_variational = use_variational
         self.quant_conv = nn.Conv2d(2 * embed_dim, (2 if use_variational else 1) * embed_dim, 1)
+        self.decoder = Decoder(ch_mult=ch_mult, z_channels=embed_dim)
+        self.post_quant_conv = nn.Conv2d(embed_dim, embed_dim, 1)
         self.embed_dim = embed_dim
         self._prep = None
         if autoencoder_path is not None and os.path.exists(autoencoder_path):
@@ -258,3 +302,33 @@ class AutoencoderKL(nn.Module):
         z = torch.empty(n, 256, self.embed_dim, dtype=F32, device=x.device)
         ops.posterior_sample(mom, eps.contiguous().float(), z, n, scale)
         return z
+
+    @torch.no_grad()
+    def decode_nhwc(self, z):
+        """z NHWC [n, 16, 16, embed] (compute dtype) -> images NHWC [n, 256, 256, CIN_PAD] (3 used)."""
+        P = self._prepared(z.device)
+        d = self.decoder
+        n, H, W, _ = z.shape
+        h = self._conv(P, "post_quant_conv", z, n, H, W)[0]
+        h, H, W, hs = self._conv(P, "decoder.conv_in", h, n, H, W, stats=True)
+        h, hs = self._resblock(P, "decoder.mid.block_1", d.mid.block_1, h, hs, n, H, W)
+        h, hs = self._attn(P, "decoder.mid.attn_1", d.mid.attn_1, h, hs, n, H, W)
+        h, hs = self._resblock(P, "decoder.mid.block_2", d.mid.block_2, h, hs, n, H, W)
+        for lvl in reversed(range(d.num_resolutions)):
+            u = d.up[lvl]
+            for j, blk in enumerate(u.block):
+                h, hs = self._resblock(P, f"decoder.up.{lvl}.block.{j}", blk, h, hs, n, H, W)
+            if hasattr(u, "upsample"):
+                hu = torch.empty(n, 2 * H, 2 * W, h.shape[-1], dtype=h.dtype, device=h.device)
+                ops.upsample_nearest2x(h, hu)
+                H, W = 2 * H, 2 * W
+                h, _, _, hs = self._conv(P, f"decoder.up.{lvl}.upsample.conv", hu, n, H, W, stats=True)
+        a, g = self._norm_act(h, hs, d.norm_out, n, H * W, h.shape[-1])
+        return self._conv(P, "decoder.conv_out", a, n, H, W, gn=g)[0]
+
+    @torch.no_grad()
+    def decode(self, z):
+        """AutoencoderKL.decode (vaekl.py:56-58): z NCHW [n, embed, 16, 16] -> images NCHW fp32 [n, 3, 256, 256]."""
+        zz = z.permute(0, 2, 3, 1).contiguous().to(cdt())
+        out = self.decode_nhwc(zz)
+        return out[..., :3].permute(0, 3, 1, 2).float().contiguous()
