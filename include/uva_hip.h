@@ -173,9 +173,11 @@ int uva_loss_grad(const float* dl, const float* w, const float* wsum, const floa
  * out: net output [rows, ld_out] (eps | var_values, 2C columns), x/noise/x_new: fp32 [rows, C]
  * (x_new may alias x), coef: HOST array of 8 floats {sqrt_recip_ac, sqrt_recipm1_ac, coef1,
  * coef2, min_log (posterior_log_variance_clipped), max_log (log beta), nonzero (t != 0),
- * temperature} of the step's spaced timestep; x_net (nullable): x_new in dtype xdt. */
+ * temperature} of the step's spaced timestep; x_net (nullable): x_new in dtype xdt; clip: clip_denoised
+ * (1 for the action head, diffusion_action_loss.py:218; 0 for the video head, diffusion_loss.py:84). */
 int uva_p_sample_step(int odt, const void* out, long long ld_out, const float* x, const float* noise,
-                      const float* coef, float* x_new, int xdt, void* x_net, int rows, int C, hipStream_t stream);
+                      const float* coef, float* x_new, int xdt, void* x_net, int clip, int rows, int C,
+                      hipStream_t stream);
 
 /* ---- few-row fused linear of the action sampler (inference, bf16; diffusion_loss.py:142-189)
  * out[R,N] = epi(A' W^T + bias), W bf16 [N,K] (K in {256, 512, 1024}), R any.

@@ -79,7 +79,7 @@ def space_timesteps(num_timesteps, section_counts):
     return steps
 
 
-def p_sample_loop(tb, model_fn, noise, step_noise, temperature=1.0):
+def p_sample_loop(tb, model_fn, noise, step_noise, temperature=1.0, clip=True):
     """gaussian_diffusion.py:260-346 (p_mean_variance, learned-range variance, eps model,
     clip_denoised) + :395-492 (p_sample / p_sample_loop_progressive); the wrapped model gets
     the base timestep (respace.py:118-130).  step_noise[k] is the k-th randn_like draw."""
@@ -91,7 +91,9 @@ def p_sample_loop(tb, model_fn, noise, step_noise, temperature=1.0):
         eps, v = out[:, :C], out[:, C:]
         frac = (v + 1) / 2
         log_var = frac * tb.gather("log_betas", t) + (1 - frac) * tb.gather("plvc", t)
-        x0 = (tb.gather("sqrt_recip_ac", t) * x - tb.gather("sqrt_recipm1_ac", t) * eps).clamp(-1, 1)
+        x0 = tb.gather("sqrt_recip_ac", t) * x - tb.gather("sqrt_recipm1_ac", t) * eps
+        if clip:
+            x0 = x0.clamp(-1, 1)
         mean = tb.gather("coef1", t) * x0 + tb.gather("coef2", t) * x
         nonzero = (t != 0).float()[:, None]
         x = mean + nonzero * torch.exp(0.5 * log_var) * step_noise[k] * temperature
@@ -266,6 +268,11 @@ class DiffLoss(nn.Module):
         loss, _, _ = diffusion_training_loss(self.tables, lambda xt, tt: self.net(xt, tt, c),
                                              tgt, t, noise)
         return (loss * m).sum() / m.sum()
+
+    def sample(self, z, noise, step_noise, temperature=1.0, respacing="100"):
+        """diffusion_loss.py:68-90 with cfg = 1.0, clip_denoised=False -> [R, C]."""
+        tb = DiffusionTables(1000, space_timesteps(1000, respacing))
+        return p_sample_loop(tb, lambda xt, tt: self.net(xt, tt, z), noise, step_noise, temperature, clip=False)
 
 
 class DiffActLoss(nn.Module):
@@ -445,6 +452,41 @@ class MAR(nn.Module):
         text = self.text_proj_cond(text_latents) if self.clip else None
         h = self.encode(x, cond, mask, None, text, mode, prop, torch.ones(B))
         return self.diffactloss.sample(self.decode(h), noise, step_noise, temperature)
+
+    @torch.no_grad()
+    def sample_video(self, c, text_latents, mode, num_iter, rng, temperature=1.0, nactions=None, prop=None):
+        """sample_tokens video modes (mar_con_unified.py:1000-1151): MaskGIT loop with the cosine
+        schedule over the generation orders (mask_by_order :17-25), action head sampled every
+        iteration, video head on the tokens predicted in that iteration."""
+        B = c.shape[0]
+        cond = self.patchify(c.reshape(B * 4, *c.shape[2:])).reshape(B, 4, 256, -1)
+        tokens = torch.zeros_like(cond)
+        text = self.text_proj_cond(text_latents) if self.clip else None
+        orders = torch.as_tensor(rng["orders"])
+        mask = torch.ones(B, 4, 256)
+        act = None
+        for step in range(num_iter):
+            h = self.encode(tokens, cond, mask.reshape(B, -1), nactions, text, mode, prop, torch.ones(B))
+            z = self.decode(h)
+            if hasattr(self, "diffactloss"):
+                act = self.diffactloss.sample(z, torch.as_tensor(rng["act_noise"][step]),
+                                              torch.as_tensor(rng["act_step_noise"][step]), temperature)
+            ratio = np.cos(math.pi / 2.0 * (step + 1) / num_iter)
+            mask_len = torch.Tensor([np.floor(256 * ratio)])
+            mask_len = torch.maximum(torch.Tensor([1]), torch.minimum(mask[:, 0].sum(-1, keepdim=True) - 1, mask_len))
+            nxt = torch.zeros(B, 256).scatter(-1, orders[:, :int(mask_len[0].item())], torch.ones(B, 256)).bool()
+            nxt = nxt[:, None, :].expand(-1, 4, -1).reshape(B, -1)
+            cur = mask.reshape(B, -1).bool()
+            to_pred = cur if step >= num_iter - 1 else torch.logical_xor(cur, nxt)
+            mask = nxt.reshape(B, 4, 256).float()
+            idx = to_pred.nonzero(as_tuple=True)
+            lat = self.diffloss.sample(z[idx], torch.as_tensor(rng["video_noise"][step]),
+                                       torch.as_tensor(rng["video_step_noise"][step]), temperature)
+            flat = tokens.reshape(B, 1024, -1).clone()
+            flat[idx] = lat
+            tokens = flat.reshape(B, 4, 256, -1)
+        out = tokens.reshape(B * 4, 16, 16, -1).permute(0, 3, 1, 2)
+        return out, act
 
     def forward(self, z, c, nactions, text_latents, mode, rng, prop=None):
         """Training forward -> (loss, video_loss, act_loss) with injected draws `rng`."""

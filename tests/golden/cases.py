@@ -178,3 +178,28 @@ POLICY_AMP_KEYS = ("img_size", "vae_stride", "patch_size", "vae_embed_dim", "mas
                    "attn_dropout", "proj_dropout", "diffloss_d", "diffloss_w", "diffloss_act_d", "diffloss_act_w",
                    "num_sampling_steps", "diffusion_batch_mul", "grad_checkpointing", "predict_video",
                    "act_diff_training_steps", "act_diff_testing_steps")
+
+
+VIDEO_SAMPLE_ITERS = 2
+
+
+def video_sample_rng(variant, num_iter=VIDEO_SAMPLE_ITERS, B=B_MAR):
+    """Draws of sample_tokens(video_model) over num_iter MaskGIT iterations: per iteration the
+    action head (x_T, 100 steps) then the video head on the tokens predicted in that iteration
+    (mar_con_unified.py:1026-1100; counts follow the cosine schedule, mask_by_order)."""
+    import math
+    v = VARIANTS[variant]
+    tag = f"vsample/{variant}"
+    r = {"orders": sample_rng(variant, B)["orders"], "act_noise": [], "act_step_noise": [],
+         "video_noise": [], "video_step_noise": []}
+    cur = 256
+    for step in range(num_iter):
+        ml = max(1.0, min(cur - 1.0, float(np.floor(256 * np.cos(math.pi / 2.0 * (step + 1) / num_iter)))))
+        pred = cur if step >= num_iter - 1 else cur - int(ml)
+        cur = int(ml)
+        rows = B * 4 * pred
+        r["act_noise"].append(hash_normal(f"{tag}/{step}/axT", (B * 16, v["Da"])))
+        r["act_step_noise"].append(hash_normal(f"{tag}/{step}/asteps", (SAMPLE_STEPS, B * 16, v["Da"])))
+        r["video_noise"].append(hash_normal(f"{tag}/{step}/vxT", (rows, 16)))
+        r["video_step_noise"].append(hash_normal(f"{tag}/{step}/vsteps", (SAMPLE_STEPS, rows, 16)))
+    return r

@@ -386,6 +386,48 @@ def gen_sample():
     np.savez(os.path.join(OUT, "g5_sample.npz"), **out)
 
 
+def gen_video_sample():
+    """sample_tokens(task_mode="video_model") of the reference (MaskGIT loop, mar_con_unified.py:
+    1000-1151), eval mode, VIDEO_SAMPLE_ITERS iterations, draws injected (cases.video_sample_rng)."""
+    out = {}
+    for variant in ("pusht", "libero"):
+        m = build_mar(variant)
+        m.eval()
+        inp = {k: torch.from_numpy(x) for k, x in cases.mar_inputs(variant).items()}
+        rng = cases.video_sample_rng(variant)
+        q_randn, q_like = [], []
+        for i in range(cases.VIDEO_SAMPLE_ITERS):
+            q_randn += [torch.from_numpy(rng["act_noise"][i]), torch.from_numpy(rng["video_noise"][i])]
+            q_like += [torch.from_numpy(a) for a in rng["act_step_noise"][i]]
+            q_like += [torch.from_numpy(a) for a in rng["video_step_noise"][i]]
+        saved = (torch.randn, torch.randn_like, torch.Tensor.cuda, ref_mar.MAR.sample_orders)
+
+        def fake_randn(*shape, **k):
+            v = q_randn.pop(0)
+            assert tuple(shape) == tuple(v.shape), (shape, v.shape)
+            return v
+
+        def fake_randn_like(x, *a, **k):
+            v = q_like.pop(0)
+            assert v.shape == x.shape, (v.shape, x.shape)
+            return v.to(x.dtype)
+
+        torch.randn, torch.randn_like = fake_randn, fake_randn_like
+        torch.Tensor.cuda = lambda self, *a, **k: self
+        ref_mar.MAR.sample_orders = lambda self, bsz: torch.from_numpy(rng["orders"])
+        try:
+            tok, act = m.sample_tokens(bsz=cases.B_MAR, cond=inp["c"], text_latents=inp.get("text_latents"),
+                                       num_iter=cases.VIDEO_SAMPLE_ITERS, cfg=1.0,
+                                       temperature=cases.SAMPLE_TEMPERATURE, task_mode="video_model")
+        finally:
+            torch.randn, torch.randn_like, torch.Tensor.cuda, ref_mar.MAR.sample_orders = saved
+        assert not q_randn and not q_like, "unconsumed draws"
+        out[f"{variant}_tokens"] = tok.detach().float().numpy()
+        out[f"{variant}_act"] = act.detach().float().numpy()
+        print(f"video sample {variant}: tokens {tuple(tok.shape)} sum={tok.sum().item():.5f}")
+    np.savez(os.path.join(OUT, "g5_video_sample.npz"), **out)
+
+
 def gen_predict():
     """UnifiedVideoActionPolicy.predict_action (policy:221-320) of the reference, eval mode, on the
     golden PushT policy (full KL-VAE, reduced MAR), draws injected (cases.predict_rng)."""
@@ -434,6 +476,6 @@ def gen_predict():
 
 if __name__ == "__main__":
     which = sys.argv[1:] or ["indexing", "mar", "block", "mlp", "diffusion_math", "vae",
-                             "resize", "ema", "policy", "sample", "predict", "vae_decode"]
+                             "resize", "ema", "policy", "sample", "predict", "vae_decode", "video_sample"]
     for w in which:
         globals()[f"gen_{w}"]()

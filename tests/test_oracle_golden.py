@@ -216,3 +216,20 @@ def test_vae_decode_oracle():
         img = dec.decode(z)
     np.testing.assert_allclose(img[:, :, ::8, ::8].numpy(), g["sub"], rtol=0, atol=1e-4)
     np.testing.assert_allclose(replay.checksum(img), g["checksum"], rtol=1e-5)
+
+
+@pytest.mark.parametrize("variant", ["pusht", "libero"])
+def test_sample_tokens_video_oracle(variant):
+    """sample_tokens(video_model): MaskGIT loop (mask schedule, order-based masking, token gather /
+    scatter) + video diffusion head without clipping, vs the reference (mar_con_unified.py:1000-1151)."""
+    g = replay.load("g5_video_sample.npz")
+    mar = O.MAR(**replay.mar_ctor_kwargs(variant))
+    hash_init_(mar, "mar.")
+    mar.eval()
+    inp = {k: torch.from_numpy(x) for k, x in cases.mar_inputs(variant).items()}
+    rng = cases.video_sample_rng(variant)
+    tok, act = mar.sample_video(inp["c"], inp.get("text_latents"), "video_model", cases.VIDEO_SAMPLE_ITERS, rng,
+                                cases.SAMPLE_TEMPERATURE)
+    ref = g[f"{variant}_tokens"]
+    np.testing.assert_allclose(tok.numpy(), ref, rtol=1e-4, atol=1e-4 * np.abs(ref).max())
+    np.testing.assert_allclose(act.numpy(), g[f"{variant}_act"], rtol=0, atol=1e-5)

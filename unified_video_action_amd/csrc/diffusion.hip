@@ -167,7 +167,7 @@ __global__ void loss_grad_kernel(const float* __restrict__ dl, const float* __re
 // One reverse step of GaussianDiffusion.p_sample for the learned-range eps model
 // (gaussian_diffusion.py:260-346 p_mean_variance, :395-440 p_sample):
 //   log_var = f*max_log + (1-f)*min_log,  f = (v+1)/2
-//   x0      = clamp(sqrt_recip_ac*x - sqrt_recipm1_ac*eps, -1, 1)
+//   x0      = sqrt_recip_ac*x - sqrt_recipm1_ac*eps   [clamped to [-1, 1] when clip_denoised]
 //   mean    = coef1*x0 + coef2*x
 //   x_new   = mean + nonzero*exp(log_var/2)*noise*temperature
 // Every row shares the step's timestep, so the eight schedule coefficients (float64 tables cast
@@ -179,7 +179,7 @@ struct PStepCoef {
 
 __global__ void p_sample_step_kernel(const void* __restrict__ out, int odt, long long ld_out, const float* x,
                                      const float* __restrict__ noise, PStepCoef k, float* x_new, void* x_net,
-                                     int xdt, int rows, int C) {
+                                     int xdt, int clip, int rows, int C) {
   long long n = (long long)rows * C;
   for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
     long long r = i / C;
@@ -190,7 +190,7 @@ __global__ void p_sample_step_kernel(const void* __restrict__ out, int odt, long
     float f = (v + 1.0f) / 2.0f;
     float log_var = f * k.max_log + (1.0f - f) * k.min_log;
     float x0 = k.sqrt_recip_ac * xi - k.sqrt_recipm1_ac * eps;
-    x0 = fminf(fmaxf(x0, -1.0f), 1.0f);
+    if (clip) x0 = fminf(fmaxf(x0, -1.0f), 1.0f);
     float mean = k.coef1 * x0 + k.coef2 * xi;
     float xn = mean + k.nonzero * expf(0.5f * log_var) * noise[i] * k.temperature;
     x_new[i] = xn;
@@ -242,12 +242,12 @@ extern "C" int uva_loss_grad(const float* dl, const float* w, const float* wsum,
 }
 
 extern "C" int uva_p_sample_step(int odt, const void* out, long long ld_out, const float* x, const float* noise,
-                                 const float* coef, float* x_new, int xdt, void* x_net, int rows, int C,
+                                 const float* coef, float* x_new, int xdt, void* x_net, int clip, int rows, int C,
                                  hipStream_t s) {
   if (rows <= 0 || C <= 0 || ld_out < 2 * C) return (int)hipErrorInvalidValue;
   PStepCoef k{coef[0], coef[1], coef[2], coef[3], coef[4], coef[5], coef[6], coef[7]};
   p_sample_step_kernel<<<grid_for((long long)rows * C), 256, 0, s>>>(out, odt, ld_out, x, noise, k, x_new, x_net,
-                                                                      xdt, rows, C);
+                                                                      xdt, clip, rows, C);
   UVA_LAUNCH_CHECK();
   return 0;
 }

@@ -163,6 +163,28 @@ class DiffLoss(nn.Module):
         self.n_frames = kwargs.get("n_frames", 4)
         self.net = SimpleMLPAdaLN(target_channels, width, target_channels * 2, z_channels, depth, grad_checkpointing)
         self.num_timesteps = 1000
+        self.num_sampling_steps = str(num_sampling_steps)
+        self._sampler = None
+
+    @torch.no_grad()
+    def sample(self, z, temperature=1.0, cfg=1.0, text_latents=None, noise=None, step_noise=None):
+        """z [R, D] decoder rows of the tokens to predict -> token latents [R, C]
+        (diffusion_loss.py:68-90: p_sample_loop over create_diffusion(num_sampling_steps), no clipping).
+        noise [R, C] / step_noise [S, R, C] may be injected."""
+        if cfg != 1.0:
+            raise NotImplementedError("classifier-free guidance (forward_with_cfg) is not on the built path")
+        from .sampler import ActionSampler
+        if self._sampler is None:
+            self._sampler = ActionSampler(self.net, self.num_sampling_steps, clip_denoised=False)
+        R = z.shape[0]
+        S = self._sampler.sched.S
+        dev = z.device
+        if noise is None:
+            noise = torch.randn(R, self.in_channels, device=dev)
+        if step_noise is None:
+            step_noise = torch.randn(S, R, self.in_channels, device=dev)
+        return self._sampler(z.float().contiguous(), noise.to(dev, torch.float32),
+                             step_noise.to(dev, torch.float32), temperature)
 
     def forward(self, target, z, mask=None, conf_score=None, text_latents=None, t=None, noise=None):
         bsz, seq_len, _ = target.shape

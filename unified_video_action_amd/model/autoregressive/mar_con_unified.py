@@ -14,6 +14,8 @@ scipy truncnorm, torch RNG).
 """
 from functools import partial
 
+import math
+
 import numpy as np
 import scipy.stats as stats
 import torch
@@ -293,40 +295,82 @@ class MAR(nn.Module):
         return self.forward_loss(z, gt, mask, nactions, task_mode, proprioception_input, draws)
 
 
-    # ---- inference (:945-1047), policy / inverse paths ---------------------------------
+    # ---- inference (:945-1151) ----------------------------------------------------------
     @torch.no_grad()
     def sample_tokens(self, bsz, cond, text_latents=None, num_iter=64, cfg=1.0, cfg_schedule="linear",
                       temperature=1.0, progress=False, history_nactions=None, nactions=None,
                       proprioception_input={}, task_mode=None, vae_model=None, x=None, rng=None):
-        """policy_model / inverse_model: one encoder+decoder pass over the (fully masked) token
-        grid, then the action head's reverse diffusion (act_cfg = 1.0) -> (None, actions
-        [B, 16, Da]).  The reference returns on the first MaskGIT iteration for these modes
-        (:1040-1041); the video-generation loop (:1043-1100) is not on this path.  `rng` may
-        inject {"noise": x_T, "step_noise": [S, B*16, Da]} (the sampler's randn draws)."""
-        if task_mode not in ("policy_model", "inverse_model"):
-            raise NotImplementedError(f"sample_tokens task_mode={task_mode}: video generation loop not built")
-        if not self.predict_action:
-            raise NotImplementedError("sample_tokens without an action head returns nothing on this path")
+        """policy_model / inverse_model: one encoder+decoder pass over the fully masked (policy) or
+        fully visible (inverse) grid, then the action head's reverse diffusion (act_cfg = 1.0)
+        -> (None, actions [B, 16, Da]) -- the reference returns on the first iteration (:1040-1041).
+        Video modes (video_model, dynamic_model, full_dynamic_model): the MaskGIT loop (:1043-1115)
+        -- each iteration re-encodes the grid, samples the action head (when present), picks the
+        tokens to predict from the cosine mask schedule over the generation order, and samples
+        them with the video diffusion head -> (latents [(B*4), C, 16, 16], actions or None).
+        `rng` injects {"orders", and per iteration i: "act_noise"/"act_step_noise"[i],
+        "video_noise"/"video_step_noise"[i]} (or "noise"/"step_noise" for the action-only modes)."""
+        if cfg != 1.0:
+            raise NotImplementedError("classifier-free guidance (forward_with_cfg) is not on the built path")
         rng = rng or {}
         dev = cond.device
         cnd = self.to_tokens(cond).to(F32)
         B = cnd.shape[0]
+        T, L = self.n_frames, self.seq_len
         if text_latents is not None and self.clip:
             text_latents = linear(text_latents.to(dev).float(), self.text_proj_cond, out_dtype=F32)
         if task_mode == "inverse_model":
             tokens = self.to_tokens(x).to(F32)
-            mask = torch.zeros(B, self.n_frames * self.seq_len, device=dev)
+            mask = np.zeros((B, L), np.float32)
         else:
-            tokens = torch.zeros(B, self.n_frames, self.seq_len, self.token_embed_dim, device=dev)
-            mask = torch.ones(B, self.n_frames * self.seq_len, device=dev)
-        if "orders" not in rng:
-            self.sample_orders(bsz)  # drawn but unused on these paths (:994), kept for RNG parity
-        h = self.forward_mae_encoder(tokens, mask, cnd, text_latents, nactions, task_mode, proprioception_input,
-                                     torch.ones(B))
-        z = self.forward_mae_decoder(h)
-        act = self.diffactloss.sample(z, temperature, cfg=1.0, text_latents=text_latents,
-                                      noise=rng.get("noise"), step_noise=rng.get("step_noise"))
-        return None, act
+            tokens = torch.zeros(B, T, L, self.token_embed_dim, device=dev)
+            mask = np.ones((B, L), np.float32)
+        orders = np.asarray(rng["orders"]) if "orders" in rng else self.sample_orders(bsz)
+        act_modes = ("policy_model", "inverse_model")
+        if task_mode not in act_modes + ("video_model", "dynamic_model", "full_dynamic_model"):
+            raise NotImplementedError(f"sample_tokens task_mode={task_mode}")
+        if task_mode in act_modes and not self.predict_action:
+            raise NotImplementedError("sample_tokens without an action head returns nothing on this path")
+        if task_mode != "policy_model" and task_mode != "inverse_model" and not self.predict_video:
+            raise NotImplementedError("video sampling without predict_video")
+
+        def pick(key, i):
+            v = rng.get(key)
+            return None if v is None else v[i]
+
+        act = None
+        for step in range(num_iter if task_mode not in act_modes else 1):
+            m_full = torch.from_numpy(np.repeat(mask[:, None, :], T, axis=1).reshape(B, T * L)).to(dev)
+            h = self.forward_mae_encoder(tokens, m_full, cnd, text_latents, nactions, task_mode,
+                                         proprioception_input, torch.ones(B))
+            z = self.forward_mae_decoder(h)
+            if self.predict_action:
+                if task_mode in act_modes:
+                    an, asn = rng.get("noise"), rng.get("step_noise")
+                else:
+                    an, asn = pick("act_noise", step), pick("act_step_noise", step)
+                act = self.diffactloss.sample(z, temperature, cfg=1.0, text_latents=text_latents, noise=an,
+                                              step_noise=asn)
+            if task_mode in act_modes:
+                return None, act
+            # mask schedule (:1049-1086), bit-exact on the host: float32 as the reference's tensors
+            ratio = np.cos(math.pi / 2.0 * (step + 1) / num_iter)
+            mask_len = np.float32(np.floor(L * ratio))
+            mask_len = max(np.float32(1.0), min(np.float32(mask[0].sum() - 1), mask_len))
+            nxt = np.zeros((B, L), np.float32)
+            np.put_along_axis(nxt, orders[:, :int(mask_len)], 1.0, axis=1)
+            cur = mask.astype(bool)
+            to_pred = cur if step >= num_iter - 1 else np.logical_xor(cur, nxt.astype(bool))
+            mask = nxt
+            sel = torch.from_numpy(np.repeat(to_pred[:, None, :], T, axis=1).reshape(-1).nonzero()[0]).to(dev)
+            zr = z.reshape(B * T * L, -1).index_select(0, sel)
+            lat = self.diffloss.sample(zr, temperature, 1.0, text_latents=text_latents,
+                                       noise=pick("video_noise", step), step_noise=pick("video_step_noise", step))
+            flat = tokens.reshape(B * T * L, -1).clone()
+            flat.index_copy_(0, sel, lat.to(flat.dtype))
+            tokens = flat.reshape(B, T, L, -1)
+        # unpatchify (patch_size 1): [(b t), s, c] -> [(b t), c, h, w]
+        out = tokens.reshape(B * T, self.seq_h, self.seq_w, -1).permute(0, 3, 1, 2).contiguous()
+        return out, act
 
 
 def _mar(D, depth, heads, **kwargs):

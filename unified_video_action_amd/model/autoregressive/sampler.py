@@ -42,8 +42,9 @@ class ActionSampler:
 
     MOD_BYTES_CAP = 16 << 30  # all-step modulation table above this is computed per step
 
-    def __init__(self, net, respacing="100", use_graph=True, use_fused=True):
+    def __init__(self, net, respacing="100", use_graph=True, use_fused=True, clip_denoised=True):
         self.net = net
+        self.clip = clip_denoised  # action head: True (diffusion_action_loss.py:218); video head: False
         self.sched = sampling_schedule(respacing)
         self.use_graph = use_graph
         self.use_fused = use_fused  # few-row fused LN+linear kernels (bf16 compute, width <= 1024)
@@ -122,7 +123,7 @@ class ActionSampler:
         else:
             self._step_unfused(x, mod, st)
         coef = list(self.sched.steps[k][2]) + [st["temperature"]]
-        ops.p_sample_step(st["out"], st["x"], st["noise"][k], coef, st["x"], st["x_net"])
+        ops.p_sample_step(st["out"], st["x"], st["noise"][k], coef, st["x"], st["x_net"], clip=self.clip)
 
     def _step_unfused(self, x, mod, st):
         """general-route step body (fp32 parity mode, or widths over the fused kernel's K limit)."""

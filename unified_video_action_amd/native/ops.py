@@ -259,7 +259,7 @@ def diffusion_loss(x0, noise, t, out, tables, loss_row, dl):
                ctypes.cast(arr, ctypes.c_void_p), ptr(loss_row), ptr(dl), rows, C, stream())
 
 
-def p_sample_step(out, x, noise, coef, x_new, x_net=None):
+def p_sample_step(out, x, noise, coef, x_new, x_net=None, clip=True):
     """One reverse diffusion step (uva_p_sample_step); coef = 8 python floats of the step."""
     rows, C = x.shape
     if out.shape[0] != rows or out.shape[1] != 2 * C or out.stride(1) != 1:
@@ -272,7 +272,7 @@ def p_sample_step(out, x, noise, coef, x_new, x_net=None):
     k = (ctypes.c_float * 8)(*coef)
     lib().call("uva_p_sample_step", dt(out), ptr(out), out.stride(0), ptr(x), ptr(noise),
                ctypes.cast(k, ctypes.c_void_p), ptr(x_new), dt(x_net) if x_net is not None else 0,
-               ptr(x_net), rows, C, stream())
+               ptr(x_net), int(clip), rows, C, stream())
 
 
 def sampler_linear(A, W, out, bias=None, act="none", ln=False, lnw=None, lnb=None, shift=None, scale=None,
