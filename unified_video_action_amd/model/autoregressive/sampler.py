@@ -41,6 +41,9 @@ class ActionSampler:
     """One p_sample_loop over the SimpleMLPAdaLN `net` conditioned on c [R, z] (fp32)."""
 
     MOD_BYTES_CAP = 16 << 30  # all-step modulation table above this is computed per step
+    # few-row kernels re-read the weights once per 32-row block: beyond ~1k rows (video sampling,
+    # B*1024 tokens) the general 256x256-tile GEMMs are the right tool
+    FUSED_MAX_ROWS = 1024
 
     def __init__(self, net, respacing="100", use_graph=True, use_fused=True, clip_denoised=True):
         self.net = net
@@ -166,7 +169,7 @@ class ActionSampler:
                   h=torch.empty(R, W, dtype=cd, device=dev), a=torch.empty(R, W, dtype=cd, device=dev),
                   mean=torch.empty(R, dtype=F32, device=dev), rstd=torch.empty(R, dtype=F32, device=dev),
                   out=torch.empty(R, 2 * C, dtype=F32, device=dev), graph=None,
-                  fused=self.use_fused and cd == torch.bfloat16 and W in (256, 512, 1024))
+                  fused=self.use_fused and cd == torch.bfloat16 and W in (256, 512, 1024) and R <= self.FUSED_MAX_ROWS)
         self._cache = st
         return st
 
