@@ -233,6 +233,11 @@ int uva_groupnorm_apply(const void* x, const float* scale, const float* shift, v
 /* y [n, 2H, 2W, C] = nearest x2 upsample of NHWC x [n, H, W, C] (decoder Upsample,
  * vaekl.py:20-33); C * sizeof(dtype) % 16 == 0. */
 int uva_upsample_nearest2x(int dtype, const void* x, void* y, int n, int H, int W, int C, hipStream_t stream);
+/* PushT training augmentation (dataset/pusht_image_dataset.py:93-130): per video b, params[b][9] =
+ * {crop (0/1), top, left, blur (0/1), k0..k4 (normalised 1-D Gaussian)}; img/out [B,T,C,S,S] fp32,
+ * crop window crop_size^2 resized back to S^2 (bilinear), then the 5x5 reflect-padded blur. */
+int uva_pusht_augment(const float* img, float* out, const float* params, int B, int T, int C, int S, int crop_size,
+                      hipStream_t stream);
 int uva_posterior_sample(int mdt, const void* moments, const float* eps, float* z, int Nimg, float scale,
                          hipStream_t stream);
 

@@ -702,6 +702,27 @@ def train_frame_indices(T=32, k=4):
     return torch.arange(0, T, T // (2 * k)) + k - 1
 
 
+def pusht_augment(image, params, crop=91):
+    """PushT dataset augmentation (pusht_image_dataset.py:93-130) with drawn parameters
+    {crop, top, left, blur, k0..k4} per video: crop -> Resize(96, antialias) -> reflect-padded
+    5x5 Gaussian (torchvision gaussian_blur restated; torchvision absent: parity unpinned)."""
+    B, T, C, S, _ = image.shape
+    out = []
+    for b in range(B):
+        x = image[b]
+        p = params[b]
+        if p[0] != 0:
+            t, l = int(p[1]), int(p[2])
+            x = F.interpolate(x[..., t:t + crop, l:l + crop], size=(S, S), mode="bilinear", align_corners=False,
+                              antialias=True)
+        if p[3] != 0:
+            k = p[4:9].float()
+            k2 = (k[:, None] * k[None, :]).expand(C, 1, 5, 5)
+            x = F.conv2d(F.pad(x, (2, 2, 2, 2), mode="reflect"), k2, groups=C)
+        out.append(x)
+    return torch.stack(out)
+
+
 def eval_frame_indices(T=32, k=4):
     """[3, 11, 19, 27] for T=32 (select_frames eval=True, data_utils.py:141-142)."""
     return torch.arange(0, T, T // k) + k - 1

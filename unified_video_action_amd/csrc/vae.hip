@@ -281,3 +281,78 @@ extern "C" int uva_upsample_nearest2x(int dtype, const void* x, void* y, int n, 
   UVA_LAUNCH_CHECK();
   return 0;
 }
+
+// PushT training augmentation on the device (dataset/pusht_image_dataset.py:93-130; the reference
+// runs it per video in the CPU dataloader with one seed for all frames):
+//   RandomApply(RandomCrop(91), p=0.5) -> Resize(96, antialias) -> RandomApply(GaussianBlur(5), p=0.5)
+// img/out: [B, T, C, S, S] fp32 in [0, 1].  prm: [B][9] floats per video
+//   {crop, top, left, blur, k0..k4}: k = the normalised 1-D Gaussian (torchvision
+//   _get_gaussian_kernel1d, computed on the host).  Upscaling 91 -> 96 with antialias reduces to
+//   bilinear with align_corners=False (triangle filter of support 1; edge taps clamp).  The blur
+//   is the separable 5x5 product kernel over the reflect-padded resized image, evaluated per
+//   output pixel from the source (the 96x96 intermediate never exists).
+__device__ __forceinline__ int reflect_idx(int i, int n) {
+  i = i < 0 ? -i : i;
+  return i >= n ? 2 * n - 2 - i : i;
+}
+
+__device__ __forceinline__ float aug_resized(const float* __restrict__ plane, int S, bool crop, int top, int left,
+                                             int cs, int y, int x) {
+  if (!crop) return plane[y * S + x];
+  const float sc = (float)cs / (float)S;
+  float sy = ((float)y + 0.5f) * sc - 0.5f, sx = ((float)x + 0.5f) * sc - 0.5f;
+  sy = sy < 0.f ? 0.f : sy;
+  sx = sx < 0.f ? 0.f : sx;
+  const int y0 = (int)sy, x0 = (int)sx;
+  const int y1 = y0 + 1 < cs ? y0 + 1 : cs - 1, x1 = x0 + 1 < cs ? x0 + 1 : cs - 1;
+  const float ly = sy - (float)y0, lx = sx - (float)x0;
+  const float* r0 = plane + (top + y0) * S + left;
+  const float* r1 = plane + (top + y1) * S + left;
+  const float a = r0[x0] * (1.f - lx) + r0[x1] * lx;
+  const float b = r1[x0] * (1.f - lx) + r1[x1] * lx;
+  return a * (1.f - ly) + b * ly;
+}
+
+__global__ void pusht_augment_kernel(const float* __restrict__ img, float* __restrict__ out, const float* __restrict__ prm,
+                                     int B, int TC, int S, int cs) {
+  const long long total = (long long)B * TC * S * S;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += (long long)gridDim.x * blockDim.x) {
+    const int x = (int)(i % S);
+    const int y = (int)((i / S) % S);
+    const long long plane_id = i / ((long long)S * S);
+    const int b = (int)(plane_id / TC);
+    const float* p = prm + b * 9;
+    const bool crop = p[0] != 0.f, blur = p[3] != 0.f;
+    const int top = (int)p[1], left = (int)p[2];
+    const float* plane = img + plane_id * S * S;
+    float v;
+    if (!blur) {
+      v = aug_resized(plane, S, crop, top, left, cs, y, x);
+    } else {
+      v = 0.f;
+#pragma unroll
+      for (int dy = -2; dy <= 2; ++dy) {
+        const int yy = reflect_idx(y + dy, S);
+        float row = 0.f;
+#pragma unroll
+        for (int dx = -2; dx <= 2; ++dx) row += p[6 + dx] * aug_resized(plane, S, crop, top, left, cs, yy, reflect_idx(x + dx, S));
+        v += p[6 + dy] * row;
+      }
+    }
+    out[i] = v;
+  }
+}
+
+extern "C" int uva_pusht_augment(const float* img, float* out, const float* params, int B, int T, int C, int S,
+                                 int crop_size, hipStream_t s) {
+  if (B <= 0 || T <= 0 || C <= 0 || S < 3 || crop_size <= 0 || crop_size > S || img == out) {
+    return (int)hipErrorInvalidValue;
+  }
+  const long long total = (long long)B * T * C * S * S;
+  long long blocks = (total + 255) / 256;
+  if (blocks > 16384) blocks = 16384;
+  pusht_augment_kernel<<<dim3((unsigned)blocks), 256, 0, s>>>(img, out, params, B, T * C, S, crop_size);
+  UVA_LAUNCH_CHECK();
+  return 0;
+}
