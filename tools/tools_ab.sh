@@ -1,5 +1,5 @@
 #!/bin/bash
-# Same-box A/B of an env switch on the full bench: bash tools_ab.sh VAR "A B" [rounds]
+# Same-box A/B of an env switch on the full bench: bash tools/tools_ab.sh VAR "A B" [rounds]
 # prints value per run, alternating A, B, A, B ... (box-to-box variance is ~2-5 %, larger than
 # most single changes).  VAR=UVA_LIB_PATH compares two builds of the library.
 VAR=$1; VALS=$2; R=${3:-2}

@@ -1,5 +1,5 @@
 """Per-tile phase split (prologue / 18-step main loop / epilogue, s_memtime ticks) of the halo conv
-at the VAE level-0 shape: UVA_CONV_VAR=1 python tools_conv_phase.py [H Ci Co]"""
+at the VAE level-0 shape: UVA_CONV_VAR=1 python tools/tools_conv_phase.py [H Ci Co]"""
 import ctypes
 import sys
 import numpy as np

@@ -1,4 +1,4 @@
-"""conv_in alone (level-0 shape), for rocprofv3 --pmc passes:  python tools_convin_pmc.py"""
+"""conv_in alone (level-0 shape), for rocprofv3 --pmc passes:  python tools/tools_convin_pmc.py"""
 import sys
 import torch
 sys.path.insert(0, ".")

@@ -1,5 +1,5 @@
 """Per-tile phase split (prologue / K loop / epilogue, s_memtime ticks) of the 8-phase GEMM at an
-M x N x K NN bf16 shape: UVA_8PH_VAR=32 python tools_gemm8_phase.py M N K"""
+M x N x K NN bf16 shape: UVA_8PH_VAR=32 python tools/tools_gemm8_phase.py M N K"""
 import ctypes
 import sys
 import numpy as np

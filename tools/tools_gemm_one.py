@@ -1,4 +1,4 @@
-"""Run one GEMM shape a few times (for rocprofv3 PMC passes): python tools_gemm_one.py M N K ta tb [iters]."""
+"""Run one GEMM shape a few times (for rocprofv3 PMC passes): python tools/tools_gemm_one.py M N K ta tb [iters]."""
 import sys
 import torch
 sys.path.insert(0, ".")

@@ -1,5 +1,5 @@
 """K / N sweep of the bf16 GEMM (NN, bf16 out) vs hipBLASLt: separates per-tile fixed cost from the
-per-K-tile main-loop cost.  python tools_gemm_sweep.py"""
+per-K-tile main-loop cost.  python tools/tools_gemm_sweep.py"""
 import sys
 import torch
 sys.path.insert(0, ".")

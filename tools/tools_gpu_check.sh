@@ -7,7 +7,7 @@ if [ -n "$FOCUS" ]; then
   tail -2 gpurun_out/pytest_focus.log
 fi
 if [ -n "$KB" ]; then
-  timeout -k 10 200 python tools_kbench.py $KB > gpurun_out/kb.log 2>&1 || { echo KB_FAIL; tail -20 gpurun_out/kb.log; exit 1; }
+  timeout -k 10 200 python tools/tools_kbench.py $KB > gpurun_out/kb.log 2>&1 || { echo KB_FAIL; tail -20 gpurun_out/kb.log; exit 1; }
   cat gpurun_out/kb.log
 fi
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1 || { echo PYTEST_FAIL; tail -30 gpurun_out/pytest_gpu.log; exit 1; }

@@ -1,6 +1,6 @@
 """Inference latency of predict_action (PushT joint config, mar_base, full KL-VAE, 100-step action
 sampler) and of the action sampler alone, graph vs eager.  Run on the GPU box:
-    python tools_infer_bench.py [--batches 1,32] [--iters 10]
+    python tools/tools_infer_bench.py [--batches 1,32] [--iters 10]
 Prints one JSON line per batch size."""
 import argparse
 import json

@@ -1,5 +1,5 @@
 """Instruction mix of a kernel's main loop from a hipcc --save-temps .s file:
-python tools_isa_loop.py file.s kernel_substring"""
+python tools/tools_isa_loop.py file.s kernel_substring"""
 import collections
 import re
 import sys

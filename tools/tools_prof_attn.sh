@@ -1,6 +1,6 @@
 export TMPDIR=/tmp
 mkdir -p gpurun_out/kt
-timeout -s KILL 120 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/kt -o run -- python3 tools_attn_one.py > gpurun_out/kt/log.txt 2>&1
+timeout -s KILL 120 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/kt -o run -- python3 tools/tools_attn_one.py > gpurun_out/kt/log.txt 2>&1
 echo rc=$?
 python3 - <<'PY'
 import csv

@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round profile: rocprofv3 kernel-trace/stats of the bench, then two PMC passes (FETCH_SIZE,
 # WRITE_SIZE; separate runs, no tracing domains) for tools_traffic.py.  Run from the repo root on
-# the GPU box:  bash tools_profile_round.sh <tag>
+# the GPU box:  bash tools/tools_profile_round.sh <tag>
 set -e
 TAG=${1:-r01}
 export TMPDIR=/tmp

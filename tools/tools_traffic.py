@@ -6,7 +6,7 @@ wide streaming reads on gfx950, MI355X_MICROARCH.md §HBM).  A bench tag that sp
 kernels (attn_bwd = pre + dK/dV + dQ) sums them; kernels shared by several tags are told
 apart by grid size.
 
-python tools_traffic.py gpurun_out/prof/pmc_fetch gpurun_out/prof/pmc_write profiles/traffic_r01.json
+python tools/tools_traffic.py gpurun_out/prof/pmc_fetch gpurun_out/prof/pmc_write profiles/traffic_r01.json
 """
 import collections
 import csv
