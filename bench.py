@@ -1,22 +1,34 @@
 """UVA training-step throughput on MI355X (BASELINE.json metric: train samples/sec).
 
-python bench.py --gpus N --steps K --warmup W        (N>1: launched by torch.distributed.run)
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config pusht_video] [--batch 32]
 
-Workload (N=1 line = BASELINE configs[1]): PushT video_model, mar_base (24 blocks, D=768,
-N=1024 tokens) + frozen KL-VAE encoder of 8 frames/sample, bf16 MFMA operands, dropout 0.1
-as configured, batch 32 per GPU, synthetic device-resident batch of the dataset shape
-([B,32,3,96,96] frames, resized on device).  One step = resize/select -> VAE encode ->
-MAR fwd -> diffusion loss -> backward (-> RCCL bucket all-reduce) -> fused AdamW+EMA.
-Weak scaling: batch per GPU fixed.  Prints ONE JSON line on rank 0.
+N > 1: run under torch.distributed.run (RANK / WORLD_SIZE / LOCAL_RANK from the environment),
+or -- when those are unset -- this process spawns N fresh worker processes (one per GPU,
+RCCL over xGMI) before it touches the GPU, and exits with their status.
+
+Workload (the N=1 line = BASELINE configs[1]): PushT video_model, mar_base (24 blocks, D=768,
+N=1024 tokens) + frozen KL-VAE encoder of 8 frames/sample, bf16 MFMA operands, dropout 0.1 as
+configured, batch 32 per GPU, synthetic device-resident batch of the dataset shape
+([B,32,3,96,96] frames, resized on device).  One step = the reference workspace's per-step body
+(workspace:283-302): policy(batch) [frame select+resize -> VAE encode -> MAR fwd -> diffusion
+loss] -> backward (-> RCCL bucket all-reduce inside backward) -> optimizer.step (fused AdamW
++ EMA) -> zero_grad -> lr_scheduler.step -> ema.step.  Weak scaling: batch per GPU fixed.
+
+Timing: W untimed warm-up steps, then exactly K steps between barrier + synchronize pairs, max
+over ranks (`value`, `ms_per_step`), plus the median of the K per-step HIP-event times.  The
+per-kernel trace for `roofline` (HIP events around the traced launches on their stream) runs
+in a separate short pass afterwards, so its event overhead is not in `value`.  At N=1 the
+default run also measures the PushT joint video+action step (BASELINE configs[2] at its
+per-GPU batch 64) and reports it under "other_configs" in the same JSON line.
+Prints ONE JSON line on rank 0.
 """
 import argparse
 import json
 import os
+import socket
+import statistics
 import sys
 import time
-
-import torch
-import torch.distributed as dist
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
@@ -26,25 +38,69 @@ PEAK_HBM_GBS = 8000.0
 # algorithmic GFLOP per sample per step (SURVEY §8d / BASELINE.md §3)
 GFLOP_PER_SAMPLE = {"pusht_video": 2611.9, "pusht_joint": 2546.2, "libero10_joint": 2641.5, "umi_multi": 2674.2}
 METRIC = "train samples/sec (video+action step) at 1/2/4/8 MI355X; loss parity"
+WORKLOAD = {
+    "pusht_video": "PushT video_model (BASELINE configs[1])",
+    "pusht_joint": "PushT joint video+action, all 5 task modes (BASELINE configs[2] per-GPU batch)",
+    "libero10_joint": "Libero10 joint + CLIP language latents, N=1088 (BASELINE configs[3] per-GPU batch)",
+    "umi_multi": "UMI-multi proprio in/out, different_history_freq, 224px frames (BASELINE configs[4])",
+}
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--batch", type=int, default=32)
     ap.add_argument("--config", default="pusht_video", choices=sorted(GFLOP_PER_SAMPLE))
     ap.add_argument("--precision", default="bf16")
+    ap.add_argument("--other-configs", default="pusht_joint:64",
+                    help="N=1 only: extra config:batch entries measured after the main line ('' = none)")
+    ap.add_argument("--other-steps", type=int, default=20)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-batch", type=int, default=2, help="CPU baseline batch (BASELINE configs[0]: 2)")
+    ap.add_argument("--cpu-steps", type=int, default=3, help="timed CPU steps (median) after one warm-up step")
     ap.add_argument("--no-trace", action="store_true")
+    ap.add_argument("--trace-steps", type=int, default=3)
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--trace-out", default="", help="write every traced kernel row (tag, launches, avg ms) here")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r01f.json"))
-    return ap.parse_args()
+    return ap.parse_args(argv)
 
 
-def setup_dist():
+# ---- process launch --------------------------------------------------------------------------
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _spawned(local_rank, world, port, argv):
+    os.environ.update(RANK=str(local_rank), LOCAL_RANK=str(local_rank), WORLD_SIZE=str(world),
+                      LOCAL_WORLD_SIZE=str(world), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    run(parse(argv))
+
+
+def launch(args, argv):
+    """--gpus N with no launcher environment: spawn N workers (fresh interpreters; this parent
+    has not initialised the GPU) and return their exit status."""
+    import torch.multiprocessing as mp
+    ctx = mp.start_processes(_spawned, args=(args.gpus, _free_port(), argv), nprocs=args.gpus, join=False,
+                             start_method="spawn")
+    try:
+        while not ctx.join():
+            pass
+    except Exception as e:  # a worker failed: its traceback is in the message
+        print(f"bench.py: worker failed: {e}", file=sys.stderr, flush=True)
+        return 1
+    return 0
+
+
+def setup_dist(args):
+    import torch
+    import torch.distributed as dist
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -52,39 +108,48 @@ def setup_dist():
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if dist.get_world_size() != args.gpus:
+            raise SystemExit(f"bench.py: --gpus {args.gpus} but the process group has {dist.get_world_size()} ranks")
+    elif args.gpus != 1:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} needs {args.gpus} processes")
     return world, rank, local
 
 
-def build(args, device, world):
+# ---- one training setup + step (the reference workspace's per-step body) ---------------------
+def build(config, precision, device):
+    import copy
+
+    import torch
     from unified_video_action_amd import presets
+    from unified_video_action_amd.model.autoregressive.ema_model import EMAModel
+    from unified_video_action_amd.model.common.lr_scheduler import get_scheduler
     from unified_video_action_amd.policy.unified_video_action_policy import UnifiedVideoActionPolicy
     from unified_video_action_amd.runtime import RT
-    from unified_video_action_amd.workspace.optim import CosineWithWarmup, GradReducer, default_buckets
-    RT.set_precision(args.precision)
+    RT.set_precision(precision)
     torch.manual_seed(42)  # identical init on every rank (the reference seeds every rank alike)
-    pol = UnifiedVideoActionPolicy(**presets.policy_kwargs(args.config)).to(device)
-    presets.fit_normalizer(args.config, pol)
-    pol.train()
+    pol = UnifiedVideoActionPolicy(**presets.policy_kwargs(config))
+    presets.fit_normalizer(config, pol)
+    ema_model = copy.deepcopy(pol)  # workspace:70-72 (before get_optimizer, as the reference)
     opt = pol.get_optimizer(weight_decay=0.02, learning_rate=1e-4, betas=(0.9, 0.95))
-    opt.ema_cfg = dict(power=0.75, inv_gamma=1.0, min_value=0.0, max_value=0.9999, update_after_step=0)
-    opt.grad_scale = 1.0 / world
-    sched = CosineWithWarmup(opt, 1000, 100000)
-    reducer = GradReducer(opt.store, default_buckets(pol.model))
-    return pol, opt, sched, reducer
+    pol.to(device).train()
+    ema_model.to(device)
+    sched = get_scheduler("cosine", opt, num_warmup_steps=1000, num_training_steps=100000)
+    ema = EMAModel(ema_model, update_after_step=0, inv_gamma=1.0, power=0.75, min_value=0.0, max_value=0.9999)
+    return pol, opt, sched, ema
 
 
-def step(pol, opt, sched, reducer, batch):
+def step(pol, opt, sched, ema, batch):
     loss, (lv, la) = pol(batch)
-    loss.backward()
-    reducer.finish()
+    loss.backward()  # the bucket reducer (world > 1) completes inside backward
     opt.step()
     opt.zero_grad()
     sched.step()
+    ema.step(pol)
     return loss
 
 
 def summarize_trace(trace):
-    """tag -> (launches, avg ms, total ms, flops/launch); the dominant kernel by total time."""
+    """tag -> (total ms, tag, launches, avg ms, flops/launch), by total time."""
     rows = []
     for tag, evs in trace.items():
         ms = [a.elapsed_time(b) for a, b, _ in evs]
@@ -93,9 +158,39 @@ def summarize_trace(trace):
     return rows
 
 
+def timed_run(config, batch_size, steps, warmup, precision, device, world, rank):
+    """-> (elapsed s max over ranks, per-step ms list, final loss, (pol, opt, sched, ema, batch))."""
+    import torch
+    import torch.distributed as dist
+    from unified_video_action_amd import presets
+    pol, opt, sched, ema = build(config, precision, device)
+    batch = presets.synthetic_batch(config, batch_size, device, seed=1000 + rank)
+    for _ in range(warmup):
+        step(pol, opt, sched, ema, batch)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
+    t0 = time.perf_counter()
+    for i in range(steps):
+        evs[i][0].record()
+        loss = step(pol, opt, sched, ema, batch)
+        evs[i][1].record()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        dist.barrier()
+        t = torch.tensor([elapsed], device=device, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = t.item()
+    per_step = [a.elapsed_time(b) for a, b in evs]
+    return elapsed, per_step, loss.item(), (pol, opt, sched, ema, batch)
+
+
 def cpu_baseline(args):
-    """oracle (PyTorch-CPU fp32 restatement, pinned to the reference) on a bounded sample:
-    one full training step of the same workload at B=1."""
+    """oracle (PyTorch-CPU fp32 restatement, pinned to the reference) on a bounded sample: the
+    same training step at BASELINE configs[0]'s batch (2), one warm-up step, median of a few."""
+    import torch
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import uva_oracle as O
     th = args.cpu_threads or torch.get_num_threads()
@@ -106,81 +201,98 @@ def cpu_baseline(args):
     vae = O.AutoencoderKLEncoder()
     pol = O.PolicyOracle(mar, vae, [2 / 512, 2 / 512], [-1.0, -1.0]).train()
     opt = torch.optim.AdamW(mar.parameters(), lr=1e-4, betas=(0.9, 0.95), weight_decay=0.02)
-    B = 1
+    B = args.cpu_batch
     img = torch.rand(B, 32, 3, 96, 96)
     act = torch.rand(B, 32, 2) * 512
-    rng = {"orders": torch.stack([torch.randperm(256) for _ in range(B)]).numpy(), "mask_rate": 0.85,
-           "randint": [torch.randint(0, 1000, (B * 1024,))], "randn_like": [torch.randn(B * 1024, 16)],
-           "vae_eps_x": torch.randn(B * 4, 16, 16, 16), "vae_eps_c": torch.randn(B * 4, 16, 16, 16)}
-    t0 = time.perf_counter()
-    loss, _ = pol.compute_loss(img, act, "video_model", rng)
-    loss.backward()
-    opt.step()
-    opt.zero_grad()
-    dt = time.perf_counter() - t0
-    return {"value": B / dt, "unit": "samples/s", "cores": th, "kind": "port",
-            "sample": f"1 full training step (resize->KL-VAE->mar_base fwd/bwd->AdamW), B={B}, PushT video_model, "
-                      f"fp32, dropout 0.1, oracle/uva_oracle.py; {dt:.1f} s"}
+
+    def one():
+        rng = {"orders": torch.stack([torch.randperm(256) for _ in range(B)]).numpy(), "mask_rate": 0.85,
+               "randint": [torch.randint(0, 1000, (B * 1024,))], "randn_like": [torch.randn(B * 1024, 16)],
+               "vae_eps_x": torch.randn(B * 4, 16, 16, 16), "vae_eps_c": torch.randn(B * 4, 16, 16, 16)}
+        t0 = time.perf_counter()
+        loss, _ = pol.compute_loss(img, act, "video_model", rng)
+        loss.backward()
+        opt.step()
+        opt.zero_grad()
+        return time.perf_counter() - t0
+
+    one()  # warm-up
+    ts = [one() for _ in range(args.cpu_steps)]
+    med = statistics.median(ts)
+    return {"value": round(B / med, 5), "unit": "samples/s", "cores": th, "kind": "port",
+            "sample": f"oracle/uva_oracle.py full training step (resize->KL-VAE->mar_base fwd/bwd->AdamW), "
+                      f"PushT video_model, fp32, dropout 0.1, B={B}: 1 warm-up + median of {args.cpu_steps} steps "
+                      f"({', '.join(f'{t:.1f}' for t in ts)} s)"}
 
 
-def main():
-    args = parse()
-    world, rank, local = setup_dist()
+def line_for(config, batch, world, steps, elapsed, per_step, loss):
+    gflop = GFLOP_PER_SAMPLE[config]
+    value = batch * world * steps / elapsed
+    ms = elapsed / steps * 1e3
+    med = statistics.median(per_step)
+    return {"config": config, "workload": WORKLOAD[config], "global_batch": batch * world, "value": round(value, 3),
+            "ms_per_step": round(ms, 2), "ms_per_step_median": round(med, 2),
+            "step_tflops_per_gpu": round(gflop * batch / (ms / 1e3) / 1e3, 1),
+            "step_mfma_frac": round(gflop * batch / (ms / 1e3) / 1e3 / PEAK_BF16_TFLOPS, 4),
+            "final_loss": round(loss, 5)}
+
+
+def run(args):
+    import torch
+    import torch.distributed as dist
+    world, rank, local = setup_dist(args)
     device = torch.device("cuda", local)
-    from unified_video_action_amd import presets
     from unified_video_action_amd.native import ops
-    pol, opt, sched, reducer = build(args, device, world)
-    batch = presets.synthetic_batch(args.config, args.batch, device, seed=1000 + rank)
-    for _ in range(args.warmup):
-        step(pol, opt, sched, reducer, batch)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    if not args.no_trace:
+    elapsed, per_step, loss, state = timed_run(args.config, args.batch, args.steps, args.warmup, args.precision,
+                                               device, world, rank)
+    main = line_for(args.config, args.batch, world, args.steps, elapsed, per_step, loss)
+    rows = None
+    if not args.no_trace:  # separate short traced pass for the roofline (HIP events per launch)
+        pol, opt, sched, ema, batch = state
         ops.TRACE = {}
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        loss = step(pol, opt, sched, reducer, batch)
-    torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
-    if world > 1:
-        dist.barrier()
-        t = torch.tensor([elapsed], device=device, dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = t.item()
-    trace, ops.TRACE = ops.TRACE, None
-    final_loss = loss.item()
+        for _ in range(args.trace_steps):
+            step(pol, opt, sched, ema, batch)
+        torch.cuda.synchronize()
+        trace, ops.TRACE = ops.TRACE, None
+        rows = summarize_trace(trace)
+    del state
+    others = []
+    if world == 1 and args.other_configs:
+        for item in args.other_configs.split(","):
+            cfg, _, b = item.partition(":")
+            b = int(b or args.batch)
+            torch.cuda.empty_cache()
+            e, ps, lo, st = timed_run(cfg, b, args.other_steps, args.warmup, args.precision, device, world, rank)
+            del st
+            others.append(dict(line_for(cfg, b, world, args.other_steps, e, ps, lo), steps=args.other_steps))
     if rank != 0:
         if world > 1:
             dist.barrier()
             dist.destroy_process_group()
         return
-    samples = args.batch * world * args.steps
-    value = samples / elapsed
-    ms = elapsed / args.steps * 1e3
-    gflop = GFLOP_PER_SAMPLE[args.config]
     out = {
-        "metric": METRIC, "value": round(value, 3), "unit": "samples/s", "n_gpus": world, "steps": args.steps,
-        "warmup": args.warmup, "ms_per_step": round(ms, 2), "higher_is_better": True, "scaling": "weak",
-        "vs_baseline": None, "dtype": "bf16" if args.precision == "bf16" else "f32",
+        "metric": METRIC, "value": main["value"], "unit": "samples/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": main["ms_per_step"], "ms_per_step_median": main["ms_per_step_median"],
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+        "dtype": "bf16" if args.precision == "bf16" else "f32",
         "data": "synthetic (device-resident, dataset shapes; random-init weights)",
-        "config": {"workload": f"{args.config}: PushT video_model step = frame select+resize -> KL-VAE encode "
-                               f"(8 frames) -> mar_base MAR fwd/bwd (N=1024) -> diffusion loss -> AdamW+EMA; "
-                               f"dropout 0.1", "model": "UVA mar_base + KL-VAE f16",
-                   "global_batch": args.batch * world, "seq_len": 1024, "parallelism": f"dp{world}"},
-        "step_tflops_per_gpu": round(gflop * args.batch / (ms / 1e3) / 1e3, 1),
-        "step_mfma_frac": round(gflop * args.batch / (ms / 1e3) / 1e3 / PEAK_BF16_TFLOPS, 4),
-        "final_loss": round(final_loss, 5),
+        "config": {"workload": f"{args.config}: {WORKLOAD[args.config]}; step = frame select+resize -> KL-VAE "
+                               f"encode (8 frames) -> mar_base MAR fwd/bwd (N=1024) -> diffusion loss -> backward "
+                               f"-> fused AdamW + EMA -> LR step; dropout 0.1",
+                   "model": "UVA mar_base + KL-VAE f16", "global_batch": args.batch * world, "seq_len": 1024,
+                   "parallelism": f"dp{world}"},
+        "rccl_world": world,
+        "step_tflops_per_gpu": main["step_tflops_per_gpu"], "step_mfma_frac": main["step_mfma_frac"],
+        "final_loss": main["final_loss"],
     }
-    if trace:
-        rows = summarize_trace(trace)
+    if rows:
         tot, tag, n, avg, fl = rows[0]
         ach = fl / (avg * 1e-3) / 1e12
         traffic = None
         if os.path.exists(args.traffic_json):
             try:
                 traffic = json.load(open(args.traffic_json)).get(tag)
-            except Exception:
+            except (OSError, ValueError):
                 traffic = None
         out["roofline"] = {"bound": "mfma", "kernel": tag, "achieved": round(ach, 1), "peak": PEAK_BF16_TFLOPS,
                            "unit": "TFLOP/s", "frac": round(ach / PEAK_BF16_TFLOPS, 4), "traffic": traffic,
@@ -188,17 +300,28 @@ def main():
                            "share_of_traced_time": round(tot / sum(r[0] for r in rows), 4)}
         if args.trace_out:
             with open(args.trace_out, "w") as f:
-                json.dump([{"kernel": t_, "launches_per_step": n_ / args.steps, "total_ms_per_step": a / args.steps,
-                            "avg_ms": av, "tflops": f_ / (av * 1e-3) / 1e12} for a, t_, n_, av, f_ in rows], f, indent=1)
-        out["top_kernels"] = [{"kernel": t_, "total_ms_per_step": round(a / args.steps, 3),
+                json.dump([{"kernel": t_, "launches_per_step": n_ / args.trace_steps,
+                            "total_ms_per_step": a / args.trace_steps, "avg_ms": av,
+                            "tflops": f_ / (av * 1e-3) / 1e12} for a, t_, n_, av, f_ in rows], f, indent=1)
+        out["top_kernels"] = [{"kernel": t_, "total_ms_per_step": round(a / args.trace_steps, 3),
                                "avg_ms": round(av, 4), "tflops": round(f_ / (av * 1e-3) / 1e12, 1)}
                               for a, t_, n_, av, f_ in rows[:8]]
+    if others:
+        out["other_configs"] = others
     if world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(args)
     print(json.dumps(out), flush=True)
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
+
+
+def main(argv=None):
+    argv = sys.argv[1:] if argv is None else argv
+    args = parse(argv)
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch(args, argv))
+    run(args)
 
 
 if __name__ == "__main__":

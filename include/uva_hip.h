@@ -192,9 +192,14 @@ int uva_sampler_linear(int ln, const void* A, long long lda, const float* lnw, c
                        long long ldo, int R, int N, int K, hipStream_t stream);
 
 /* ---- optimizer + EMA (policy:343-360 torch AdamW; ema_model.py:57-89) ----------------- */
+/* One launch per parameter group region (16-B aligned p/g/m/v/ema): n_decay = n applies the
+ * group's weight decay wd, n_decay = 0 none.  ema (nullable) gets the fused EMA update with
+ * ema_decay; p_bf16 (nullable) the refreshed bf16 shadow. */
 int uva_adamw_ema(float* p, const float* g, float* m, float* v, float* ema, void* p_bf16, long long n,
                   long long n_decay, float lr, float b1, float b2, float eps, float wd, int step, float grad_scale,
                   float ema_decay, hipStream_t stream);
+/* EMAModel.step over the flat buffer (ema_model.py:78-85): ema = d*ema + (1-d)*p (16-B aligned). */
+int uva_ema_update(float* ema, const float* p, long long n, float decay, hipStream_t stream);
 
 /* ---- fused attention, head_dim 64, bf16 (timm Attention / SDPA with attn dropout,
  *      mar_con_unified.py:201-249 -> timm 0.9.7 Attention.forward, F.scaled_dot_product_attention).

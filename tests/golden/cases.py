@@ -203,3 +203,34 @@ def video_sample_rng(variant, num_iter=VIDEO_SAMPLE_ITERS, B=B_MAR):
         r["video_noise"].append(hash_normal(f"{tag}/{step}/vxT", (rows, 16)))
         r["video_step_noise"].append(hash_normal(f"{tag}/{step}/vsteps", (SAMPLE_STEPS, rows, 16)))
     return r
+
+
+# ---- workspace trace (reference per-step body, workspace:279-302) -------------------------
+TRACE_STEPS = 4
+TRACE_MODES = ["full_dynamic_model", "video_model", "policy_model", "full_dynamic_model"]
+TRACE_LR = dict(name="cosine", warmup=1, total=10, lr=1e-4, betas=(0.9, 0.95), weight_decay=0.02)
+TRACE_EMA = dict(update_after_step=0, inv_gamma=1.0, power=0.75, min_value=0.0, max_value=0.9999)
+TRACE_PARAMS = ("model.z_proj.weight", "model.encoder_blocks.0.attn.qkv.weight", "model.decoder_norm.weight",
+                "model.diffloss.net.res_blocks.0.mlp.0.weight", "model.diffactloss.net.final_layer.linear.bias")
+
+
+def trace_batch(step, B=POLICY_B):
+    img = (hash_tensor(f"trace/{step}/image", (B, 32, 3, 96, 96)) + 1.0) * 0.5
+    pos = (hash_tensor(f"trace/{step}/agent_pos", (B, 32, 2)) + 1.0) * 256.0
+    act = (hash_tensor(f"trace/{step}/action", (B, 32, 2)) + 1.0) * 256.0
+    return {"image": img, "agent_pos": pos, "action": act}
+
+
+def trace_rng(step, B=POLICY_B):
+    mode = TRACE_MODES[step]
+    tag = f"trace/{step}/{mode}"
+    r = mar_rng("pusht", mode, B)
+    # distinct draws per step (mar_rng is keyed by mode only)
+    r["orders"] = orders(tag, B)
+    r["mask_rate"] = mask_rate(tag)
+    r["randint"] = [t_steps(f"{tag}/{i}", len(x)) for i, x in enumerate(r["randint"])]
+    r["randn_like"] = [hash_normal(f"{tag}/{i}/noise", x.shape) for i, x in enumerate(r["randn_like"])]
+    r["vae_eps_x"] = hash_normal(tag + "/eps_x", (B * 4, 16, 16, 16))
+    r["vae_eps_c"] = hash_normal(tag + "/eps_c", (B * 4, 16, 16, 16))
+    r["task_mode"] = mode
+    return r

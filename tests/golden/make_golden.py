@@ -474,6 +474,82 @@ def gen_predict():
     print("predict pusht: action_pred", tuple(res["action_pred"].shape), res["action_pred"][0, :3].tolist())
 
 
+def gen_workspace_trace():
+    """The reference's per-step training body (workspace:279-302) on the golden PushT policy
+    (full KL-VAE, reduced MAR, joint model): deepcopy EMA policy, policy.get_optimizer (torch
+    AdamW, two groups), cosine-with-warmup LambdaLR (diffusers restated: diffusers is absent),
+    the reference EMAModel, step order fwd -> bwd -> opt.step -> zero_grad -> lr.step -> ema.step;
+    draws injected per step (cases.trace_rng)."""
+    import copy
+    import math
+    from unified_video_action.policy.unified_video_action_policy import UnifiedVideoActionPolicy
+
+    class AD(dict):
+        def __getattr__(self, k):
+            if k.startswith("__"):
+                raise AttributeError(k)
+            v = self[k]
+            return AD(v) if isinstance(v, dict) else v
+
+    ref_mar.mar_golden = lambda **kw: ref_mar.MAR(
+        norm_layer=partial(nn.LayerNorm, eps=1e-6), **cases.MAR_GOLDEN, **kw)
+    amp = dict(pretrained_model_path=None, model_size="mar_golden")
+    for k in cases.POLICY_AMP_KEYS:
+        amp[k] = cases.MAR_KW[k]
+    pol = _ref_policy(UnifiedVideoActionPolicy, AD, amp)
+    pol.train()
+    ema_model = copy.deepcopy(pol)
+    L = cases.TRACE_LR
+    opt = pol.get_optimizer(weight_decay=L["weight_decay"], learning_rate=L["lr"], betas=L["betas"])
+
+    def cosine(step, warm=L["warmup"], total=L["total"]):
+        if step < warm:
+            return step / max(1, warm)
+        prog = (step - warm) / max(1, total - warm)
+        return max(0.0, 0.5 * (1.0 + math.cos(math.pi * 0.5 * 2.0 * prog)))
+
+    sched = torch.optim.lr_scheduler.LambdaLR(opt, cosine, last_epoch=-1)
+    ema = EMAModel(ema_model, **cases.TRACE_EMA)
+
+    class Cfg:
+        class task:
+            name = "pusht"
+
+    rows = []
+    for step in range(cases.TRACE_STEPS):
+        b = cases.trace_batch(step)
+        batch = {"obs": {"image": torch.from_numpy(b["image"]), "agent_pos": torch.from_numpy(b["agent_pos"])},
+                 "action": torch.from_numpy(b["action"])}
+        batch = data_utils.resize_image(Cfg, batch)
+        rng = cases.trace_rng(step)
+        pol.model.mask_ratio_generator = type("G", (), {"rvs": staticmethod(
+            lambda n, r=rng["mask_rate"]: np.array([r]))})()
+        with injected(rng):
+            loss, (lv, la) = pol(batch)
+        loss.backward()
+        opt.step()
+        opt.zero_grad()
+        sched.step()
+        ema.step(pol)
+        rows.append([loss.item(), float(lv), float(la), sched.get_last_lr()[0], ema.decay])
+        print(f"trace step {step} {rng['task_mode']}: loss={loss.item():.6f} lr={rows[-1][3]:.3e} "
+              f"decay={ema.decay:.6f}")
+    live = dict(pol.named_parameters())
+    avg = dict(ema_model.named_parameters())
+    out = {"rows": np.array(rows, np.float64), "names": np.array(cases.TRACE_PARAMS)}
+    out["live"] = np.stack([checksum(live[n]) for n in cases.TRACE_PARAMS])
+    out["ema"] = np.stack([checksum(avg[n]) for n in cases.TRACE_PARAMS])
+    def heads(d):
+        h = np.zeros((len(cases.TRACE_PARAMS), 8), np.float64)
+        for i, n in enumerate(cases.TRACE_PARAMS):
+            v = d[n].detach().double().reshape(-1)[:8].numpy()
+            h[i, :len(v)] = v
+        return h
+
+    out["live_heads"], out["ema_heads"] = heads(live), heads(avg)
+    np.savez(os.path.join(OUT, "g6_workspace_trace.npz"), **out)
+
+
 if __name__ == "__main__":
     which = sys.argv[1:] or ["indexing", "mar", "block", "mlp", "diffusion_math", "vae",
                              "resize", "ema", "policy", "sample", "predict", "vae_decode", "video_sample"]

@@ -59,3 +59,42 @@ def grad_rel_errors(named_params, fixture, names_key, sums_key, heads_key):
         e_head = np.max(np.abs(h - heads[i][: len(h)])) / scale
         errs[n] = max(e_sum, e_sq, e_head)
     return errs
+
+
+def golden_policy(predict_action=True, normalizer=True):
+    """This build's UnifiedVideoActionPolicy configured like make_golden._ref_policy: full KL-VAE,
+    reduced MAR (cases.MAR_GOLDEN) as model_size "mar_golden", hash-initialised, PushT limits
+    normalizer; on the CPU, train mode."""
+    from functools import partial
+
+    import torch.nn as nn
+    from unified_video_action_amd.model.autoregressive import mar_con_unified as pmar
+    from unified_video_action_amd.model.common.normalizer import LinearNormalizer
+    from unified_video_action_amd.policy.unified_video_action_policy import UnifiedVideoActionPolicy
+    pmar.mar_golden = lambda **kw: pmar.MAR(norm_layer=partial(nn.LayerNorm, eps=1e-6), **cases.MAR_GOLDEN, **kw)
+    amp = dict(pretrained_model_path=None, model_size="mar_golden")
+    for k in cases.POLICY_AMP_KEYS:
+        amp[k] = cases.MAR_KW[k]
+    pol = UnifiedVideoActionPolicy(
+        vae_model_params=dict(autoencoder_path=None, ddconfig=dict(vae_embed_dim=16, ch_mult=[1, 1, 2, 2, 4])),
+        autoregressive_model_params=amp,
+        action_model_params=dict(predict_action=predict_action, act_model_type="conv_fc"),
+        shape_meta={"action": {"shape": [2]}}, n_action_steps=8, shift_action=True, language_emb_model=None,
+        task_name="pusht", task_modes=[], normalizer_type="all", selected_training_mode=None,
+        use_history_action=False, use_proprioception=False, action_mask_ratio=0.5, different_history_freq=False,
+        predict_wrist_img=False, predict_proprioception=False)
+    hash_init_(pol.vae_model, "vae.")
+    hash_init_(pol.model, "mar.")
+    if normalizer:
+        norm = LinearNormalizer()
+        lim = torch.zeros(2, 2)
+        lim[1] = 512.0
+        norm.fit({"action": lim, "agent_pos": lim})
+        pol.set_normalizer(norm)
+    return pol.train()
+
+
+def device_batch(b, device):
+    return {"obs": {"image": torch.from_numpy(b["image"]).to(device),
+                    "agent_pos": torch.from_numpy(b["agent_pos"]).to(device)},
+            "action": torch.from_numpy(b["action"]).to(device)}

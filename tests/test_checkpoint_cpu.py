@@ -1,15 +1,18 @@
-"""Reference-layout `.ckpt` payloads (workspace/checkpoint.py; base_workspace.py:33-135): round
-trip through torch.save / torch.load(weights_only=True), and the optimizer state exchanged with
-torch.optim.AdamW built the way policy.get_optimizer builds it (policy:326-360)."""
+"""Reference-layout `.ckpt` payloads (workspace/checkpoint.py, workspace/base_workspace.py;
+reference base_workspace.py:33-135): round trip, optimizer state exchanged with a real
+torch.optim.AdamW built like the reference policy.get_optimizer (policy:326-360), loading a
+payload whose cfg pickles as OmegaConf objects through the restricted loader (nothing from the
+file executes), refusal of any other global, and the pretrained warm start
+(policy:113-118,140-218) from MAR `model_ema` and UVA `state_dicts.ema_model` payloads."""
+import copy
 import pickle
-from functools import partial
+import sys
+import types
 
 import pytest
 import torch
-import torch.nn as nn
 
-import cases
-from hashinit import hash_init_
+import replay
 
 
 @pytest.fixture
@@ -20,104 +23,152 @@ def fp32():
     RT.set_precision("bf16")
 
 
-def _policy():
-    from unified_video_action_amd.model.autoregressive import mar_con_unified as pmar
-    from unified_video_action_amd.policy.unified_video_action_policy import UnifiedVideoActionPolicy
-    pmar.mar_golden = lambda **kw: pmar.MAR(norm_layer=partial(nn.LayerNorm, eps=1e-6), **cases.MAR_GOLDEN, **kw)
-    amp = dict(pretrained_model_path=None, model_size="mar_golden")
-    for k in cases.POLICY_AMP_KEYS:
-        amp[k] = cases.MAR_KW[k]
-    pol = UnifiedVideoActionPolicy(
-        vae_model_params=dict(autoencoder_path=None, ddconfig=dict(vae_embed_dim=16, ch_mult=[1, 1, 2, 2, 4])),
-        autoregressive_model_params=amp, action_model_params=dict(predict_action=True, act_model_type="conv_fc"),
-        shape_meta={"action": {"shape": [2]}}, n_action_steps=8, shift_action=True, language_emb_model=None,
-        task_name="pusht", task_modes=[], normalizer_type="all", selected_training_mode=None,
-        use_history_action=False, use_proprioception=False, action_mask_ratio=0.5, different_history_freq=False,
-        predict_wrist_img=False, predict_proprioception=False)
-    hash_init_(pol.model, "mar.")
-    return pol
+def _packed(opt, buf):
+    """the parameter regions of a flat optimizer buffer (group padding dropped)."""
+    return torch.cat([buf[o:o + k] for o, k in (opt.store.offsets[id(p)] for _, p in opt.store.order)])
 
 
-def _opt(pol):
+def _opt_with_state(pol):
     opt = pol.get_optimizer(weight_decay=0.02, learning_rate=1e-4, betas=(0.9, 0.95))
     g = torch.Generator().manual_seed(0)
     opt.m.copy_(torch.randn(opt.m.shape, generator=g))
     opt.v.copy_(torch.rand(opt.v.shape, generator=g))
-    opt.ema.copy_(torch.randn(opt.ema.shape, generator=g))
-    opt.step_count = opt.ema_step_count = 7
+    opt.step_count = 7
     return opt
 
 
-def test_checkpoint_round_trip(tmp_path, fp32):
-    from unified_video_action_amd.workspace.checkpoint import load_checkpoint, save_checkpoint
-    from unified_video_action_amd.workspace.optim import CosineWithWarmup
-    pol = _policy()
-    opt = _opt(pol)
-    sch = CosineWithWarmup(opt, 10, 100)
+def test_payload_round_trip(tmp_path, fp32):
+    from unified_video_action_amd.model.common.lr_scheduler import get_scheduler
+    from unified_video_action_amd.workspace.checkpoint import load_checkpoint, safe_load, save_checkpoint
+    pol = replay.golden_policy()
+    ema = copy.deepcopy(pol)
+    with torch.no_grad():
+        for p in ema.model.parameters():
+            p.mul_(0.5)
+    opt = _opt_with_state(pol)
+    sch = get_scheduler("cosine", opt, num_warmup_steps=10, num_training_steps=100)
     for _ in range(12):
         sch.step()
     path = tmp_path / "latest.ckpt"
-    save_checkpoint(path, pol, opt, sch, global_step=12, epoch=3, cfg={"name": "uva_pusht"})
-    payload = torch.load(path, weights_only=True)  # loadable with the safe loader
-    assert set(payload) == {"cfg", "state_dicts", "pickles"}
+    save_checkpoint(path, pol, ema, opt, sch, cfg={"name": "uva_pusht"}, global_step=12, epoch=3)
+    payload = torch.load(path, weights_only=True)  # plain tensors / containers only
     assert set(payload["state_dicts"]) == {"model", "ema_model", "optimizer", "lr_scheduler"}
-    assert pickle.loads(payload["pickles"]["global_step"]) == 12
+    assert "ddp_anchor" not in payload["state_dicts"]["model"]
+    assert payload["state_dicts"]["optimizer"]["param_groups"][0]["weight_decay"] == 0.0
+    assert payload["state_dicts"]["optimizer"]["param_groups"][1]["weight_decay"] == 0.02
 
-    pol2 = _policy()
+    pol2 = replay.golden_policy()
     with torch.no_grad():
         for p in pol2.model.parameters():
             p.zero_()
+    ema2 = copy.deepcopy(pol2)
     opt2 = pol2.get_optimizer(weight_decay=0.02, learning_rate=1e-4, betas=(0.9, 0.95))
-    sch2 = CosineWithWarmup(opt2, 10, 100)
-    meta = load_checkpoint(path, pol2, opt2, sch2)
-    assert meta == {"cfg": {"name": "uva_pusht"}, "global_step": 12, "epoch": 3}
-    assert torch.equal(opt2.store.flat, opt.store.flat)
-    assert torch.equal(opt2.m, opt.m) and torch.equal(opt2.v, opt.v) and torch.equal(opt2.ema, opt.ema)
+    sch2 = get_scheduler("cosine", opt2, num_warmup_steps=10, num_training_steps=100)
+    meta = load_checkpoint(path, pol2, ema2, opt2, sch2)
+    assert meta["global_step"] == 12 and meta["epoch"] == 3 and meta["cfg"] == {"name": "uva_pusht"}
+    for (n, a), (_, b) in zip(pol.state_dict().items(), pol2.state_dict().items()):
+        assert torch.equal(a, b), n
+    for (n, a), (_, b) in zip(ema.state_dict().items(), ema2.state_dict().items()):
+        assert torch.equal(a, b), n
+    assert torch.equal(_packed(opt2, opt2.m), _packed(opt, opt.m)) and torch.equal(_packed(opt2, opt2.v), _packed(opt, opt.v))
     assert opt2.step_count == 7
-    assert sch2.last_epoch == sch.last_epoch and opt2.param_groups[0]["lr"] == opt.param_groups[0]["lr"]
-    for k, v in pol.state_dict().items():
-        assert torch.equal(pol2.state_dict()[k], v), k
-    # EMA weights can be loaded as the model (load_payload without "model", base_workspace.py:115-124)
-    pol3 = _policy()
-    load_checkpoint(path, pol3, use_ema_weights=True)
-    ema = opt.ema_state()
-    for n, p in pol3.model.named_parameters():
-        assert torch.equal(p.detach(), ema[n]), n
+    assert sch2.last_epoch == sch.last_epoch and sch2.get_last_lr() == sch.get_last_lr()
+    assert safe_load(path)["state_dicts"]["optimizer"]["state"][0]["step"].item() == 7.0
 
 
 def test_optimizer_state_exchanges_with_torch_adamw(fp32):
-    """ours -> torch AdamW.load_state_dict -> its state_dict -> ours: identical, and the layout
-    (groups, ids, per-param state) is the one torch produces for policy.get_optimizer's groups."""
-    from unified_video_action_amd.workspace.checkpoint import load_optimizer_state_torch, optimizer_state_torch
-    pol = _policy()
-    opt = _opt(pol)
-    sd = optimizer_state_torch(opt, pol.model)
-    ref_model = _policy().model
-    groups = pol.add_weight_decay(ref_model, 0.02)  # same grouping rule as the reference (policy:326-342)
-    topt = torch.optim.AdamW(groups, lr=1e-4, betas=(0.9, 0.95))
-    for g in topt.param_groups:
-        g["initial_lr"] = g["lr"]
-    topt.load_state_dict(sd)
-    tsd = topt.state_dict()
-    assert [len(g["params"]) for g in tsd["param_groups"]] == [len(g["params"]) for g in sd["param_groups"]]
-    assert [g["weight_decay"] for g in tsd["param_groups"]] == [0.0, 0.02]
-    for i, s in sd["state"].items():
-        assert torch.equal(tsd["state"][i]["exp_avg"], s["exp_avg"])
-        assert float(tsd["state"][i]["step"]) == 7.0
-    # a state produced by torch itself (one real AdamW step) loads into ours
-    for p in ref_model.parameters():
-        p.grad = torch.randn_like(p)
-    topt.step()
+    pol = replay.golden_policy()
+    opt = _opt_with_state(pol)
+    sd = opt.state_dict()
+    ref = torch.optim.AdamW(pol.add_weight_decay(pol.model, 0.02), lr=1e-4, betas=(0.9, 0.95))
+    ref.load_state_dict(copy.deepcopy(sd))  # the reference workspace resumes from our optimizer state
+    for (n, p) in pol.model.named_parameters():
+        o, k = opt.store.offsets[id(p)]
+        assert torch.equal(ref.state[p]["exp_avg"].reshape(-1), opt.m[o:o + k]), n
     opt2 = pol.get_optimizer(weight_decay=0.02, learning_rate=1e-4, betas=(0.9, 0.95))
-    load_optimizer_state_torch(opt2, pol.model, topt.state_dict())
-    assert opt2.step_count == 8
-    back = optimizer_state_torch(opt2, pol.model)
-    for i, s in topt.state_dict()["state"].items():
-        assert torch.equal(back["state"][i]["exp_avg_sq"], s["exp_avg_sq"])
+    opt2.load_state_dict(ref.state_dict())  # and we resume from the reference's
+    assert torch.equal(_packed(opt2, opt2.m), _packed(opt, opt.m)) and torch.equal(_packed(opt2, opt2.v), _packed(opt, opt.v))
+    assert opt2.step_count == 7
 
 
-def test_checkpoint_pickles_refuse_globals(tmp_path, fp32):
-    from unified_video_action_amd.workspace.checkpoint import _loads_primitive
-    assert _loads_primitive(pickle.dumps(5)) == 5
+def _fake_omegaconf():
+    """stand-ins for omegaconf's container classes (omegaconf is not installed), pickled as
+    module "omegaconf.dictconfig" like the reference's cfg."""
+    mod = types.ModuleType("omegaconf")
+    sub = types.ModuleType("omegaconf.dictconfig")
+
+    class DictConfig:
+        def __init__(self, content):
+            self._content = content
+
+        def __getstate__(self):
+            return {"_content": self._content, "_metadata": None, "_parent": None}
+
+        def __setstate__(self, s):
+            self.__dict__.update(s)
+
+    DictConfig.__module__ = "omegaconf.dictconfig"
+    DictConfig.__qualname__ = "DictConfig"
+    sub.DictConfig = DictConfig
+    mod.dictconfig = sub
+    return mod, sub, DictConfig
+
+
+def test_reference_style_cfg_loads_without_executing(tmp_path, fp32):
+    from unified_video_action_amd.workspace.checkpoint import load_checkpoint, make_payload
+    pol = replay.golden_policy()
+    mod, sub, DictConfig = _fake_omegaconf()
+    sys.modules["omegaconf"], sys.modules["omegaconf.dictconfig"] = mod, sub
+    try:
+        payload = make_payload(pol, global_step=5, epoch=1)
+        payload["cfg"] = DictConfig({"name": "uva", "training": DictConfig({"seed": 42})})
+        path = tmp_path / "ref.ckpt"
+        torch.save(payload, path)
+    finally:
+        del sys.modules["omegaconf"], sys.modules["omegaconf.dictconfig"]
     with pytest.raises(pickle.UnpicklingError):
-        _loads_primitive(pickle.dumps(torch.float32))
+        torch.load(path, weights_only=True)  # what the previous loader did: the whole file refused
+    pol2 = replay.golden_policy()
+    meta = load_checkpoint(path, pol2)
+    assert meta["cfg"] == {"name": "uva", "training": {"seed": 42}} and meta["global_step"] == 5
+    assert "omegaconf" not in sys.modules
+
+
+class _Evil:
+    def __reduce__(self):
+        return (print, ("executed from a checkpoint",))
+
+
+def test_restricted_loader_refuses_other_globals(tmp_path):
+    from unified_video_action_amd.workspace.checkpoint import safe_load
+    path = tmp_path / "evil.ckpt"
+    torch.save({"state_dicts": {}, "cfg": _Evil()}, path)
+    with pytest.raises(pickle.UnpicklingError, match="refused"):
+        safe_load(path)
+
+
+@pytest.mark.parametrize("layout", ["mar", "uva"])
+def test_pretrained_warm_start(tmp_path, layout, fp32):
+    from unified_video_action_amd.model.autoregressive import mar_con_unified as pmar  # noqa: F401
+    src = replay.golden_policy()
+    with torch.no_grad():
+        for p in src.model.parameters():
+            p.add_(1.0)
+    sd = src.model.state_dict()
+    sd["z_proj.weight"] = torch.zeros(3, 3)  # shape mismatch: must keep its own init
+    sd["not_a_param"] = torch.ones(2)
+    path = tmp_path / f"{layout}.pth"
+    if layout == "mar":
+        torch.save({"model_ema": sd, "epoch": 3}, path)
+    else:
+        torch.save({"state_dicts": {"ema_model": {"model." + k: v for k, v in sd.items()}}}, path)
+    pol = replay.golden_policy()
+    init = {k: v.clone() for k, v in pol.model.state_dict().items()}
+    pol.pretrained_model_path = str(path)
+    rep = pol.load_pretrained_model()
+    got = pol.model.state_dict()
+    assert torch.equal(got["z_proj.weight"], init["z_proj.weight"])
+    assert "z_proj.weight" in rep["kept_init"]
+    for k in got:
+        if k != "z_proj.weight":
+            assert torch.equal(got[k], sd[k]), k

@@ -1,6 +1,10 @@
-"""Data-parallel reducer on CPU with torch.distributed gloo, world_size 2: bucket layout of
-the flat gradient buffer, async per-bucket launches + tail bucket, 1/world averaging, and
-equality with a single-process run on the concatenated batch."""
+"""Data-parallel reducer on the CPU with torch.distributed gloo, world_size 2:
+  * the real policy (mar_base, PushT joint, fp32): get_optimizer's flat layout + default_buckets
+    cover every trainable parameter exactly once (buckets + tail), every Block / diffusion trunk
+    carries its bucket hook, and the reducer is created lazily once the process group exists;
+  * the reducer protocol on a small torch model: async per-bucket launches from backward, the
+    end-of-backward completion callback, the tail bucket, 1/world averaging -- equal to a
+    single-process run on the concatenated batch."""
 import os
 import socket
 
@@ -29,11 +33,32 @@ class Tiny(nn.Module):
     def forward(self, x):
         h = self.embed(x)
         for b in self.blocks:
-            h = h + b(h)
+            h = h + _Hook.apply(b(h), b)
         return self.head(h).square().mean()
 
 
-def _worker(rank, world, port, q):
+class _Hook(torch.autograd.Function):
+    """stands in for BlockFn's backward, which calls the bucket hook after its grads are enqueued."""
+
+    @staticmethod
+    def forward(ctx, x, mod):
+        ctx.mod = mod
+        return x.view_as(x)
+
+    @staticmethod
+    def backward(ctx, g):
+        hook = getattr(ctx.mod, "_uva_bucket_hook", None)
+        ctx.mod._pending_hook = hook  # fire once the module's own parameter grads exist (next step)
+        return g, None
+
+
+def _named_groups(m):
+    from unified_video_action_amd.workspace.optim import is_no_decay
+    named = [(n, p) for n, p in m.named_parameters()]
+    return [[x for x in named if is_no_decay(*x)], [x for x in named if not is_no_decay(*x)]]
+
+
+def _tiny_worker(rank, world, port, q):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     from unified_video_action_amd.runtime import RT
@@ -41,16 +66,26 @@ def _worker(rank, world, port, q):
     RT.set_precision("fp32")
     torch.manual_seed(0)
     m = Tiny()
-    store = ParamStore(m)
+    store = ParamStore(_named_groups(m))
     red = GradReducer(store, [(b, b) for b in m.blocks])
     assert len(red.buckets) == 3 and all(len(r) <= 2 for r in red.buckets)
+    assert int(red.coverage().min()) == 1 and int(red.coverage().max()) == 1
     g = torch.Generator().manual_seed(123)
     x = torch.randn(8, 4, generator=g)[rank * 4:(rank + 1) * 4]
-    loss = m(x)
-    loss.backward()
-    for i in reversed(range(3)):  # what the fused Block backward hooks do, in backward order
-        m.blocks[i]._uva_bucket_hook()
-    red.finish()
+    red.arm()
+
+    # launch each block's bucket from inside backward, after its parameter grads are accumulated
+    def post_hook(mod):
+        def fn(*_):
+            if getattr(mod, "_pending_hook", None) is not None:
+                mod._pending_hook()
+        return fn
+
+    handles = [b[0].weight.register_post_accumulate_grad_hook(post_hook(b)) for b in m.blocks]
+    m(x).backward()  # the queued end-of-backward callback completes the reduction
+    assert not red.pending and not red.handles
+    for h in handles:
+        h.remove()
     q.put((rank, (store.grad / world).clone()))
     dist.destroy_process_group()
 
@@ -60,23 +95,69 @@ def test_grad_reducer_world2_matches_single_process():
     world, port = 2, _free_port()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    procs = [ctx.Process(target=_tiny_worker, args=(r, world, port, q)) for r in range(world)]
     for p in procs:
         p.start()
     res = dict(q.get(timeout=100) for _ in range(world))
     for p in procs:
         p.join(timeout=30)
     assert torch.allclose(res[0], res[1])
-    # single process on the full batch = mean of the two half-batch gradients
     from unified_video_action_amd.runtime import RT
     from unified_video_action_amd.workspace.optim import ParamStore
     RT.set_precision("fp32")
     torch.manual_seed(0)
     m = Tiny()
-    store = ParamStore(m)
+    store = ParamStore(_named_groups(m))
     g = torch.Generator().manual_seed(123)
     x = torch.randn(8, 4, generator=g)
     m(x[:4]).backward()
     m(x[4:]).backward()
     RT.set_precision("bf16")
     assert torch.allclose(res[0], store.grad / 2, atol=1e-6)
+
+
+def _policy_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.set_num_threads(2)
+    from unified_video_action_amd import presets
+    from unified_video_action_amd.model.autoregressive.diffusion_loss import SimpleMLPAdaLN
+    from unified_video_action_amd.model.autoregressive.mar_con_unified import Block
+    from unified_video_action_amd.policy.unified_video_action_policy import UnifiedVideoActionPolicy
+    from unified_video_action_amd.runtime import RT
+    RT.set_precision("fp32")
+    torch.manual_seed(0)
+    pol = UnifiedVideoActionPolicy(**presets.policy_kwargs("pusht_joint"))
+    opt = pol.get_optimizer(weight_decay=0.02, learning_rate=1e-4, betas=(0.9, 0.95))
+    assert opt.maybe_init_reducer(pol.model) is None  # no process group yet (accelerate order)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    red = opt.maybe_init_reducer(pol.model)
+    cov = red.coverage()
+    st = opt.store
+    inside = torch.zeros(st.total, dtype=torch.bool)
+    for _, p in st.order:
+        o, k = st.offsets[id(p)]
+        inside[o:o + k] = True
+    n_trainable = sum(p.numel() for p in pol.model.parameters() if p.requires_grad)
+    hooked = [m for m in pol.model.modules() if isinstance(m, (Block, SimpleMLPAdaLN))]
+    q.put((rank, int(cov[inside].min()), int(cov[inside].max()), int(cov.max()), st.n_params, n_trainable,
+           len(hooked), sum(callable(getattr(m, "_uva_bucket_hook", None)) for m in hooked), opt.grad_scale,
+           len(red.buckets)))
+    dist.destroy_process_group()
+
+
+@pytest.mark.timeout(300)
+def test_mar_base_buckets_cover_every_param_once():
+    world, port = 2, _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_policy_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=280) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=30)
+    for rank, cmin, cmax, call, n_store, n_train, n_hooked, n_with_hook, scale, n_buckets in res:
+        assert cmin == 1 and cmax == 1 and call == 1, (cmin, cmax, call)
+        assert n_store == n_train == 261_079_156, n_store  # PushT joint MAR
+        assert n_hooked == 26 and n_with_hook == 26 and n_buckets == 26  # 24 Blocks + 2 diffusion trunks
+        assert scale == 0.5

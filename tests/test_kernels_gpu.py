@@ -307,10 +307,13 @@ def test_timestep_features():
 
 
 def test_adamw_ema_matches_torch():
+    """one launch per param group region (16-B aligned; n = 6001 exercises the scalar tail),
+    1/world gradient scaling, fused EMA, bf16 shadow; plus the standalone EMA kernel."""
     from unified_video_action_amd.native import ops
-    n, n_decay = 10000, 6000
+    n_a, n_b, off_b = 6001, 3999, 6016
+    n = off_b + n_b
     p0 = torch.randn(n, device=DEV)
-    pa, pb = p0[:n_decay].clone(), p0[n_decay:].clone()
+    pa, pb = p0[:n_a].clone(), p0[off_b:].clone()
     opt = torch.optim.AdamW([{"params": [pa], "weight_decay": 0.02},
                              {"params": [pb], "weight_decay": 0.0}], lr=1e-3, betas=(0.9, 0.95))
     p = p0.clone()
@@ -319,15 +322,27 @@ def test_adamw_ema_matches_torch():
     ema = p0.clone()
     pbf = torch.empty(n, device=DEV, dtype=torch.bfloat16)
     ema_ref = p0.clone()
+    regions = ((0, n_a, 0.02), (off_b, n_b, 0.0))
     for step in range(1, 4):
         g = torch.randn(n, device=DEV)
-        pa.grad, pb.grad = g[:n_decay].clone(), g[n_decay:].clone()
+        pa.grad, pb.grad = g[:n_a].clone(), g[off_b:].clone()
         opt.step()
-        ops.adamw_ema(p, g * 2.0, m, v, ema, pbf, n_decay, 1e-3, 0.9, 0.95, 1e-8, 0.02, step, 0.5, 0.7)
-        ema_ref = ema_ref * 0.7 + torch.cat([pa, pb]).detach() * 0.3
-        assert rel_err(p, torch.cat([pa, pb]).detach()) < 1e-6
-    assert rel_err(ema, ema_ref) < 1e-6
-    assert torch.equal(pbf, p.to(torch.bfloat16))
+        for o, k, wd in regions:
+            sl = slice(o, o + k)
+            ops.adamw_ema(p[sl], (g * 2.0)[sl], m[sl], v[sl], ema[sl], pbf[sl], k if wd else 0, 1e-3, 0.9, 0.95,
+                          1e-8, wd, step, 0.5, 0.7)
+        ref = torch.cat([pa, p0[n_a:off_b], pb]).detach()
+        ema_ref = ema_ref * 0.7 + ref * 0.3
+        for o, k, _ in regions:
+            assert rel_err(p[o:o + k], ref[o:o + k]) < 1e-6
+    for o, k, _ in regions:
+        assert rel_err(ema[o:o + k], ema_ref[o:o + k]) < 1e-6
+        assert torch.equal(pbf[o:o + k], p[o:o + k].to(torch.bfloat16))
+    e2 = ema.clone()
+    ops.ema_update(e2, p, 0.25)
+    assert rel_err(e2, ema * 0.25 + p * 0.75) < 1e-6
+    with pytest.raises(RuntimeError):  # misaligned region
+        ops.adamw_ema(p[1:5], g[1:5], m[1:5], v[1:5], None, None, 4, 1e-3, 0.9, 0.95, 1e-8, 0.0, 1, 1.0, 0.0)
 
 
 @pytest.mark.parametrize("rows,cols", [(64, 3072), (1000, 768)])

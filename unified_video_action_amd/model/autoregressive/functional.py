@@ -37,12 +37,14 @@ def compute_weight(p):
     if cdt() == F32:
         return p.detach()
     sh = getattr(p, "_uva_shadow", None)
-    if sh is not None and getattr(p, "_uva_shadow_static", False):
-        return sh
-    if sh is None or getattr(p, "_uva_shadow_ver", None) != p._version:
+    if sh is not None and getattr(p, "_uva_shadow_owner", None) == id(p):
+        return sh  # a view of the ParamStore's bf16 buffer, refreshed by the optimizer kernel
+    # parameters rewritten by HIP kernels (an EMA model) do not bump _version: key on RT's generation
+    key = (p._version, p.data_ptr(), RT.param_gen if getattr(p, "_uva_raw_updated", False) else 0)
+    if sh is None or getattr(p, "_uva_shadow_ver", None) != key:
         sh = as_dtype(p.detach(), cdt())
         p._uva_shadow = sh
-        p._uva_shadow_ver = p._version
+        p._uva_shadow_ver = key
     return sh
 
 

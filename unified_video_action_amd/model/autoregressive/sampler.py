@@ -23,7 +23,7 @@ import os
 import torch
 
 from ...native import ops
-from ...runtime import cdt
+from ...runtime import RT, cdt
 from .diffusion import SamplingSchedule, timestep_freqs
 from .functional import F32, compute_weight
 
@@ -54,6 +54,16 @@ class ActionSampler:
         # LN inside fc1's A staging: every 64-column block re-normalises its 32 rows (16x redundant
         # at width 1024), measured slower than the separate LN kernel (B=32: 27.8 vs 26.0 ms / loop)
         self.fuse_ln = os.environ.get("UVA_SAMPLER_FUSE_LN", "0") == "1"
+
+    def __deepcopy__(self, memo):
+        """copies (the reference's deepcopy'd EMA policy) start without the cached buffers / graph."""
+        import copy
+        new = ActionSampler.__new__(ActionSampler)
+        memo[id(self)] = new
+        for k, v in self.__dict__.items():
+            if k != "_cache":
+                new.__dict__[k] = copy.deepcopy(v, memo)
+        return new
 
     # ---- hoisted conditioning -------------------------------------------------------------
     def _weights(self):
@@ -149,7 +159,9 @@ class ActionSampler:
         """Persistent step buffers (+ captured graph) per (rows, channels, dtype, weights)."""
         net = self.net
         cd = cdt()
-        sig = (R, C, str(cd), float(temperature), str(dev), self.use_fused,
+        # RT.param_gen: the optimizer / EMA kernels rewrite weights without bumping _version, and the
+        # captured graph and the concatenated modulation weights (wcat / bcat) must follow them
+        sig = (R, C, str(cd), float(temperature), str(dev), self.use_fused, RT.param_gen,
                tuple((p.data_ptr(), p._version) for p in net.parameters()))
         cache = getattr(self, "_cache", None)
         if cache is not None and cache["sig"] == sig:

@@ -315,6 +315,13 @@ def adamw_ema(p, g, m, v, ema, p_bf16, n_decay, lr, b1, b2, eps, wd, step, grad_
                float(ema_decay), stream())
 
 
+def ema_update(ema, p, decay):
+    """ema = decay * ema + (1 - decay) * p over two flat fp32 buffers (uva_ema_update)."""
+    if ema.dtype != torch.float32 or p.dtype != torch.float32 or ema.numel() != p.numel():
+        raise ValueError("ema_update: two fp32 buffers of equal size")
+    lib().call("uva_ema_update", ptr(ema), ptr(p), ema.numel(), float(decay), stream())
+
+
 def attn_mask_alloc(B, N, H, device):
     return torch.empty(lib().query("uva_attn_mask_bytes", B, N, H), dtype=torch.uint8, device=device)
 

@@ -14,8 +14,19 @@ VAE encoder, MAR, diffusion heads, backward).  Inference: predict_action(obs_dic
 Differences that do not change results: frames are selected before the bilinear resize
 (per-frame op), and the "loss += 0*p.sum()" DDP workaround (policy:421-423) is replaced
 by the zero-initialised flat gradient buffer that the DP reducer all-reduces whole.
+
+Data parallel under the reference's launcher (`accelerate launch`, workspace:208-220): the
+fused backward writes parameter gradients straight into the optimizer's flat buffer, which
+DDP's autograd hooks never see.  The policy therefore lists every parameter in
+`_ddp_params_and_buffers_to_ignore` (DDP skips them: no broadcast hooks, no reducer buckets)
+except one zero-valued `ddp_anchor` scalar that DDP reduces instead (it enters the loss as
+0 * anchor, and is dropped from state dicts), and the optimizer's own RCCL bucket reducer
+(workspace/optim.GradReducer, created on the first forward after the process group exists)
+all-reduces the flat gradients from inside backward.
 """
+import os
 import random
+import weakref
 
 import numpy as np
 import torch
@@ -45,6 +56,20 @@ def _plain(cfg):
     if hasattr(cfg, "items"):
         return {k: _plain(v) for k, v in cfg.items()}
     return cfg
+
+
+def _drop_anchor(module, state_dict, prefix, local_metadata):
+    state_dict.pop(prefix + "ddp_anchor", None)
+    return state_dict
+
+
+def _add_anchor(module, state_dict, prefix, local_metadata, strict, missing_keys, unexpected_keys, error_msgs):
+    state_dict.setdefault(prefix + "ddp_anchor", torch.zeros((), device=module.ddp_anchor.device))
+
+
+def _ddp_active():
+    import torch.distributed as dist
+    return dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1
 
 
 class UnifiedVideoActionPolicy(nn.Module):
@@ -95,6 +120,18 @@ class UnifiedVideoActionPolicy(nn.Module):
             predict_proprioception=kwargs.get("predict_proprioception") or False, task_name=self.task_name,
             language_emb_model=language_emb_model, shape_meta=shape_meta)
         self.normalizer = LinearNormalizer()
+        # DDP anchor (see module docstring); not part of state dicts
+        self.ddp_anchor = nn.Parameter(torch.zeros(()))
+        self._register_state_dict_hook(_drop_anchor)
+        self._register_load_state_dict_pre_hook(_add_anchor, with_module=True)
+        self._uva_opt = None
+        # warm start (policy:112-118): a MAR checkpoint's model_ema or a UVA .ckpt's ema_model
+        self.pretrained_model_path = _get(ap, "pretrained_model_path", None)
+        if self.pretrained_model_path is not None:
+            if os.path.exists(self.pretrained_model_path):
+                self.load_pretrained_model()
+            else:
+                print("pretrained model not found: ", self.pretrained_model_path)
         if self.selected_training_mode is None:
             if len(self.task_modes) == 0:
                 self.task_modes = list(ALL_TASK_MODES)
@@ -120,8 +157,59 @@ class UnifiedVideoActionPolicy(nn.Module):
         return [{"params": no_decay, "weight_decay": 0.0}, {"params": decay, "weight_decay": weight_decay}]
 
     def get_optimizer(self, weight_decay, learning_rate, betas):
+        """policy:343-360: AdamW over (no-decay, decay) groups of self.model, initial_lr set --
+        as the flat-buffer FusedAdamWEMA (a torch.optim.Optimizer)."""
         from ..workspace.optim import FusedAdamWEMA
-        return FusedAdamWEMA(self.model, lr=learning_rate, betas=tuple(betas), weight_decay=weight_decay)
+        groups = self.add_weight_decay(self.model, weight_decay=weight_decay)
+        opt = FusedAdamWEMA(groups, lr=learning_rate, betas=tuple(betas), named=list(self.model.named_parameters()),
+                            prefix="model.")
+        for g in opt.param_groups:
+            g.setdefault("initial_lr", g["lr"])
+        self._uva_opt = (weakref.ref(opt), id(self))  # a deepcopy (the EMA policy) does not inherit it
+        return opt
+
+    def bound_optimizer(self):
+        """the flat-buffer optimizer built by this policy's get_optimizer (None otherwise)."""
+        if self._uva_opt is None or self._uva_opt[1] != id(self):
+            return None
+        return self._uva_opt[0]()
+
+    def _apply(self, fn, *args, **kwargs):
+        out = super()._apply(fn, *args, **kwargs)
+        opt = self.bound_optimizer()
+        if opt is not None:
+            opt._sync()  # .to(device) replaced the parameter tensors: re-bind the flat buffers
+        return out
+
+    @property
+    def _ddp_params_and_buffers_to_ignore(self):
+        return [n for n, _ in self.named_parameters() if n != "ddp_anchor"] + [n for n, _ in self.named_buffers()]
+
+    def load_pretrained_model(self):
+        """policy:140-218: name- and shape-filtered load into self.model from a UVA checkpoint's
+        state_dicts.ema_model ("model." prefix stripped) or a MAR checkpoint's model_ema.  Read with
+        the checkpoint module's safe loader (no code executes from the file)."""
+        from ..workspace.checkpoint import safe_load
+        ck = safe_load(self.pretrained_model_path)
+        if "state_dicts" in ck:
+            if "ema_model" not in ck["state_dicts"]:
+                raise NotImplementedError("UVA checkpoint without state_dicts.ema_model")
+            src = {k[6:]: v for k, v in ck["state_dicts"]["ema_model"].items() if k.startswith("model.")}
+        elif "model_ema" in ck:
+            src = ck["model_ema"]
+        else:
+            raise NotImplementedError("pretrained checkpoint has neither state_dicts.ema_model nor model_ema")
+        sd = self.model.state_dict()
+        take = {k: v for k, v in src.items() if k in sd and sd[k].size() == v.size()}
+        skipped = [k for k, v in sd.items() if k not in src or src[k].size() != v.size()]
+        if not sd or not take:
+            raise ValueError(f"pretrained checkpoint {self.pretrained_model_path}: no matching parameters")
+        sd.update(take)
+        missing, unexpected = self.model.load_state_dict(sd, strict=False)
+        RT.bump_params()
+        self.pretrained_report = {"loaded": sorted(take), "kept_init": skipped, "missing": list(missing),
+                                  "unexpected": list(unexpected)}
+        return self.pretrained_report
 
     def _normalize(self, key, x):
         if self.normalizer_type == "all" and key in self.normalizer:
@@ -143,6 +231,16 @@ class UnifiedVideoActionPolicy(nn.Module):
                 raise NotImplementedError("CLIP text encoding needs network weights; pass language_latents")
             text_latents = batch["language_latents"]
         nactions = self._normalize("action", batch["action"].float())
+        if self.normalizer_type == "all":  # normalize_obs: every non-image key (policy:389-393)
+            obs = dict(obs)
+            for k in list(obs):
+                if "image" not in k and k in self.normalizer:
+                    obs[k] = self.normalizer[k].normalize(obs[k])
+        opt = self.bound_optimizer()
+        if opt is not None and self.training:
+            red = opt.maybe_init_reducer(self.model)
+            if red is not None:
+                red.arm()
         indices, prop = None, {}
         if "umi" in self.task_name:
             sel = np.arange(T)
@@ -170,6 +268,8 @@ class UnifiedVideoActionPolicy(nn.Module):
         mode = rng.get("task_mode") or random.choice(self.task_modes)
         loss, video_loss, act_loss = self.model(z, c, None, trajectory, text_latents, task_mode=mode,
                                                 proprioception_input=prop, rng=rng)
+        if torch.is_grad_enabled() and _ddp_active():
+            loss = loss + 0.0 * self.ddp_anchor  # the one parameter DDP reduces (see module docstring)
         return loss, (video_loss, act_loss)
 
     def forward(self, batch, **kwargs):

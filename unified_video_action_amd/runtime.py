@@ -26,6 +26,9 @@ class _Runtime:
         self._attn_shapes = {}
         self._attn_ready = {}
         self._side = None
+        # bumped whenever HIP kernels rewrite parameters in place (optimizer / EMA steps): caches
+        # keyed on parameters (non-static compute shadows, the sampler's captured graphs) compare it
+        self.param_gen = 0
 
     def set_precision(self, name):
         name = str(name).lower()
@@ -37,6 +40,9 @@ class _Runtime:
             self.compute_dtype = torch.bfloat16
         else:
             raise ValueError(f"unknown precision {name}")
+
+    def bump_params(self):
+        self.param_gen += 1
 
     def seed(self, base):
         self._seed_base = int(base)

@@ -2,26 +2,103 @@
 
 Reference: BaseWorkspace.save_checkpoint / load_payload (workspace/base_workspace.py:33-135):
     torch.save({"cfg": cfg, "state_dicts": {"model", "ema_model", "optimizer", "lr_scheduler"},
-                "pickles": {"global_step": dill bytes, "epoch": dill bytes}}, path)
+                "pickles": {"global_step": dill bytes, "epoch": dill bytes, ...}}, path)
 with "model" / "ema_model" = UnifiedVideoActionPolicy.state_dict() (vae_model.*, model.*,
 normalizer.*), "optimizer" = torch.optim.AdamW.state_dict() over the two groups of
 policy.get_optimizer (no-decay first, then decay; policy:326-360) and "lr_scheduler" = the
-diffusers LambdaLR state.
+LambdaLR state.  The build's FusedAdamWEMA produces / consumes that AdamW layout itself, the
+EMA policy is an ordinary module (its parameters are views of the EMA flat buffer), and the
+schedulers are torch LambdaLRs, so the payload is built from plain `state_dict()`s both ways.
 
-The build's optimizer keeps flat fp32 m / v / EMA buffers (workspace/optim.py); this module
-converts them to and from that per-parameter layout, so a run can resume from a reference
-checkpoint and the reference workspace can resume from ours.  Files are read with
-`torch.load(weights_only=True)`; the two `pickles` entries are decoded by an unpickler that
-admits no globals at all (plain ints / floats / strings only), so nothing from a checkpoint
-executes code.  `cfg` is written as a plain dict (the reference writes an OmegaConf object,
-which a weights-only load refuses; it is then skipped).
+Loading never executes code from a file (`safe_load`):
+  1. torch.load(weights_only=True);
+  2. if that refuses the file because of non-tensor globals -- the reference stores its
+     OmegaConf `cfg` (base_workspace.py:52), a MAR checkpoint its argparse `args` -- a
+     restricted unpickler: torch's own weights-only allowlist, plus inert stand-in classes for
+     globals of the configuration modules (omegaconf / hydra / argparse / typing / pathlib),
+     which only record the state they are given.  Every other global is refused.  The
+     stand-in cfg is converted to plain Python containers where its layout is recognised.
+The `pickles` entries (dill / pickle bytes of ints) are decoded with no globals admitted.
 """
 import io
 import pickle
+import types
 
 import torch
 
-from .optim import is_no_decay
+STUB_ROOTS = ("omegaconf", "hydra", "argparse", "typing", "pathlib", "enum")
+_STUBS = {}
+
+
+class _Inert:
+    """Stand-in for a configuration-module global: records args / state, runs nothing."""
+
+    def __new__(cls, *args, **kwargs):
+        obj = object.__new__(cls)
+        obj._args = args
+        obj._state = None
+        return obj
+
+    def __init__(self, *args, **kwargs):
+        pass
+
+    def __setstate__(self, state):
+        self._state = state
+
+    def __repr__(self):
+        return f"<inert {type(self).__module__}.{type(self).__qualname__}>"
+
+
+def _stub(module, name):
+    key = (module, name)
+    if key not in _STUBS:
+        _STUBS[key] = type(name, (_Inert,), {"__module__": module, "__qualname__": name})
+    return _STUBS[key]
+
+
+def _restricted_pickle_module():
+    from torch import _weights_only_unpickler as W
+    allowed = W._get_allowed_globals()
+
+    class Unpickler(pickle.Unpickler):
+        def find_class(self, module, name):
+            key = f"{module}.{name}"
+            if key in allowed:
+                return allowed[key]
+            if module.split(".")[0] in STUB_ROOTS:
+                return _stub(module, name)
+            raise pickle.UnpicklingError(f"checkpoint global {key} refused (only tensors, containers and "
+                                         f"configuration objects are loaded)")
+
+    mod = types.ModuleType("uva_restricted_pickle")
+    mod.Unpickler = Unpickler
+    mod.load = lambda f, **kw: Unpickler(f, **kw).load()
+    mod.__name__ = "uva_restricted_pickle"
+    return mod
+
+
+def to_plain(obj):
+    """best-effort: OmegaConf DictConfig / ListConfig / value-node stand-ins -> dict / list / value."""
+    if isinstance(obj, _Inert):
+        st = obj._state if isinstance(obj._state, dict) else {}
+        if "_content" in st:
+            return to_plain(st["_content"])
+        if "_val" in st:
+            return to_plain(st["_val"])
+        return None
+    if isinstance(obj, dict):
+        return {k: to_plain(v) for k, v in obj.items()}
+    if isinstance(obj, (list, tuple)):
+        return [to_plain(v) for v in obj]
+    return obj
+
+
+def safe_load(path, map_location="cpu"):
+    try:
+        return torch.load(path, map_location=map_location, weights_only=True)
+    except pickle.UnpicklingError:
+        pass
+    return torch.load(path, map_location=map_location, weights_only=False, pickle_module=_restricted_pickle_module())
 
 
 class _PrimitiveUnpickler(pickle.Unpickler):
@@ -33,136 +110,73 @@ def _loads_primitive(b):
     return _PrimitiveUnpickler(io.BytesIO(b)).load()
 
 
-def _strip_module(sd):
+def strip_module(sd):
     """DDP / accelerate prefixes, as load_payload does (base_workspace.py:94-100)."""
     return {k.replace("module.", ""): v for k, v in sd.items()}
 
 
-def _trainable(model):
-    return [(n, p) for n, p in model.named_parameters() if p.requires_grad]
+def _cpu(x):
+    """base_workspace._copy_to_cpu."""
+    if torch.is_tensor(x):
+        return x.detach().to("cpu").clone()
+    if isinstance(x, dict):
+        return {k: _cpu(v) for k, v in x.items()}
+    if isinstance(x, (list, tuple)):
+        return type(x)(_cpu(v) for v in x)
+    return x
 
 
-def _groups(model):
-    """(no_decay, decay) name lists in named_parameters order (policy.add_weight_decay)."""
-    tr = _trainable(model)
-    return [n for n, p in tr if is_no_decay(n, p)], [n for n, p in tr if not is_no_decay(n, p)]
-
-
-def optimizer_state_torch(opt, model):
-    """FusedAdamWEMA -> torch.optim.AdamW.state_dict() layout (CPU tensors)."""
-    st = opt.store
-    params = dict(_trainable(model))
-    nod, dec = _groups(model)
-    g = opt.param_groups[0]
-    state, groups, idx = {}, [], 0
-    for names, wd in ((nod, 0.0), (dec, g["weight_decay"])):
-        ids = []
-        for n in names:
-            o, k = st.offsets[id(params[n])]
-            if opt.step_count > 0:
-                shp = params[n].shape
-                state[idx] = {"step": torch.tensor(float(opt.step_count)),
-                              "exp_avg": opt.m[o:o + k].detach().reshape(shp).cpu().clone(),
-                              "exp_avg_sq": opt.v[o:o + k].detach().reshape(shp).cpu().clone()}
-            ids.append(idx)
-            idx += 1
-        groups.append({"lr": g["lr"], "betas": tuple(g["betas"]), "eps": g["eps"], "weight_decay": wd,
-                       "amsgrad": False, "foreach": None, "maximize": False, "capturable": False,
-                       "differentiable": False, "fused": None, "initial_lr": g.get("initial_lr", g["lr"]),
-                       "params": ids})
-    return {"state": state, "param_groups": groups}
-
-
-def load_optimizer_state_torch(opt, model, sd):
-    """torch.optim.AdamW.state_dict() (two groups, policy.get_optimizer order) -> FusedAdamWEMA."""
-    st = opt.store
-    params = dict(_trainable(model))
-    nod, dec = _groups(model)
-    groups = sd["param_groups"]
-    if len(groups) != 2 or len(groups[0]["params"]) != len(nod) or len(groups[1]["params"]) != len(dec):
-        raise ValueError("optimizer state does not match policy.get_optimizer's (no-decay, decay) groups")
-    steps = set()
-    for names, grp in ((nod, groups[0]), (dec, groups[1])):
-        for n, pid in zip(names, grp["params"]):
-            s = sd["state"].get(pid, sd["state"].get(str(pid)))
-            if s is None:
-                continue
-            o, k = st.offsets[id(params[n])]
-            if s["exp_avg"].numel() != k:
-                raise ValueError(f"optimizer state of {n}: {s['exp_avg'].numel()} values, parameter has {k}")
-            opt.m[o:o + k].copy_(s["exp_avg"].reshape(-1))
-            opt.v[o:o + k].copy_(s["exp_avg_sq"].reshape(-1))
-            steps.add(int(float(s["step"])))
-    if len(steps) > 1:
-        raise ValueError(f"per-parameter step counts differ: {sorted(steps)}")
-    opt.step_count = steps.pop() if steps else 0
-    g = groups[1]
-    opt.param_groups[0].update(lr=g["lr"], betas=tuple(g["betas"]), eps=g["eps"], weight_decay=g["weight_decay"],
-                               initial_lr=g.get("initial_lr", g["lr"]))
-
-
-def lr_scheduler_state(sched):
-    """diffusers LambdaLR.state_dict() fields (lr_lambdas are not stored by torch for plain functions)."""
-    return {"base_lrs": list(sched.base) * 2, "last_epoch": sched.last_epoch, "_step_count": sched.last_epoch + 1,
-            "verbose": False, "_get_lr_called_within_step": False,
-            "_last_lr": sched.get_last_lr() * 2, "lr_lambdas": [None, None]}
-
-
-def load_lr_scheduler_state(sched, sd):
-    sched.last_epoch = int(sd["last_epoch"]) - 1
-    sched.step()
-
-
-def ema_policy_state(policy, opt):
-    """The EMA copy of the whole policy (the reference EMAs a deepcopy of the policy; frozen VAE and
-    normaliser entries equal the live ones)."""
-    sd = {k: v.detach().cpu().clone() for k, v in policy.state_dict().items()}
-    if opt is not None and opt.ema is not None:
-        for n, t in opt.ema_state().items():
-            sd["model." + n] = t.detach().cpu().clone()
-    return sd
-
-
-def make_payload(policy, optimizer=None, lr_scheduler=None, global_step=0, epoch=0, cfg=None):
-    sds = {"model": {k: v.detach().cpu().clone() for k, v in policy.state_dict().items()}}
+def make_payload(model, ema_model=None, optimizer=None, lr_scheduler=None, cfg=None, **pickles):
+    sds = {"model": _cpu(model.state_dict())}
+    if ema_model is not None:
+        sds["ema_model"] = _cpu(ema_model.state_dict())
     if optimizer is not None:
-        if optimizer.ema is not None:
-            sds["ema_model"] = ema_policy_state(policy, optimizer)
-        sds["optimizer"] = optimizer_state_torch(optimizer, policy.model)
+        sds["optimizer"] = _cpu(optimizer.state_dict())
     if lr_scheduler is not None:
-        sds["lr_scheduler"] = lr_scheduler_state(lr_scheduler)
-    return {"cfg": cfg, "state_dicts": sds,
-            "pickles": {"global_step": pickle.dumps(int(global_step)), "epoch": pickle.dumps(int(epoch))}}
+        sds["lr_scheduler"] = _cpu(lr_scheduler.state_dict())
+    return {"cfg": _plain_cfg(cfg), "state_dicts": sds,
+            "pickles": {k: pickle.dumps(v) for k, v in pickles.items()}}
 
 
-def save_checkpoint(path, policy, optimizer=None, lr_scheduler=None, global_step=0, epoch=0, cfg=None):
-    torch.save(make_payload(policy, optimizer, lr_scheduler, global_step, epoch, cfg), path)
+def _plain_cfg(cfg):
+    if cfg is None or isinstance(cfg, (int, float, str, bool)):
+        return cfg
+    if hasattr(cfg, "items"):
+        return {k: _plain_cfg(v) for k, v in cfg.items()}
+    if isinstance(cfg, (list, tuple)):
+        return [_plain_cfg(v) for v in cfg]
+    return str(cfg)
+
+
+def save_checkpoint(path, model, ema_model=None, optimizer=None, lr_scheduler=None, cfg=None, **pickles):
+    torch.save(make_payload(model, ema_model, optimizer, lr_scheduler, cfg, **pickles), path)
     return str(path)
 
 
-def load_checkpoint(path, policy, optimizer=None, lr_scheduler=None, use_ema_weights=False):
-    """-> {"global_step", "epoch", "cfg"}.  Restores policy (or its EMA weights), optimizer m/v/step
-    and the LR schedule position."""
-    payload = torch.load(path, map_location="cpu", weights_only=True)
+def load_payload(payload, model, ema_model=None, optimizer=None, lr_scheduler=None):
+    """BaseWorkspace.load_payload (base_workspace.py:86-120): every present state dict into its
+    object ("module." stripped), the EMA weights into the model when "model" is absent.
+    -> {"cfg", pickles...}."""
     sds = payload["state_dicts"]
-    key = "ema_model" if (use_ema_weights or "model" not in sds) else "model"
-    policy.load_state_dict(_strip_module(sds[key]))
-    if optimizer is not None:
-        if optimizer.store.shadow is not None:
-            optimizer.store.refresh_shadow()
-        if "optimizer" in sds:
-            load_optimizer_state_torch(optimizer, policy.model, _strip_module(sds["optimizer"]))
-        if optimizer.ema is not None and "ema_model" in sds:
-            ema = _strip_module(sds["ema_model"])
-            st = optimizer.store
-            for n, p in st.order:
-                o, k = st.offsets[id(p)]
-                optimizer.ema[o:o + k].copy_(ema["model." + n].reshape(-1))
-            optimizer.ema_step_count = optimizer.step_count
+    if "model" in sds:
+        model.load_state_dict(strip_module(sds["model"]))
+    elif "ema_model" in sds:
+        model.load_state_dict(strip_module(sds["ema_model"]))
+    if ema_model is not None and "ema_model" in sds:
+        ema_model.load_state_dict(strip_module(sds["ema_model"]))
+    if optimizer is not None and "optimizer" in sds:
+        osd = sds["optimizer"]
+        if "base_optimizer_state" not in osd:  # DeepSpeed layout is skipped, as the reference does
+            optimizer.load_state_dict(osd)
     if lr_scheduler is not None and "lr_scheduler" in sds:
-        load_lr_scheduler_state(lr_scheduler, sds["lr_scheduler"])
-    pk = payload.get("pickles", {})
-    out = {"cfg": payload.get("cfg")}
-    for k in ("global_step", "epoch"):
-        out[k] = _loads_primitive(pk[k]) if k in pk else 0
+        lr_scheduler.load_state_dict(sds["lr_scheduler"])
+    from ..runtime import RT
+    RT.bump_params()
+    out = {"cfg": to_plain(payload.get("cfg"))}
+    for k, b in payload.get("pickles", {}).items():
+        out[k] = _loads_primitive(b)
     return out
+
+
+def load_checkpoint(path, model, ema_model=None, optimizer=None, lr_scheduler=None):
+    return load_payload(safe_load(path), model, ema_model, optimizer, lr_scheduler)

@@ -1,61 +1,116 @@
-"""Flat parameter store, fused AdamW+EMA optimizer and the data-parallel gradient reducer.
+"""Flat parameter store, fused AdamW(+EMA) optimizer and the data-parallel gradient reducer.
 
-ParamStore: every trainable parameter becomes a view of ONE fp32 buffer (decay group
-first, then the no-decay group -- policy:326-341 split), every `.grad` a view of ONE
+ParamStore: every trainable parameter becomes a view of ONE fp32 buffer, laid out group by
+group in the optimizer's param_groups order (policy.add_weight_decay: no-decay group, then the
+decay group -- policy:326-341), each group region 256-B aligned; every `.grad` a view of ONE
 zero-initialised fp32 gradient buffer, and (bf16 mode) every compute shadow a view of ONE
-bf16 buffer.  Parameters of one module (a transformer Block, a diffusion head) stay
-contiguous inside each group, so a module = one DP bucket.
+bf16 buffer.  Parameters of one module (a transformer Block, a diffusion trunk) stay
+contiguous inside each group, so a module = one DP bucket per group.  When the owning module
+is moved (`.to(device)`, as accelerate.prepare does after get_optimizer) the store re-binds
+the moved tensors into fresh flat buffers on the new device, values and gradients kept.
 
-FusedAdamWEMA: torch.optim.AdamW semantics (policy:343-360) + EMA (ema_model.py:45-89,
-power 0.75) + bf16 shadow refresh + 1/world gradient averaging in one HIP pass
-(uva_adamw_ema).  Exposes param_groups/step/zero_grad/state_dict like a torch optimizer
-so a diffusers-style LR scheduler drives it.
+FusedAdamWEMA: a torch.optim.Optimizer with torch.optim.AdamW semantics (policy:343-360):
+torch-format param_groups (dicts holding "params"), state_dict()/load_state_dict() in
+torch.optim.AdamW's layout (per-parameter exp_avg / exp_avg_sq / step), so diffusers / torch
+LambdaLR schedulers, accelerate's AcceleratedOptimizer + GradScaler.unscale_, and the reference
+workspace's checkpoint payloads all work on it.  One HIP pass per param group does AdamW +
+1/world gradient averaging + bf16 shadow refresh, and -- when an EMAModel is attached
+(model/autoregressive/ema_model.py) -- the EMA update of the same step (ema_model.py:57-89).
 
 GradReducer: DP gradient all-reduce over RCCL (torch.distributed "nccl") overlapped with
-backward: each fused Block / diffusion-trunk backward ends by launching the async
-all-reduce of its own bucket; the rest is reduced once at the end of backward.
+backward, the build's replacement of DDP's bucketed reducer (accelerate.prepare,
+workspace:208-220): each fused Block / diffusion-trunk backward launches the async
+all-reduce of its own bucket the moment its last gradient is enqueued; at the end of the
+backward pass (an autograd engine callback, as DDP's) the rest is reduced and the compute
+stream waits for every bucket.
 """
 import math
+import weakref
 
 import torch
 import torch.distributed as dist
 
 from ..native import ops
-from ..runtime import cdt
+from ..runtime import RT, cdt
+
+GROUP_ALIGN = 64  # elements: 256-B aligned group regions (float4 optimizer body)
 
 
 def is_no_decay(name, p):
+    """policy.add_weight_decay's split (policy:326-341)."""
     return p.ndim == 1 or name.endswith(".bias")
 
 
+def _align(n, a=GROUP_ALIGN):
+    return (n + a - 1) // a * a
+
+
 class ParamStore:
-    def __init__(self, model):
-        named = [(n, p) for n, p in model.named_parameters() if p.requires_grad]
-        decay = [(n, p) for n, p in named if not is_no_decay(n, p)]
-        nodecay = [(n, p) for n, p in named if is_no_decay(n, p)]
-        self.order = decay + nodecay
-        self.n_decay = sum(p.numel() for _, p in decay)
-        total = sum(p.numel() for _, p in self.order)
-        dev = named[0][1].device
-        self.flat = torch.empty(total, dtype=torch.float32, device=dev)
-        self.grad = torch.zeros(total, dtype=torch.float32, device=dev)
-        self.shadow = None
-        if cdt() == torch.bfloat16:
-            self.shadow = torch.empty(total, dtype=torch.bfloat16, device=dev)
+    def __init__(self, named_groups, prefix=""):
+        """named_groups: [[(name, param), ...] per param group]; names relative to the module the
+        optimizer was built over, `prefix` its name in the policy (e.g. "model.")."""
+        self.groups = [list(g) for g in named_groups]
+        self.prefix = prefix
+        self.order = [x for g in self.groups for x in g]
         self.offsets = {}
+        self.group_ranges = []
         off = 0
+        for g in self.groups:
+            off = _align(off)
+            start = off
+            for n, p in g:
+                self.offsets[id(p)] = (off, p.numel())
+                off += p.numel()
+            self.group_ranges.append((start, off - start))
+        self.total = _align(off)
+        self.n_params = sum(p.numel() for _, p in self.order)
+        self.flat = self.grad = self.shadow = None
+        self._bind(self.order[0][1].device)
+
+    # ---- binding ------------------------------------------------------------------------
+    def _bind(self, dev):
+        flat = torch.zeros(self.total, dtype=torch.float32, device=dev)
+        grad = torch.zeros(self.total, dtype=torch.float32, device=dev)
+        shadow = None
+        if cdt() == torch.bfloat16 and dev.type == "cuda":
+            shadow = torch.zeros(self.total, dtype=torch.bfloat16, device=dev)
         for n, p in self.order:
-            k = p.numel()
-            self.flat[off:off + k].copy_(p.detach().reshape(-1))
-            p.data = self.flat[off:off + k].view_as(p)
-            p.grad = self.grad[off:off + k].view_as(p)
-            if self.shadow is not None:
-                p._uva_shadow = self.shadow[off:off + k].view_as(p)
-                p._uva_shadow_static = True
-            self.offsets[id(p)] = (off, k)
-            off += k
-        self.total = total
+            o, k = self.offsets[id(p)]
+            flat[o:o + k].copy_(p.detach().reshape(-1))
+            if p.grad is not None:
+                grad[o:o + k].copy_(p.grad.detach().reshape(-1))
+            p.data = flat[o:o + k].view_as(p)
+            p.grad = grad[o:o + k].view_as(p)
+            if shadow is not None:
+                p._uva_shadow = shadow[o:o + k].view_as(p)
+                p._uva_shadow_owner = id(p)
+            else:
+                p.__dict__.pop("_uva_shadow", None)
+                p.__dict__.pop("_uva_shadow_owner", None)
+        self.flat, self.grad, self.shadow = flat, grad, shadow
         self.refresh_shadow()
+
+    @property
+    def device(self):
+        return self.flat.device
+
+    def is_bound(self):
+        """every parameter (checked at both ends of the layout) still a view of the flat buffer."""
+        for _, p in (self.order[0], self.order[-1]):
+            o, _ = self.offsets[id(p)]
+            if p.device != self.flat.device or p.data_ptr() != self.flat.data_ptr() + 4 * o:
+                return False
+            if p.grad is None or p.grad.data_ptr() != self.grad.data_ptr() + 4 * o:
+                return False
+        return True
+
+    def rebind(self):
+        """re-create the flat buffers on the parameters' current device (after a module move);
+        -> True when it re-bound."""
+        if self.is_bound():
+            return False
+        self._bind(self.order[0][1].device)
+        return True
 
     def refresh_shadow(self):
         if self.shadow is not None:
@@ -77,6 +132,7 @@ class ParamStore:
 
 
 def ema_decay(step, update_after_step=0, inv_gamma=1.0, power=0.75, min_value=0.0, max_value=0.9999):
+    """EMAModel.get_decay (ema_model.py:45-55)."""
     s = max(0, step - update_after_step - 1)
     if s <= 0:
         return 0.0
@@ -84,78 +140,145 @@ def ema_decay(step, update_after_step=0, inv_gamma=1.0, power=0.75, min_value=0.
     return max(min_value, min(v, max_value))
 
 
-class FusedAdamWEMA:
-    def __init__(self, model, lr=1e-4, betas=(0.9, 0.95), weight_decay=0.02, eps=1e-8, use_ema=True, ema_cfg=None):
-        self.store = ParamStore(model)
-        self.param_groups = [{"lr": lr, "initial_lr": lr, "betas": betas, "weight_decay": weight_decay,
-                              "eps": eps}]
-        self.defaults = dict(self.param_groups[0])
+_ADAMW_GROUP_KEYS = dict(amsgrad=False, foreach=None, maximize=False, capturable=False, differentiable=False,
+                         fused=None)
+
+
+class FusedAdamWEMA(torch.optim.Optimizer):
+    """torch.optim.AdamW over flat buffers, one fused HIP pass per param group."""
+
+    def __init__(self, params, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=1e-2, named=None, prefix=""):
+        self._ready = False
+        super().__init__(params, dict(lr=lr, betas=tuple(betas), eps=eps, weight_decay=weight_decay))
+        for g in self.param_groups:
+            g.setdefault("initial_lr", g["lr"])
+            g["betas"] = tuple(g["betas"])
+        names = {id(p): n for n, p in (named or [])}
+        groups = [[(names.get(id(p), f"param{gi}.{i}"), p) for i, p in enumerate(g["params"])]
+                  for gi, g in enumerate(self.param_groups)]
+        self.store = ParamStore(groups, prefix)
         self.m = torch.zeros_like(self.store.flat)
         self.v = torch.zeros_like(self.store.flat)
-        self.ema = self.store.flat.clone() if use_ema else None
-        self.ema_cfg = dict(ema_cfg or {})
         self.step_count = 0
-        self.ema_step_count = 0
         self.grad_scale = 1.0
-        self.state = {}
+        self.reducer = None
+        self._ema_ref = None
+        self._ready = True
 
-    def zero_grad(self, set_to_none=False):
+    # ---- torch.optim.Optimizer surface ----------------------------------------------------
+    def add_param_group(self, param_group):
+        if getattr(self, "_ready", False):
+            raise NotImplementedError("FusedAdamWEMA: param groups are fixed at construction (flat layout)")
+        super().add_param_group(param_group)
+
+    def _sync(self):
+        """follow a module move of the parameters (m / v move with them)."""
+        if self.store.rebind():
+            self.m = self.m.to(self.store.device)
+            self.v = self.v.to(self.store.device)
+
+    def zero_grad(self, set_to_none=True):
+        """zeroes the flat gradient buffer; gradients stay views of it (set_to_none is ignored:
+        a None grad would break the flat layout the fused kernels write into)."""
+        self._sync()
         self.store.zero_grad()
 
-    def step(self):
-        g = self.param_groups[0]
+    @torch.no_grad()
+    def step(self, closure=None):
+        loss = None
+        if closure is not None:
+            with torch.enable_grad():
+                loss = closure()
+        self._sync()
+        if self.reducer is not None:
+            self.reducer.finish()
         self.step_count += 1
-        d = ema_decay(self.ema_step_count, **self.ema_cfg) if self.ema is not None else 0.0
-        self.ema_step_count += 1
-        b1, b2 = g["betas"]
-        ops.adamw_ema(self.store.flat, self.store.grad, self.m, self.v, self.ema, self.store.shadow,
-                      self.store.n_decay, g["lr"], b1, b2, g["eps"], g["weight_decay"], self.step_count,
-                      self.grad_scale, d)
+        ema = self.attached_ema()
+        d = ema.get_decay(ema.optimization_step) if ema is not None else 0.0
+        st = self.store
+        for g, (off, n) in zip(self.param_groups, st.group_ranges):
+            if n == 0:
+                continue
+            b1, b2 = g["betas"]
+            sl = slice(off, off + n)
+            ops.adamw_ema(st.flat[sl], st.grad[sl], self.m[sl], self.v[sl],
+                          ema.flat[sl] if ema is not None else None,
+                          st.shadow[sl] if st.shadow is not None else None, n, n if g["weight_decay"] else 0,
+                          g["lr"], b1, b2, g["eps"], g["weight_decay"], self.step_count, self.grad_scale, d)
+        if ema is not None:
+            ema.mark_fused(self.step_count)
+        RT.bump_params()
+        return loss
 
+    # ---- EMA fusion ------------------------------------------------------------------------
+    def attach_ema(self, ema):
+        self._ema_ref = weakref.ref(ema) if ema is not None else None
+
+    def attached_ema(self):
+        ema = self._ema_ref() if self._ema_ref is not None else None
+        if ema is None or ema.flat is None or ema.flat.device != self.store.device:
+            return None
+        return ema
+
+    # ---- data parallel ---------------------------------------------------------------------
+    def maybe_init_reducer(self, model):
+        """create the RCCL bucket reducer once a process group of world > 1 exists (accelerate /
+        torchrun initialise it after get_optimizer)."""
+        if self.reducer is not None or not (dist.is_available() and dist.is_initialized()):
+            return self.reducer
+        world = dist.get_world_size()
+        if world > 1:
+            self.reducer = GradReducer(self.store, default_buckets(model))
+            self.grad_scale = 1.0 / world
+        return self.reducer
+
+    # ---- torch.optim.AdamW state_dict layout -------------------------------------------------
     def state_dict(self):
-        return {"step": self.step_count, "ema_step": self.ema_step_count, "m": self.m, "v": self.v,
-                "param_groups": [dict(x) for x in self.param_groups]}
+        st = self.store
+        state, groups, idx = {}, [], 0
+        for g, names in zip(self.param_groups, st.groups):
+            ids = []
+            for n, p in names:
+                if self.step_count > 0:
+                    o, k = st.offsets[id(p)]
+                    state[idx] = {"step": torch.tensor(float(self.step_count)),
+                                  "exp_avg": self.m[o:o + k].view_as(p), "exp_avg_sq": self.v[o:o + k].view_as(p)}
+                ids.append(idx)
+                idx += 1
+            d = {k: v for k, v in g.items() if k != "params"}
+            for k, v in _ADAMW_GROUP_KEYS.items():
+                d.setdefault(k, v)
+            d["params"] = ids
+            groups.append(d)
+        return {"state": state, "param_groups": groups}
 
     def load_state_dict(self, sd):
-        self.step_count = sd["step"]
-        self.ema_step_count = sd.get("ema_step", sd["step"])
-        self.m.copy_(sd["m"])
-        self.v.copy_(sd["v"])
-        self.param_groups = [dict(x) for x in sd["param_groups"]]
-
-    def ema_state(self):
-        """EMA weights as a name -> tensor dict (frozen VAE EMA == VAE, not stored)."""
-        out = {}
-        for n, p in self.store.order:
-            o, k = self.store.offsets[id(p)]
-            out[n] = self.ema[o:o + k].view_as(p)
-        return out
-
-
-class CosineWithWarmup:
-    """diffusers 0.18.2 get_cosine_schedule_with_warmup (restated; lr_scheduler.py:10-59)."""
-
-    def __init__(self, optimizer, num_warmup_steps, num_training_steps, num_cycles=0.5, last_epoch=-1):
-        self.opt = optimizer
-        self.warm, self.total, self.cycles = num_warmup_steps, num_training_steps, num_cycles
-        self.base = [g["initial_lr"] for g in optimizer.param_groups]
-        self.last_epoch = last_epoch
-        self.step()
-
-    def factor(self, step):
-        if step < self.warm:
-            return step / max(1, self.warm)
-        prog = (step - self.warm) / max(1, self.total - self.warm)
-        return max(0.0, 0.5 * (1.0 + math.cos(math.pi * self.cycles * 2.0 * prog)))
-
-    def step(self):
-        self.last_epoch += 1
-        f = self.factor(self.last_epoch)
-        for g, b in zip(self.opt.param_groups, self.base):
-            g["lr"] = b * f
-
-    def get_last_lr(self):
-        return [g["lr"] for g in self.opt.param_groups]
+        """torch.optim.AdamW.state_dict() with the same groups -> flat m / v / step count."""
+        self._sync()
+        st = self.store
+        groups = sd["param_groups"]
+        if len(groups) != len(st.groups) or any(len(a["params"]) != len(b) for a, b in zip(groups, st.groups)):
+            raise ValueError("optimizer state does not match this optimizer's param groups "
+                             f"({[len(g['params']) for g in groups]} vs {[len(g) for g in st.groups]})")
+        steps = set()
+        for grp, names in zip(groups, st.groups):
+            for (n, p), pid in zip(names, grp["params"]):
+                s = sd["state"].get(pid, sd["state"].get(str(pid)))
+                if s is None:
+                    continue
+                o, k = st.offsets[id(p)]
+                if s["exp_avg"].numel() != k:
+                    raise ValueError(f"optimizer state of {n}: {s['exp_avg'].numel()} values, parameter has {k}")
+                self.m[o:o + k].copy_(s["exp_avg"].reshape(-1))
+                self.v[o:o + k].copy_(s["exp_avg_sq"].reshape(-1))
+                steps.add(int(float(s["step"])))
+        if len(steps) > 1:
+            raise ValueError(f"per-parameter step counts differ: {sorted(steps)}")
+        self.step_count = steps.pop() if steps else 0
+        for mine, theirs in zip(self.param_groups, groups):
+            for k in ("lr", "betas", "eps", "weight_decay", "initial_lr"):
+                if k in theirs:
+                    mine[k] = tuple(theirs[k]) if k == "betas" else theirs[k]
 
 
 def default_buckets(model):
@@ -173,7 +296,10 @@ def default_buckets(model):
 
 
 class GradReducer:
-    """Bucketed async all-reduce of the flat gradient buffer, launched from inside backward."""
+    """Bucketed async all-reduce (sum; the optimizer applies 1/world) of the flat gradient buffer,
+    launched from inside backward.  One reduction per backward pass (gradient accumulation over
+    several backward passes is not supported: the reference configs all use
+    gradient_accumulate_every = 1)."""
 
     def __init__(self, store, buckets, group=None):
         """buckets: [(module whose params form the bucket, module whose fused backward fires the hook)]"""
@@ -183,6 +309,8 @@ class GradReducer:
         self.handles = []
         self.done = set()
         self.buckets = []
+        self.pending = False
+        self._queued = False
         covered = []
         for i, (m, owner) in enumerate(buckets):
             rs = store.ranges_of(m)
@@ -190,7 +318,7 @@ class GradReducer:
             covered += rs
             if self.world > 1:
                 owner._uva_bucket_hook = (lambda i=i: self.launch(i))
-        # complement of all hooked ranges -> one tail bucket
+        # complement of all hooked ranges -> the tail bucket (reduced at the end of backward)
         covered.sort()
         tail, pos = [], 0
         for o, k in covered:
@@ -201,22 +329,49 @@ class GradReducer:
             tail.append((pos, store.total - pos))
         self.tail = tail
 
-    def launch(self, i):
-        if self.world <= 1 or i in self.done:
+    def coverage(self):
+        """per flat element: in how many reduced ranges it lies (must be exactly 1 everywhere)."""
+        cnt = torch.zeros(self.store.total, dtype=torch.int32)
+        for rs in self.buckets + [self.tail]:
+            for o, k in rs:
+                cnt[o:o + k] += 1
+        return cnt
+
+    def arm(self):
+        """a forward pass ran: the next finish() must reduce (even if no bucket hook fires)."""
+        self.pending = self.world > 1
+
+    def _launch(self, i):
+        if i in self.done:
             return
         self.done.add(i)
+        grad = self.store.grad
         for o, k in self.buckets[i]:
-            self.handles.append(dist.all_reduce(self.store.grad[o:o + k], group=self.group, async_op=True))
+            self.handles.append(dist.all_reduce(grad[o:o + k], group=self.group, async_op=True))
 
-    def finish(self):
-        """after loss.backward(): reduce what is left, then make the compute stream wait."""
+    def launch(self, i):
+        """bucket hook, called by a fused backward once all of bucket i's gradients are enqueued."""
         if self.world <= 1:
             return
+        if not self._queued:
+            # DDP-style: complete the reduction when the autograd engine finishes this backward
+            torch.autograd.Variable._execution_engine.queue_callback(self.finish)
+            self._queued = True
+        self.pending = True
+        self._launch(i)
+
+    def finish(self):
+        """reduce what is left, then make the compute stream wait (no-op when already done)."""
+        self._queued = False
+        if not self.pending:
+            return
         for i in range(len(self.buckets)):
-            self.launch(i)
+            self._launch(i)
+        grad = self.store.grad
         for o, k in self.tail:
-            self.handles.append(dist.all_reduce(self.store.grad[o:o + k], group=self.group, async_op=True))
+            self.handles.append(dist.all_reduce(grad[o:o + k], group=self.group, async_op=True))
         for h in self.handles:
             h.wait()
         self.handles = []
         self.done = set()
+        self.pending = False

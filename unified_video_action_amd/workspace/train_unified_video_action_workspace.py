@@ -1,0 +1,291 @@
+"""TrainUnifiedVideoActionWorkspace: the reference's training loop
+(workspace/train_unified_video_action_workspace.py:41-422), selected by `model._target_`
+(config/model/uva.yaml:1) and run by train.py (`cls(cfg).run()`, train.py:58-60).
+
+Same structure and order:
+  __init__ (:44-79)   seed torch / numpy / random = training.seed on every rank; instantiate
+                      model.policy with task_name / task_modes / normalizer_type /
+                      language_emb_model; ema_model = deepcopy(model); optimizer =
+                      model.get_optimizer(**model.policy.optimizer).
+  run (:82-422)       dataloaders (DataLoader(dataset, **dataloader), rank-sharded), normalizer
+                      from the dataset on rank 0 -> every rank, lr scheduler (get_scheduler,
+                      num_training_steps = len(dl) * num_epochs // grad_accum,
+                      last_epoch = global_step - 1), resume from latest.ckpt, EMAModel via
+                      `ema._target_`, debug overrides (:222-229), then per batch:
+                        device transfer -> model(batch) -> backward -> optimizer.step ->
+                        zero_grad -> lr_scheduler.step -> ema.step(model) -> step log
+                      and per epoch the checkpoint (latest + top-k on rank 0).
+MI355X differences (results unchanged):
+  * no accelerate / DDP wrapper: one process per GPU (torchrun or `accelerate launch` env),
+    torch.distributed over RCCL; the optimizer's bucket reducer all-reduces the flat gradient
+    buffer from inside backward (workspace/optim.GradReducer) and the AdamW kernel averages.
+  * `mixed_precision` fp16 / bf16 -> bf16 MFMA operands with fp32 accumulation, residual
+    streams and master weights (no GradScaler needed); "no" -> fp32.
+  * the frame resize runs inside the policy (fused with frame selection), so the workspace
+    does not call resize_image.
+  * step logs are read back one step late (a pinned host copy + event instead of three
+    blocking .item() calls), so the host keeps queueing the next step.
+  * epoch-end FVD / action-L2 evaluation and env rollouts are out of scope; the
+    checkpoint's top-k monitor falls back to train_loss when the configured key is absent.
+"""
+import copy
+import json
+import os
+import random
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+from .. import config as C
+from ..runtime import RT
+from .base_workspace import BaseWorkspace
+
+
+def dist_env():
+    """(world, rank, local_rank) from torchrun / accelerate-launch environment variables."""
+    return (int(os.environ.get("WORLD_SIZE", "1")), int(os.environ.get("RANK", "0")),
+            int(os.environ.get("LOCAL_RANK", "0")))
+
+
+def init_distributed(device_type="cuda"):
+    world, rank, local = dist_env()
+    if world > 1 and not dist.is_initialized():
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        if device_type == "cuda":
+            torch.cuda.set_device(local)
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group("gloo")
+    return world, rank, local
+
+
+def _to_device(x, dev):
+    if isinstance(x, dict):
+        return {k: _to_device(v, dev) for k, v in x.items()}
+    return x.to(dev, non_blocking=True) if torch.is_tensor(x) else x
+
+
+class TopKCheckpointManager:
+    """common/checkpoint_util.py:5-60."""
+
+    def __init__(self, save_dir, monitor_key, mode="min", k=1, format_str="epoch={epoch:03d}.ckpt"):
+        assert mode in ("max", "min") and k >= 0
+        self.save_dir, self.monitor_key, self.mode, self.k, self.format_str = save_dir, monitor_key, mode, k, format_str
+        self.path_value_map = {}
+
+    def get_ckpt_path(self, data):
+        if self.k == 0 or self.monitor_key not in data:
+            return None
+        value = data[self.monitor_key]
+        path = os.path.join(self.save_dir, self.format_str.format(**data))
+        if len(self.path_value_map) < self.k:
+            self.path_value_map[path] = value
+            return path
+        ranked = sorted(self.path_value_map.items(), key=lambda x: x[1])
+        drop = None
+        if self.mode == "max" and value > ranked[0][1]:
+            drop = ranked[0][0]
+        elif self.mode == "min" and value < ranked[-1][1]:
+            drop = ranked[-1][0]
+        if drop is None:
+            return None
+        del self.path_value_map[drop]
+        self.path_value_map[path] = value
+        if os.path.exists(drop):
+            os.remove(drop)
+        return path
+
+
+class _LaggedLog:
+    """step losses copied to pinned host memory behind an event; read one step later."""
+
+    def __init__(self):
+        self.pending = None
+
+    def push(self, tensors, meta):
+        host = torch.empty(len(tensors), dtype=torch.float32, pin_memory=torch.cuda.is_available())
+        dev = torch.stack([t.detach().float().reshape(()) for t in tensors])
+        host.copy_(dev, non_blocking=True)
+        ev = None
+        if dev.is_cuda:
+            ev = torch.cuda.Event()
+            ev.record()
+        prev, self.pending = self.pending, (host, ev, meta)
+        return self._read(prev)
+
+    def flush(self):
+        prev, self.pending = self.pending, None
+        return self._read(prev)
+
+    @staticmethod
+    def _read(item):
+        if item is None:
+            return None
+        host, ev, meta = item
+        if ev is not None:
+            ev.synchronize()
+        vals = host.tolist()
+        out = dict(meta)
+        out.update(train_loss=vals[0], diffusion_loss=vals[1], action_loss=vals[2])
+        return out
+
+
+class TrainUnifiedVideoActionWorkspace(BaseWorkspace):
+    include_keys = ["global_step", "epoch"]
+
+    def __init__(self, cfg, output_dir=None):
+        super().__init__(cfg, output_dir=output_dir)
+        seed = cfg.training.seed
+        torch.manual_seed(seed)
+        np.random.seed(seed)
+        random.seed(seed)
+        RT.set_precision(_precision(cfg))
+        language_emb_model = cfg.task.dataset.get("language_emb_model")
+        if cfg.training.get("deepspeed_config") is not None:
+            language_emb_model = None  # workspace:57-61
+        self.model = C.instantiate(cfg.model.policy, task_name=cfg.task.name, task_modes=cfg.task.task_modes,
+                                   normalizer_type=cfg.task.dataset.normalizer_type,
+                                   language_emb_model=language_emb_model)
+        self.ema_model = copy.deepcopy(self.model) if cfg.training.use_ema else None
+        self.optimizer = self.model.get_optimizer(**cfg.model.policy.optimizer)
+        self.global_step = 0
+        self.epoch = 0
+
+    # ---- setup (the part of run() before the loop) ------------------------------------------
+    def setup(self, device=None):
+        cfg = self.cfg
+        self.world, self.rank, local = init_distributed("cuda" if torch.cuda.is_available() else "cpu")
+        self.device = torch.device(device) if device is not None else (
+            torch.device("cuda", local) if torch.cuda.is_available() else torch.device("cpu"))
+        if cfg.training.debug:
+            cfg.training.num_epochs = 2
+            cfg.training.max_train_steps = 3
+            cfg.training.max_val_steps = 3
+            cfg.training.rollout_every = 1
+            cfg.training.checkpoint_every = 1
+            cfg.training.val_every = 1
+            cfg.training.sample_every = 1
+        self.dataset = C.instantiate(cfg.task.dataset)
+        sampler = None
+        dl_kw = dict(cfg.dataloader)
+        if self.world > 1:
+            sampler = torch.utils.data.distributed.DistributedSampler(
+                self.dataset, num_replicas=self.world, rank=self.rank, shuffle=bool(dl_kw.get("shuffle", False)),
+                seed=cfg.training.seed)
+            dl_kw.pop("shuffle", None)
+        if not torch.cuda.is_available():
+            dl_kw["pin_memory"] = False
+        self.train_dataloader = torch.utils.data.DataLoader(self.dataset, sampler=sampler, **dl_kw)
+        # normalizer: fitted on rank 0, its tensors broadcast to every rank (workspace:150-168)
+        normalizer = self.dataset.get_normalizer()
+        if self.world > 1:
+            _broadcast_module_state(normalizer, self.device)
+        self.model.set_normalizer(normalizer)
+        if self.ema_model is not None:
+            self.ema_model.set_normalizer(normalizer)
+        from ..model.common.lr_scheduler import get_scheduler
+        self.lr_scheduler = get_scheduler(
+            cfg.training.lr_scheduler, optimizer=self.optimizer, num_warmup_steps=cfg.training.lr_warmup_steps,
+            num_training_steps=(len(self.train_dataloader) * cfg.training.num_epochs)
+            // cfg.training.gradient_accumulate_every,
+            last_epoch=self.global_step - 1)
+        if cfg.training.get("resume") and self.get_checkpoint_path().is_file():
+            print(f"Resuming from checkpoint {self.get_checkpoint_path()}")
+            self.load_checkpoint(path=self.get_checkpoint_path())
+        self.model.to(self.device)
+        if self.ema_model is not None:
+            self.ema_model.to(self.device)
+        # a fresh EMAModel after the (optional) resume, as the reference builds it (:190-193)
+        self.ema = C.instantiate(cfg.ema, model=self.ema_model) if cfg.training.use_ema else None
+        self.model.train()
+        return self
+
+    # ---- one training step (workspace:279-302) -------------------------------------------------
+    def train_step(self, batch, rng=None):
+        """-> (raw_loss, diffusion_loss, action_loss) device tensors."""
+        cfg = self.cfg
+        raw_loss, (loss_diffusion, loss_action) = self.model(batch, rng=rng) if rng is not None else self.model(batch)
+        raw_loss.backward()
+        if self.global_step % cfg.training.gradient_accumulate_every == 0:
+            self.optimizer.step()
+            self.optimizer.zero_grad()
+            self.lr_scheduler.step()
+        if self.ema is not None:
+            self.ema.step(self.model)
+        return raw_loss, loss_diffusion, loss_action
+
+    def run(self):
+        cfg = self.cfg
+        self.setup()
+        topk = TopKCheckpointManager(save_dir=os.path.join(self.output_dir, "checkpoints"), **cfg.checkpoint.topk)
+        os.makedirs(self.output_dir, exist_ok=True)
+        log_path = os.path.join(self.output_dir, "logs.json.txt")
+        logf = open(log_path, "a") if self.rank == 0 else None
+        lag = _LaggedLog()
+        zero = torch.zeros((), device=self.device)
+
+        def emit(rec):
+            if rec is not None and logf is not None:
+                logf.write(json.dumps(rec) + "\n")
+                logf.flush()
+            return rec
+
+        for _ in range(cfg.training.num_epochs):
+            if isinstance(self.train_dataloader.sampler, torch.utils.data.distributed.DistributedSampler):
+                self.train_dataloader.sampler.set_epoch(self.epoch)
+            losses = []
+            n_batches = len(self.train_dataloader)
+            for batch_idx, batch in enumerate(self.train_dataloader):
+                batch = _to_device(batch, self.device)
+                raw, lv, la = self.train_step(batch)
+                meta = {"global_step": self.global_step, "epoch": self.epoch,
+                        "lr": self.lr_scheduler.get_last_lr()[0]}
+                rec = emit(lag.push([raw, lv if lv is not None else zero, la if la is not None else zero], meta))
+                if rec is not None:
+                    losses.append(rec["train_loss"])
+                if batch_idx != n_batches - 1:
+                    self.global_step += 1
+                if cfg.training.max_train_steps is not None and batch_idx >= cfg.training.max_train_steps - 1:
+                    break
+            rec = emit(lag.flush())
+            if rec is not None:
+                losses.append(rec["train_loss"])
+            step_log = {"train_loss": float(np.mean(losses)) if losses else float("nan"),
+                        "global_step": self.global_step, "epoch": self.epoch}
+            if self.epoch % cfg.training.checkpoint_every == 0 and self.rank == 0:
+                if cfg.checkpoint.save_last_ckpt:
+                    self.save_checkpoint()
+                metric = {k.replace("/", "_"): v for k, v in step_log.items()}
+                path = topk.get_ckpt_path(metric)
+                if path is not None:
+                    self.save_checkpoint(path=path)
+            emit(dict(step_log, epoch_end=True))
+            self.global_step += 1
+            self.epoch += 1
+        self.wait_for_save()
+        if logf is not None:
+            logf.close()
+        return self
+
+
+def _precision(cfg):
+    mp = str(cfg.training.get("mixed_precision", "fp16") or "no").lower()
+    return "fp32" if mp in ("no", "fp32", "none") else "bf16"
+
+
+def _broadcast_module_state(module, device):
+    """rank 0's tensors of `module` to every rank (replaces the reference's normalizer pickle)."""
+    sd = module.state_dict()
+    keys = sorted(sd)
+    meta = [(k, tuple(sd[k].shape)) for k in keys] if dist.get_rank() == 0 else None
+    obj = [meta]
+    dist.broadcast_object_list(obj, src=0)
+    meta = obj[0]
+    backend_dev = device if dist.get_backend() == "nccl" else torch.device("cpu")
+    new = {}
+    for k, shp in meta:
+        t = sd[k].to(backend_dev).float().contiguous() if k in sd else torch.zeros(shp, device=backend_dev)
+        dist.broadcast(t, src=0)
+        new[k] = t.cpu()
+    module.load_state_dict(new)
