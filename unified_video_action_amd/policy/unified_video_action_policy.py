@@ -67,6 +67,15 @@ def _add_anchor(module, state_dict, prefix, local_metadata, strict, missing_keys
     state_dict.setdefault(prefix + "ddp_anchor", torch.zeros((), device=module.ddp_anchor.device))
 
 
+def _after_load(module, incompatible_keys):
+    """loaded weights went into the flat fp32 buffer in place: refresh its bf16 compute shadow."""
+    opt = module.bound_optimizer()
+    if opt is not None:
+        opt.store.refresh_shadow()
+    from ..runtime import RT
+    RT.bump_params()
+
+
 def _ddp_active():
     import torch.distributed as dist
     return dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1
@@ -124,6 +133,7 @@ class UnifiedVideoActionPolicy(nn.Module):
         self.ddp_anchor = nn.Parameter(torch.zeros(()))
         self._register_state_dict_hook(_drop_anchor)
         self._register_load_state_dict_pre_hook(_add_anchor, with_module=True)
+        self.register_load_state_dict_post_hook(_after_load)
         self._uva_opt = None
         # warm start (policy:112-118): a MAR checkpoint's model_ema or a UVA .ckpt's ema_model
         self.pretrained_model_path = _get(ap, "pretrained_model_path", None)
@@ -206,7 +216,7 @@ class UnifiedVideoActionPolicy(nn.Module):
             raise ValueError(f"pretrained checkpoint {self.pretrained_model_path}: no matching parameters")
         sd.update(take)
         missing, unexpected = self.model.load_state_dict(sd, strict=False)
-        RT.bump_params()
+        _after_load(self, None)
         self.pretrained_report = {"loaded": sorted(take), "kept_init": skipped, "missing": list(missing),
                                   "unexpected": list(unexpected)}
         return self.pretrained_report

@@ -24,7 +24,6 @@ all-reduce of its own bucket the moment its last gradient is enqueued; at the en
 backward pass (an autograd engine callback, as DDP's) the rest is reduced and the compute
 stream waits for every bucket.
 """
-import math
 import weakref
 
 import torch
@@ -203,7 +202,7 @@ class FusedAdamWEMA(torch.optim.Optimizer):
             sl = slice(off, off + n)
             ops.adamw_ema(st.flat[sl], st.grad[sl], self.m[sl], self.v[sl],
                           ema.flat[sl] if ema is not None else None,
-                          st.shadow[sl] if st.shadow is not None else None, n, n if g["weight_decay"] else 0,
+                          st.shadow[sl] if st.shadow is not None else None, n if g["weight_decay"] else 0,
                           g["lr"], b1, b2, g["eps"], g["weight_decay"], self.step_count, self.grad_scale, d)
         if ema is not None:
             ema.mark_fused(self.step_count)
