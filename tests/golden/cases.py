@@ -234,3 +234,55 @@ def trace_rng(step, B=POLICY_B):
     r["vae_eps_c"] = hash_normal(tag + "/eps_c", (B * 4, 16, 16, 16))
     r["task_mode"] = mode
     return r
+
+
+# ---- policy-level Libero / UMI cases (config 4 / 5 plumbing through compute_loss) ----------
+POLICY_VARIANT_MODES = {"libero": ["full_dynamic_model", "policy_model"],
+                        "umi": ["full_dynamic_model", "policy_model"]}
+
+
+def umi_img_indices(tag, B):
+    out = np.zeros((B, 8, 1), np.float32)
+    for b in range(B):
+        u = uniform_pm1(f"{tag}/idx/{b}", 16)
+        hist = np.sort(np.argsort(u, kind="stable")[:4])
+        out[b, :, 0] = np.concatenate([hist, [19, 23, 27, 31]])
+    return out
+
+
+def policy_variant_batch(variant, B=POLICY_B):
+    tag = f"policy/{variant}"
+    if variant == "libero":
+        return {"obs": {"agentview_rgb": (hash_tensor(tag + "/img", (B, 32, 3, 128, 128)) + 1.0) * 0.5},
+                "action": hash_tensor(tag + "/action", (B, 32, 10)),
+                "language_latents": hash_normal(tag + "/text", (B, 512)) * 0.1}
+    obs = {"camera0_rgb": (hash_tensor(tag + "/img", (B, 8, 3, 224, 224)) + 1.0) * 0.5,
+           "img_indices": umi_img_indices(tag, B)}
+    for k, d in (("robot0_eef_pos", 3), ("robot0_eef_rot_axis_angle", 6), ("robot0_gripper_width", 1),
+                 ("robot0_eef_rot_axis_angle_wrt_start", 6)):
+        obs[k] = hash_normal(f"{tag}/{k}", (B, 32, d))
+    return {"obs": obs, "action": hash_normal(tag + "/action", (B, 32, 10)),
+            "language_latents": hash_normal(tag + "/text", (B, 512)) * 0.1}
+
+
+def policy_variant_rng(variant, mode, B=POLICY_B):
+    tag = f"policy/{variant}/{mode}"
+    r = mar_rng(variant, mode, B)
+    r["vae_eps_x"] = hash_normal(tag + "/eps_x", (B * 4, 16, 16, 16))
+    r["vae_eps_c"] = hash_normal(tag + "/eps_c", (B * 4, 16, 16, 16))
+    r["task_mode"] = mode
+    return r
+
+
+def policy_variant_kwargs(variant):
+    """UnifiedVideoActionPolicy kwargs (besides vae / autoregressive params) of the variant."""
+    v = VARIANTS[variant]
+    umi = variant == "umi"
+    return dict(action_model_params=dict(predict_action=True, act_model_type="conv_fc"),
+                shape_meta={"action": {"shape": [v["Da"]]}}, n_action_steps=8, shift_action=not umi,
+                language_emb_model="clip", task_name=v["task_name"],
+                task_modes=["policy_model", "full_dynamic_model"] if umi else [],
+                normalizer_type="none" if umi else "all", selected_training_mode=None, use_history_action=False,
+                use_proprioception=v["use_proprioception"], action_mask_ratio=0.5,
+                different_history_freq=v["different_history_freq"], predict_wrist_img=False,
+                predict_proprioception=v["predict_proprioception"])

@@ -474,6 +474,78 @@ def gen_predict():
     print("predict pusht: action_pred", tuple(res["action_pred"].shape), res["action_pred"][0, :3].tolist())
 
 
+def gen_policy_variants():
+    """compute_loss of the reference policy for the Libero (CLIP latents, Da = 10, 128-px agentview
+    resized to 256) and UMI (proprioception in/out, img_indices gather, different_history_freq,
+    8 frames at 224 px, no normalizer, shift_action False) variants: full KL-VAE, reduced MAR,
+    draws injected; plus the UMI process_data gather itself (integer indexing, bit-exact)."""
+    from unified_video_action.model.common.normalizer import LinearNormalizer
+    from unified_video_action.policy.unified_video_action_policy import UnifiedVideoActionPolicy
+
+    class AD(dict):
+        def __getattr__(self, k):
+            if k.startswith("__"):
+                raise AttributeError(k)
+            v = self[k]
+            return AD(v) if isinstance(v, dict) else v
+
+    ref_mar.mar_golden = lambda **kw: ref_mar.MAR(
+        norm_layer=partial(nn.LayerNorm, eps=1e-6), **cases.MAR_GOLDEN, **kw)
+    amp = dict(pretrained_model_path=None, model_size="mar_golden")
+    for k in cases.POLICY_AMP_KEYS:
+        amp[k] = cases.MAR_KW[k]
+    out = {}
+    for variant, modes in cases.POLICY_VARIANT_MODES.items():
+        kw = cases.policy_variant_kwargs(variant)
+        for mode in modes:
+            pol = UnifiedVideoActionPolicy(
+                vae_model_params=AD(autoencoder_path=None, ddconfig=AD(vae_embed_dim=16, ch_mult=[1, 1, 2, 2, 4])),
+                autoregressive_model_params=AD(amp), action_model_params=AD(kw["action_model_params"]),
+                shape_meta=AD(kw["shape_meta"]), **{k: v for k, v in kw.items()
+                                                    if k not in ("action_model_params", "shape_meta")}, debug=False)
+            hash_init_(pol.vae_model, "vae.")
+            hash_init_(pol.model, "mar.")
+            if variant == "libero":
+                norm = LinearNormalizer()
+                norm.fit({"action": torch.tensor([[-1.0] * 10, [1.0] * 10])})
+                pol.set_normalizer(norm)
+            pol.train()
+            b = cases.policy_variant_batch(variant)
+            batch = {"obs": {k: torch.from_numpy(v) for k, v in b["obs"].items()},
+                     "action": torch.from_numpy(b["action"]),
+                     "language_latents": torch.from_numpy(b["language_latents"])}
+
+            class Cfg:
+                class task:
+                    name = kw["task_name"]
+
+            batch = data_utils.resize_image(Cfg, batch)
+            rng = cases.policy_variant_rng(variant, mode)
+            pol.model.mask_ratio_generator = type("G", (), {"rvs": staticmethod(
+                lambda n, r=rng["mask_rate"]: np.array([r]))})()
+            with injected(rng):
+                loss, (lv, la) = pol.compute_loss(batch)
+            loss.backward()
+            names, sums, heads = grad_table(pol.model)
+            out[f"{variant}_{mode}_loss"] = np.array([loss.item(), float(lv), float(la)], np.float64)
+            out[f"{variant}_{mode}_gnames"], out[f"{variant}_{mode}_gsums"], out[f"{variant}_{mode}_gheads"] = \
+                names, sums, heads
+            print(f"policy {variant} {mode}: loss={loss.item():.6f} Lv={float(lv):.6f} La={float(la):.6f}")
+    # process_data's UMI gather (data_utils.py:214-219, 291-360), train and eval
+    b = cases.policy_variant_batch("umi", B=3)
+    batch = {"obs": {k: torch.from_numpy(v) for k, v in b["obs"].items()}}
+    batch["obs"]["image"] = torch.zeros(3, 8, 3, 4, 4)
+    for ev in (False, True):
+        _, prop, idx = data_utils.process_data(batch, task_name="umi", eval=ev, use_proprioception=True,
+                                               different_history_freq=True)
+        tag = "eval" if ev else "train"
+        out[f"umi_gather_{tag}_indices"] = idx.numpy()
+        for k, v in prop.items():
+            if v is not None:
+                out[f"umi_gather_{tag}_{k}"] = v.numpy()
+    np.savez(os.path.join(OUT, "g2_policy_variants.npz"), **out)
+
+
 def gen_workspace_trace():
     """The reference's per-step training body (workspace:279-302) on the golden PushT policy
     (full KL-VAE, reduced MAR, joint model): deepcopy EMA policy, policy.get_optimizer (torch

@@ -233,3 +233,24 @@ def test_sample_tokens_video_oracle(variant):
     ref = g[f"{variant}_tokens"]
     np.testing.assert_allclose(tok.numpy(), ref, rtol=1e-4, atol=1e-4 * np.abs(ref).max())
     np.testing.assert_allclose(act.numpy(), g[f"{variant}_act"], rtol=0, atol=1e-5)
+
+
+def test_umi_proprio_gather_bit_exact_vs_reference():
+    """process_data's UMI branch (data_utils.py:214-219, 291-360): per-sample img_indices gather of the
+    history half, train and eval, against the reference's own outputs (g2_policy_variants)."""
+    import torch
+    import cases
+    from unified_video_action_amd.utils.data_utils import umi_proprioception
+    g = replay.load("g2_policy_variants.npz")
+    b = cases.policy_variant_batch("umi", B=3)
+    obs = {k: torch.from_numpy(v) for k, v in b["obs"].items()}
+    idx = obs["img_indices"].int().squeeze(2)
+    for tag, train in (("train", True), ("eval", False)):
+        np.testing.assert_array_equal(idx.numpy(), g[f"umi_gather_{tag}_indices"])
+        got = umi_proprioception(obs, idx, different_history_freq=True, train=train)
+        keys = [k[len(f"umi_gather_{tag}_"):] for k in g.files if k.startswith(f"umi_gather_{tag}_")
+                and not k.endswith("_indices")]
+        assert keys
+        for k in keys:
+            assert got[k] is not None, k
+            np.testing.assert_array_equal(got[k].numpy(), g[f"umi_gather_{tag}_{k}"], err_msg=k)
