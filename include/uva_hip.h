@@ -201,6 +201,19 @@ int uva_adamw_ema(float* p, const float* g, float* m, float* v, float* ema, void
 /* EMAModel.step over the flat buffer (ema_model.py:78-85): ema = d*ema + (1-d)*p (16-B aligned). */
 int uva_ema_update(float* ema, const float* p, long long n, float decay, hipStream_t stream);
 
+/* ---- fp8 (OCP e4m3) attention forward, head_dim 64 (BASELINE config 5 "fp8 MFMA attention";
+ *      same call site as uva_attn_fwd: timm Attention / SDPA, mar_con_unified.py:201-249).
+ * uva_attn_quant_fp8: per (batch, head, q|k|v, 64-row tile) power-of-two scales; rounds the bf16
+ *      qkv [B,N,3,H,64] IN PLACE to the fp8 grid (the backward then runs uva_attn_bwd on it:
+ *      straight-through rounding) and fills `workspace` (uva_attn_fp8_workspace bytes, 256-B
+ *      aligned) with the fp8 Q/K rows, the key-permuted fp8 V^T and the scales.
+ * uva_attn_fwd_fp8: Q.K^T and P.V on v_mfma_f32_16x16x32_fp8_fp8, fp32 online softmax; out / lse2
+ *      / mask as uva_attn_fwd.  N % 64 == 0. */
+long long uva_attn_fp8_workspace(int B, int N, int H);
+int uva_attn_quant_fp8(void* qkv, void* workspace, int B, int N, int H, hipStream_t stream);
+int uva_attn_fwd_fp8(const void* workspace, void* out, float* lse2, const void* mask, int B, int N, int H, float scale,
+                     float drop_p, hipStream_t stream);
+
 /* ---- fused attention, head_dim 64, bf16 (timm Attention / SDPA with attn dropout,
  *      mar_con_unified.py:201-249 -> timm 0.9.7 Attention.forward, F.scaled_dot_product_attention).
  *      qkv: [B,N,3,H,64] (the qkv GEMM output), out/dout: [B,N,H,64], lse2: [B,H,N] log2-domain

@@ -234,8 +234,16 @@ class BlockFn(torch.autograd.Function):
         if flash:
             o = torch.empty(M, D, dtype=c, device=dev)
             lse = torch.empty(B, H, N, dtype=F32, device=dev)
-            amask = ops.attn_fwd(qkv, o, lse, B, N, H, scale, p_attn, seeds[0],
-                                 mask=premask[1] if premask is not None else None)
+            pm = premask[1] if premask is not None else None
+            if RT.attn_fp8:
+                # qkv is rounded in place to the fp8 grid: the saved tensor (and so the bf16 backward)
+                # sees exactly what the fp8 forward multiplied
+                ws = ops.attn_fp8_workspace(B, N, H, dev)
+                ops.attn_quant_fp8(qkv, ws, B, N, H)
+                amask = ops.attn_fwd_fp8(ws, o, lse, B, N, H, scale, p_attn, seeds[0], mask=pm)
+                del ws
+            else:
+                amask = ops.attn_fwd(qkv, o, lse, B, N, H, scale, p_attn, seeds[0], mask=pm)
             P, Pd = None, amask
         else:
             o, P, Pd = _attn_mat_fwd(qkv, B, N, H, scale, p_attn, seeds[0])

@@ -348,6 +348,29 @@ def attn_fwd(qkv, out, lse2, B, N, H, scale, drop_p=0.0, seed=0, mask=None):
     return mask if drop_p > 0 else None
 
 
+def attn_fp8_workspace(B, N, H, device):
+    return torch.empty(lib().query("uva_attn_fp8_workspace", B, N, H), dtype=torch.uint8, device=device)
+
+
+def attn_quant_fp8(qkv, ws, B, N, H):
+    """round qkv [B,N,3,H,64] bf16 in place to the fp8 grid; fp8 Q/K, V^T and scales -> ws."""
+    assert qkv.dtype == torch.bfloat16 and qkv.is_contiguous() and qkv.numel() == B * N * 3 * H * 64
+    assert N % 64 == 0 and ws.dtype == torch.uint8 and ws.numel() >= lib().query("uva_attn_fp8_workspace", B, N, H)
+    lib().call("uva_attn_quant_fp8", ptr(qkv), ptr(ws), B, N, H, stream())
+
+
+def attn_fwd_fp8(ws, out, lse2, B, N, H, scale, drop_p=0.0, seed=0, mask=None, device=None):
+    """fp8 forward from attn_quant_fp8's workspace -> the dropout mask planes (None when p == 0)."""
+    assert out.dtype == torch.bfloat16 and out.is_contiguous() and out.numel() == B * N * H * 64
+    assert lse2.numel() == B * H * N and N % 64 == 0
+    with _traced(f"attn_fwd_fp8 B{B} N{N} H{H}", 4.0 * B * H * N * N * 64):
+        if drop_p > 0 and mask is None:
+            mask = attn_dropmask(B, N, H, drop_p, seed, out.device)
+        lib().call("uva_attn_fwd_fp8", ptr(ws), ptr(out), ptr(lse2), ptr(mask) if drop_p > 0 else None, B, N, H,
+                   float(scale), float(drop_p), stream())
+    return mask if drop_p > 0 else None
+
+
 def attn_bwd(qkv, out, dout, lse2, dvec, dqkv, B, N, H, scale, drop_p=0.0, seed=0, mask=None):
     assert dout.dtype == torch.bfloat16 and dout.is_contiguous() and dqkv.is_contiguous()
     assert dout.numel() == B * N * H * 64 and dqkv.numel() == B * N * 3 * H * 64 and dvec.numel() == B * H * N

@@ -10,6 +10,10 @@ class _Runtime:
     def __init__(self):
         self.compute_dtype = torch.bfloat16   # GEMM/attention operand dtype ("bf16" bench mode)
         self.flash_attention = True           # bf16 fused attention; False -> materialised GEMM+softmax
+        # "fp8_attn" precision: attention forward on fp8 (e4m3) MFMA with per-tile power-of-two
+        # scales, bf16 everywhere else (BASELINE config 5); backward = bf16 kernels on the fp8-rounded
+        # q / k / v (straight-through)
+        self.attn_fp8 = False
         # VAE ResnetBlock: GroupNorm+SiLU applied inside the halo conv's input staging (True) or as
         # a separate apply pass (False); UVA_VAE_GN_IN_CONV=0/1 overrides
         self.vae_gn_in_conv = os.environ.get("UVA_VAE_GN_IN_CONV", "1") == "1"
@@ -32,12 +36,16 @@ class _Runtime:
 
     def set_precision(self, name):
         name = str(name).lower()
+        self.attn_fp8 = False
         if name in ("fp32", "float32", "no"):
             self.compute_dtype = torch.float32
         elif name in ("bf16", "bfloat16", "fp16"):
             # fp16 autocast of the reference maps to bf16 MFMA here (same 16-bit storage,
             # wider exponent; no GradScaler needed)
             self.compute_dtype = torch.bfloat16
+        elif name in ("fp8_attn", "fp8"):
+            self.compute_dtype = torch.bfloat16
+            self.attn_fp8 = True
         else:
             raise ValueError(f"unknown precision {name}")
 
