@@ -53,7 +53,7 @@ def parse(argv=None):
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--batch", type=int, default=32)
     ap.add_argument("--config", default="pusht_video", choices=sorted(GFLOP_PER_SAMPLE))
-    ap.add_argument("--precision", default="bf16")
+    ap.add_argument("--precision", default="bf16", help="bf16 | fp8_attn (fp8 e4m3 attention) | fp32")
     ap.add_argument("--other-configs", default="pusht_joint:64",
                     help="N=1 only: extra config:batch entries measured after the main line ('' = none)")
     ap.add_argument("--other-steps", type=int, default=20)
@@ -274,7 +274,7 @@ def run(args):
         "metric": METRIC, "value": main["value"], "unit": "samples/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": main["ms_per_step"], "ms_per_step_median": main["ms_per_step_median"],
         "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
-        "dtype": "bf16" if args.precision == "bf16" else "f32",
+        "dtype": {"bf16": "bf16", "fp8_attn": "bf16 (attention fp8 e4m3)"}.get(args.precision, "f32"),
         "data": "synthetic (device-resident, dataset shapes; random-init weights)",
         "config": {"workload": f"{args.config}: {WORKLOAD[args.config]}; step = frame select+resize -> KL-VAE "
                                f"encode (8 frames) -> mar_base MAR fwd/bwd (N=1024) -> diffusion loss -> backward "

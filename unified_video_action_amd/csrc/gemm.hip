@@ -943,11 +943,58 @@ __global__ __launch_bounds__(512, 1) void gemm_8ph(const bf16* __restrict__ A, c
   // stage layout: [A-h0][A-h1][B-h0][B-h1]
   auto img_a = [&](int buf, int h) { return lds + buf * G::STAGE + h * G::A_HALF; };
   auto img_b = [&](int buf, int h) { return lds + buf * G::STAGE + 2 * G::A_HALF + h * G::B_HALF; };
+  // VAR & 256 (fast path; full tiles, K range a multiple of 64, TA != 2): the per-lane DMA sources of
+  // K-tile 0 are computed once and advanced by one uniform stride per K-tile -- the general path
+  // re-derives them (swizzle, bounds, zero page) for every half-tile, ~25 VALU per DMA instruction
+  // per-lane 32-bit byte offsets from the (uniform) operand base, so every DMA is SGPR base + VGPR
+  // offset with no per-tile vector address arithmetic (operands < 4 GiB: checked by the launcher)
+  unsigned offA[2][G::GA], offB[2][G::GB];
+  const long long stepA = (TA == 1 ? 64 * lda : 64) * 2, stepB = (TB == 1 ? 64 * ldb : 64) * 2;  // bytes
+  if constexpr ((VAR & 256) != 0) {
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+#pragma unroll
+      for (int i = 0; i < G::GA; ++i)
+        offA[h][i] = (unsigned)((const char*)dma8_addr<TA, G::RWA, G::WA, G::GA>(A, lda, m0, M, kbeg, kend, h, i, cp, cr) -
+                                (const char*)A);
+#pragma unroll
+      for (int i = 0; i < G::GB; ++i)
+        offB[h][i] = (unsigned)((const char*)dma8_addr<TB, G::RWB, G::WB, G::GB>(B, ldb, n0, N, kbeg, kend, h, i, cp, cr) -
+                                (const char*)B);
+    }
+  }
+  const int w8 = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  // buffer descriptors built from kernargs only (wave-uniform by construction): the per-tile step is
+  // the SGPR soffset, so the DMA issue needs no vector address arithmetic at all
+  const int nrA = __builtin_amdgcn_readfirstlane(
+      (int)(unsigned)min(2ull * (unsigned long long)(TA == 1 ? K : M) * (unsigned long long)lda, 0xffffffffull));
+  const int nrB = __builtin_amdgcn_readfirstlane(
+      (int)(unsigned)min(2ull * (unsigned long long)(TB == 1 ? K : N) * (unsigned long long)ldb, 0xffffffffull));
+  const auto rsA = __builtin_amdgcn_make_buffer_rsrc((void*)A, 0, nrA, 0x00020000);
+  const auto rsB = __builtin_amdgcn_make_buffer_rsrc((void*)B, 0, nrB, 0x00020000);
   // issue half-tile q of K-tile t (q order A-h0, B-h0, B-h1, A-h1; global sequence S = 4t + q)
   auto stage = [&](auto qc, int t) {
     constexpr int q = decltype(qc)::value;
     const int buf = t & 1, k0 = kbeg + t * 64;
-    if constexpr (q == 0 || q == 3) {
+    if constexpr ((VAR & 256) != 0) {
+      if constexpr (q == 0 || q == 3) {
+        constexpr int h = q == 0 ? 0 : 1;
+        bf16* img = img_a(buf, h);
+        const int so = (int)(unsigned)(t * stepA);
+#pragma unroll
+        for (int i = 0; i < G::GA; ++i)
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(rsA, (__attribute__((address_space(3))) void*)(img + (w8 * G::GA + i) * 512),
+                                                   16, (int)offA[h][i], so, 0, 0);
+      } else {
+        constexpr int h = q - 1;
+        bf16* img = img_b(buf, h);
+        const int so = (int)(unsigned)(t * stepB);
+#pragma unroll
+        for (int i = 0; i < G::GB; ++i)
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(rsB, (__attribute__((address_space(3))) void*)(img + (w8 * G::GB + i) * 512),
+                                                   16, (int)offB[h][i], so, 0, 0);
+      }
+    } else if constexpr (q == 0 || q == 3) {
       constexpr int h = q == 0 ? 0 : 1;
       dma8_half<TA, G::RWA, G::WA, G::GA>(A, lda, m0, M, k0, kend, h, img_a(buf, h), cp, cr);
     } else {
@@ -1364,17 +1411,25 @@ static int launch_8ph(int ta, int tb, const void* A, const void* B, void* C, int
   const long long nblk = pl.nblk;
   float* part = splits > 1 ? ws : nullptr;
   dim3 grid((unsigned)nblk, splits, batch);
-#define G8(a, b, BNV)                                                                                       \
+#define G8X(a, b, BNV, VV)                                                                                  \
   do {                                                                                                      \
     static bool attr = false;                                                                               \
     const int lb = Gemm8Cfg<BNV>::LDS_BYTES;                                                                \
     if (!attr) {                                                                                            \
-      (void)hipFuncSetAttribute((const void*)gemm_8ph<a, b, BNV, TC>, hipFuncAttributeMaxDynamicSharedMemorySize, lb); \
+      (void)hipFuncSetAttribute((const void*)gemm_8ph<a, b, BNV, TC, VV>, hipFuncAttributeMaxDynamicSharedMemorySize, lb); \
       attr = true;                                                                                          \
     }                                                                                                       \
-    gemm_8ph<a, b, BNV, TC><<<grid, 512, lb, s>>>((const bf16*)A, (const bf16*)B, (TC*)C, M, N, K, lda, ldb, ldc, \
-                                                  bs, ep, cp, part, kps);                                   \
+    gemm_8ph<a, b, BNV, TC, VV><<<grid, 512, lb, s>>>((const bf16*)A, (const bf16*)B, (TC*)C, M, N, K, lda, ldb, ldc, \
+                                                      bs, ep, cp, part, kps);                               \
   } while (0)
+  // full tiles + K a multiple of 64 (every K-slice then is one too): the precomputed-source fast path
+  static const int fast_env = env_int("UVA_8PH_FAST", 1);
+  auto span = [](int t, int rows, int cols, long long ld) {  // bytes an operand's offsets can reach
+    return 2.0 * ((t == 1 ? (double)cols : (double)rows) * (double)ld);
+  };
+  const bool fast = fast_env && ta != 2 && M % 256 == 0 && N % bn == 0 && K % 64 == 0 && batch == 1 &&
+                    span(ta, M, K, lda) < 4.0e9 && span(tb, N, K, ldb) < 4.0e9;
+#define G8(a, b, BNV) do { if (fast) G8X(a, b, BNV, 256); else G8X(a, b, BNV, 0); } while (0)
 #define G8B(a, b) do { if (bn == 256) G8(a, b, 256); else G8(a, b, 128); } while (0)
   static const int var = env_int("UVA_8PH_VAR", 0);
 #define G8V(V)                                                                                              \
@@ -1413,6 +1468,7 @@ static int launch_8ph(int ta, int tb, const void* A, const void* B, void* C, int
   else return -(int)hipErrorInvalidValue;
 #undef G8B
 #undef G8
+#undef G8X
   UVA_LAUNCH_CHECK();
   if (part) {
     launch_splitk_reduce<TC>(part, splits, C, M, N, ldc, ep, s);
