@@ -291,59 +291,75 @@ __device__ __forceinline__ int xcd_remap(int bid, int nblk) {
   return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + bid / 8;
 }
 
-// one row segment of 8 consecutive columns (16-B aligned in C): epilogue math with vector loads of
-// C (beta), residual and vector stores; o = the values as stored (for fused statistics)
+// one row segment of 8 consecutive columns (16-B aligned in C): the row-wise epilogue inputs (C for
+// beta, residual, gate) are loaded by epi_load_row8 and consumed by epi_apply_row8, so a caller can
+// issue the next row's loads before this row's store -- a load issued after a store waits for that
+// store on the in-order vector-memory counter, which serialised the epilogue on the store latency
+struct EpiRow {
+  float prev[8], res[8], gate[8];
+};
+
+__device__ __forceinline__ void epi_load_bias8(const EpiParams& ep, int col0, float (&bv)[8]) {
+  if (ep.bias) {
+    const float4 b0 = *(const float4*)(ep.bias + col0), b1 = *(const float4*)(ep.bias + col0 + 4);
+    bv[0] = b0.x; bv[1] = b0.y; bv[2] = b0.z; bv[3] = b0.w; bv[4] = b1.x; bv[5] = b1.y; bv[6] = b1.z; bv[7] = b1.w;
+  } else {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) bv[e] = 0.f;
+  }
+}
+
 template <typename TC>
-__device__ __forceinline__ void epi_row8(TC* __restrict__ C, long long cbase, const EpiParams& ep, long long roff,
-                                         int row, int col0, int z, int M, int N, const float (&v)[8], float (&o)[8]) {
-  float prev[8];
+__device__ __forceinline__ void epi_load_row8(const TC* __restrict__ C, long long cbase, const EpiParams& ep,
+                                              long long roff, int row, int col0, EpiRow& in) {
   if (ep.beta != 0.f) {
     if constexpr (sizeof(TC) == 2) {
       bf16x8 pv = *(const bf16x8*)(C + cbase);
 #pragma unroll
-      for (int e = 0; e < 8; ++e) prev[e] = (float)pv[e];
+      for (int e = 0; e < 8; ++e) in.prev[e] = (float)pv[e];
     } else {
       float4 p0 = *(const float4*)(C + cbase), p1 = *(const float4*)(C + cbase + 4);
-      prev[0] = p0.x; prev[1] = p0.y; prev[2] = p0.z; prev[3] = p0.w;
-      prev[4] = p1.x; prev[5] = p1.y; prev[6] = p1.z; prev[7] = p1.w;
+      in.prev[0] = p0.x; in.prev[1] = p0.y; in.prev[2] = p0.z; in.prev[3] = p0.w;
+      in.prev[4] = p1.x; in.prev[5] = p1.y; in.prev[6] = p1.z; in.prev[7] = p1.w;
     }
   }
-  float resv[8];
   if (ep.residual) {
     const long long ri = roff + (long long)row * ep.ldr + col0;
     if (ep.res_dt == UVA_DT_BF16 && (ri % 8 == 0)) {
       bf16x8 rv = *(const bf16x8*)((const bf16*)ep.residual + ri);
 #pragma unroll
-      for (int e = 0; e < 8; ++e) resv[e] = (float)rv[e];
+      for (int e = 0; e < 8; ++e) in.res[e] = (float)rv[e];
     } else if (ep.res_dt != UVA_DT_BF16 && (ri % 4 == 0)) {
       float4 r0 = *(const float4*)((const float*)ep.residual + ri);
       float4 r1 = *(const float4*)((const float*)ep.residual + ri + 4);
-      resv[0] = r0.x; resv[1] = r0.y; resv[2] = r0.z; resv[3] = r0.w;
-      resv[4] = r1.x; resv[5] = r1.y; resv[6] = r1.z; resv[7] = r1.w;
+      in.res[0] = r0.x; in.res[1] = r0.y; in.res[2] = r0.z; in.res[3] = r0.w;
+      in.res[4] = r1.x; in.res[5] = r1.y; in.res[6] = r1.z; in.res[7] = r1.w;
     } else {
 #pragma unroll
       for (int e = 0; e < 8; ++e)
-        resv[e] = ep.res_dt == UVA_DT_BF16 ? (float)((const bf16*)ep.residual)[ri + e]
-                                           : ((const float*)ep.residual)[ri + e];
+        in.res[e] = ep.res_dt == UVA_DT_BF16 ? (float)((const bf16*)ep.residual)[ri + e]
+                                             : ((const float*)ep.residual)[ri + e];
     }
-  }
-  float bv[8], gv[8];
-  if (ep.bias) {
-    const float4 b0 = *(const float4*)(ep.bias + col0), b1 = *(const float4*)(ep.bias + col0 + 4);
-    bv[0] = b0.x; bv[1] = b0.y; bv[2] = b0.z; bv[3] = b0.w; bv[4] = b1.x; bv[5] = b1.y; bv[6] = b1.z; bv[7] = b1.w;
   }
   if (ep.gate) {
     const long long gi = (long long)row * ep.ldg + col0;
     if (ep.gate_dt == UVA_DT_BF16 && gi % 8 == 0) {
       const bf16x8 g8 = *(const bf16x8*)((const bf16*)ep.gate + gi);
 #pragma unroll
-      for (int e = 0; e < 8; ++e) gv[e] = (float)g8[e];
+      for (int e = 0; e < 8; ++e) in.gate[e] = (float)g8[e];
     } else {
 #pragma unroll
       for (int e = 0; e < 8; ++e)
-        gv[e] = ep.gate_dt == UVA_DT_BF16 ? (float)((const bf16*)ep.gate)[gi + e] : ((const float*)ep.gate)[gi + e];
+        in.gate[e] = ep.gate_dt == UVA_DT_BF16 ? (float)((const bf16*)ep.gate)[gi + e] : ((const float*)ep.gate)[gi + e];
     }
   }
+}
+
+// o = the values as stored (for fused statistics)
+template <typename TC, bool NT = false>
+__device__ __forceinline__ void epi_apply_row8(TC* __restrict__ C, long long cbase, const EpiParams& ep,
+                                               const float (&bv)[8], const EpiRow& in, int row, int col0, int z,
+                                               int M, int N, const float (&v)[8], float (&o)[8]) {
   bool keep[8] = {true, true, true, true, true, true, true, true};
   if (ep.drop_thresh) {
     const uint64_t d0 = (uint64_t)((long long)z * M * N + (long long)row * N + col0);
@@ -357,7 +373,7 @@ __device__ __forceinline__ void epi_row8(TC* __restrict__ C, long long cbase, co
   }
   float x[8];
 #pragma unroll
-  for (int e = 0; e < 8; ++e) x[e] = ep.alpha * v[e] + (ep.bias ? bv[e] : 0.f);
+  for (int e = 0; e < 8; ++e) x[e] = ep.alpha * v[e] + bv[e];
   if (ep.aux) {  // pre-activation copy, one 16-B (bf16) / 2 x 16-B (fp32) store
     if constexpr (sizeof(TC) == 2) {
       bf16x8 av;
@@ -390,22 +406,37 @@ __device__ __forceinline__ void epi_row8(TC* __restrict__ C, long long cbase, co
   for (int e = 0; e < 8; ++e) {
     float t = x[e];
     if (ep.drop_thresh) t = keep[e] ? t * ep.drop_scale : 0.f;
-    if (ep.gate) t *= gv[e];
-    if (ep.residual) t += resv[e];
-    if (ep.beta != 0.f) t += ep.beta * prev[e];
+    if (ep.gate) t *= in.gate[e];
+    if (ep.residual) t += in.res[e];
+    if (ep.beta != 0.f) t += ep.beta * in.prev[e];
     o[e] = t;
   }
   if constexpr (sizeof(TC) == 2) {
     bf16x8 ov;
 #pragma unroll
     for (int e = 0; e < 8; ++e) ov[e] = (bf16)o[e];
-    *(bf16x8*)(C + cbase) = ov;
+    if constexpr (NT) {
+      typedef unsigned u32x4_nt __attribute__((ext_vector_type(4)));
+      __builtin_nontemporal_store(__builtin_bit_cast(u32x4_nt, ov), (u32x4_nt*)(C + cbase));
+    } else {
+      *(bf16x8*)(C + cbase) = ov;
+    }
 #pragma unroll
     for (int e = 0; e < 8; ++e) o[e] = (float)ov[e];
   } else {
     *(float4*)(C + cbase) = make_float4(o[0], o[1], o[2], o[3]);
     *(float4*)(C + cbase + 4) = make_float4(o[4], o[5], o[6], o[7]);
   }
+}
+
+template <typename TC, bool NT = false>
+__device__ __forceinline__ void epi_row8(TC* __restrict__ C, long long cbase, const EpiParams& ep, long long roff,
+                                         int row, int col0, int z, int M, int N, const float (&v)[8], float (&o)[8]) {
+  float bv[8];
+  EpiRow in;
+  epi_load_bias8(ep, col0, bv);
+  epi_load_row8<TC>(C, cbase, ep, roff, row, col0, in);
+  epi_apply_row8<TC, NT>(C, cbase, ep, bv, in, row, col0, z, M, N, v, o);
 }
 
 // Epilogue staged through LDS: the 128x128 fp32 accumulator tile is written to LDS with
@@ -442,6 +473,51 @@ __device__ __forceinline__ void epilogue_tile(const f32x4 (&acc)[4][4], char* sm
   float gs_s[8], gs_q[8];
 #pragma unroll
   for (int e = 0; e < 8; ++e) gs_s[e] = gs_q[e] = 0.f;
+  const bool plain = !ep.residual && !ep.gate && !ep.aux && ep.act == 0 && ep.drop_thresh == 0 && ep.beta == 0.f;
+  if (!pslab && full && !gn_part) {
+    float bv[8];
+    epi_load_bias8(ep, col0, bv);
+    if (plain) {  // no loads inside the loop: no store waits for an earlier one (see EpiRow)
+#pragma unroll
+      for (int it = 0; it < 8; ++it) {
+        const int rl = it * 16 + rsub, row = m0 + rl;
+        if (row < M) {
+          const float4 a = *(const float4*)(T + rl * EPI_TP + c8 * 8);
+          const float4 b = *(const float4*)(T + rl * EPI_TP + c8 * 8 + 4);
+          const float v[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+          TC* dst = C + coff + (long long)row * ldc + col0;
+          if constexpr (sizeof(TC) == 2) {
+            bf16x8 ov;
+#pragma unroll
+            for (int e = 0; e < 8; ++e) ov[e] = (bf16)(ep.alpha * v[e] + bv[e]);
+            *(bf16x8*)dst = ov;
+          } else {
+            *(float4*)dst = make_float4(ep.alpha * v[0] + bv[0], ep.alpha * v[1] + bv[1], ep.alpha * v[2] + bv[2],
+                                        ep.alpha * v[3] + bv[3]);
+            *(float4*)(dst + 4) = make_float4(ep.alpha * v[4] + bv[4], ep.alpha * v[5] + bv[5],
+                                              ep.alpha * v[6] + bv[6], ep.alpha * v[7] + bv[7]);
+          }
+        }
+      }
+    } else {  // the next row's inputs are loaded before this row's store
+      EpiRow cur, nxt;
+      if (m0 + rsub < M) epi_load_row8<TC>(C, coff + (long long)(m0 + rsub) * ldc + col0, ep, roff, m0 + rsub, col0, cur);
+#pragma unroll 1
+      for (int it = 0; it < 8; ++it) {
+        const int rl = it * 16 + rsub, row = m0 + rl;
+        if (it + 1 < 8 && row + 16 < M)
+          epi_load_row8<TC>(C, coff + (long long)(row + 16) * ldc + col0, ep, roff, row + 16, col0, nxt);
+        if (row < M) {
+          const float4 a = *(const float4*)(T + rl * EPI_TP + c8 * 8);
+          const float4 b = *(const float4*)(T + rl * EPI_TP + c8 * 8 + 4);
+          const float v[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+          float o[8];
+          epi_apply_row8<TC>(C, coff + (long long)row * ldc + col0, ep, bv, cur, row, col0, z, M, N, v, o);
+        }
+        cur = nxt;
+      }
+    }
+  } else
   for (int it = 0; it < 8; ++it) {
     const int rl = it * 16 + rsub;
     const int row = m0 + rl;
@@ -893,7 +969,8 @@ struct Gemm8Cfg {
 // VAR: diagnostic build bits (0 = production): 1 s_memtime stamps per phase segment, 2 no wave-group
 // stagger, 4 no compiler memory fences around barriers, 8 lgkmcnt after the barrier (timing only:
 // breaks the WAR order), 16 no s_setprio, 32 per-tile prologue / K-loop / epilogue stamps,
-// 64 LDS-only epilogue barriers, 128 (with 32) epilogue chunk-0 staging / store split
+// 64 __syncthreads() epilogue barriers (drain the stores; the default orders LDS only), 128 (with 32) epilogue chunk-0 staging / store split, 256 the fast-path
+// DMA (full tiles), 512 no output stores (timing only), 1024 non-temporal output stores
 // (tools_gemm8_phase.py: the epilogue of a 256x256 bf16 tile is ~29k ticks at K=768, mostly the
 // output stores of all CUs landing at once)
 #define GEMM8_SYNC()                                     \
@@ -912,6 +989,12 @@ __global__ __launch_bounds__(512, 1) void gemm_8ph(const bf16* __restrict__ A, c
   bf16* lds = (bf16*)smem;
   unsigned long long st_entry = 0, st_after_pro = 0, st_after_loop = 0, st_e1 = 0, st_e2 = 0;
   if constexpr (VAR & 32) asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(st_entry)::"memory");
+  if constexpr ((VAR & 2048) != 0) {  // experiment: stagger the first round of blocks in 4 groups
+    if (blockIdx.x < 256) {
+      const int n = (blockIdx.x & 3) * 2;
+      for (int i = 0; i < n; ++i) __builtin_amdgcn_s_sleep(127);
+    }
+  }
   const int z = blockIdx.z, zo = z / bs.binner, zi = z % bs.binner;
   A += zo * bs.sAo + zi * bs.sAi;
   B += zo * bs.sBo + zi * bs.sBi;
@@ -1158,6 +1241,9 @@ __global__ __launch_bounds__(512, 1) void gemm_8ph(const bf16* __restrict__ A, c
   const int c8 = threadIdx.x % C8, rsub = threadIdx.x / C8;
   const int col0 = n0 + c8 * 8;
   const bool full = (col0 + 8 <= N) && (ldc % 8 == 0) && ((coff + col0) % 8 == 0);
+  float bv[8];
+  if (!pslab && full) epi_load_bias8(ep, col0, bv);
+  const bool plain = !ep.residual && !ep.gate && !ep.aux && ep.act == 0 && ep.drop_thresh == 0 && ep.beta == 0.f;
 #pragma unroll
   for (int chunk = 0; chunk < 2; ++chunk) {
     float gs_s[8], gs_q[8];
@@ -1174,10 +1260,73 @@ __global__ __launch_bounds__(512, 1) void gemm_8ph(const bf16* __restrict__ A, c
           for (int r = 0; r < 4; ++r)
             T[(rbase + i * 16 + (lane >> 4) * 4 + r) * G::TP + wc * G::RWB + j * 16 + (lane & 15)] = acc[i][j][r];
     }
-    if constexpr (VAR & 64) epi_lds_barrier(); else __syncthreads();
+    if constexpr (VAR & 64) __syncthreads(); else epi_lds_barrier();
     if constexpr (VAR & 128) {
       if (chunk == 0) asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(st_e1)::"memory");
     }
+    constexpr int NIT = EPI8_ROWS / RPP;
+    const int rowb = m0 + chunk * EPI8_ROWS + rsub;
+    // (the conv variant keeps the general loop: the GN statistics leave no registers for these)
+    if (TA != 2 && !pslab && full && plain && !(VAR & 512)) {
+      // alpha * acc (+ bias): no loads inside the loop, so no store ever waits for an earlier one
+#pragma unroll
+      for (int it = 0; it < NIT; ++it) {
+        const int row = rowb + it * RPP;
+        if (row < M) {
+          const int rl = it * RPP + rsub;
+          const float4 a = *(const float4*)(T + rl * G::TP + c8 * 8);
+          const float4 b = *(const float4*)(T + rl * G::TP + c8 * 8 + 4);
+          const float v[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+          float o[8];
+#pragma unroll
+          for (int e = 0; e < 8; ++e) o[e] = ep.alpha * v[e] + bv[e];
+          TC* dst = C + coff + (long long)row * ldc + col0;
+          if constexpr (sizeof(TC) == 2) {
+            bf16x8 ov;
+#pragma unroll
+            for (int e = 0; e < 8; ++e) ov[e] = (bf16)o[e];
+            *(bf16x8*)dst = ov;
+#pragma unroll
+            for (int e = 0; e < 8; ++e) o[e] = (float)ov[e];
+          } else {
+            *(float4*)dst = make_float4(o[0], o[1], o[2], o[3]);
+            *(float4*)(dst + 4) = make_float4(o[4], o[5], o[6], o[7]);
+          }
+          if constexpr (TA == 2) {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+              gs_s[e] += o[e];
+              gs_q[e] += o[e] * o[e];
+            }
+          }
+        }
+      }
+    } else if (TA != 2 && !pslab && full && !(VAR & 512)) {
+      // row it+1's inputs are loaded before row it's store (see EpiRow)
+      EpiRow cur, nxt;
+      if (rowb < M) epi_load_row8<TC>(C, coff + (long long)rowb * ldc + col0, ep, roff, rowb, col0, cur);
+#pragma unroll 1
+      for (int it = 0; it < NIT; ++it) {
+        const int row = rowb + it * RPP;
+        if (it + 1 < NIT && row + RPP < M)
+          epi_load_row8<TC>(C, coff + (long long)(row + RPP) * ldc + col0, ep, roff, row + RPP, col0, nxt);
+        if (row < M) {
+          const int rl = it * RPP + rsub;
+          const float4 a = *(const float4*)(T + rl * G::TP + c8 * 8);
+          const float4 b = *(const float4*)(T + rl * G::TP + c8 * 8 + 4);
+          const float v[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+          float o[8];
+          epi_apply_row8<TC, (VAR & 1024) != 0>(C, coff + (long long)row * ldc + col0, ep, bv, cur, row, col0, z, M,
+                                                 N, v, o);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            gs_s[e] += o[e];
+            gs_q[e] += o[e] * o[e];
+          }
+        }
+        cur = nxt;
+      }
+    } else
     for (int it = 0; it < EPI8_ROWS / RPP; ++it) {
       const int rl = it * RPP + rsub;
       const int row = m0 + chunk * EPI8_ROWS + rl;
@@ -1186,6 +1335,10 @@ __global__ __launch_bounds__(512, 1) void gemm_8ph(const bf16* __restrict__ A, c
       const float4 a = *(const float4*)(T + rl * G::TP + c8 * 8);
       const float4 b = *(const float4*)(T + rl * G::TP + c8 * 8 + 4);
       v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+      if constexpr ((VAR & 512) != 0) {  // timing only: no output stores
+        if (v[0] == 1234.5f && v[7] == -1234.5f) C[0] = (TC)0.f;
+        continue;
+      }
       if (pslab) {
         float* dst = pslab + (long long)row * N + col0;
         if (col0 + 8 <= N && N % 4 == 0) {
@@ -1199,7 +1352,7 @@ __global__ __launch_bounds__(512, 1) void gemm_8ph(const bf16* __restrict__ A, c
       const long long cbase = coff + (long long)row * ldc + col0;
       if (full) {
         float o[8];
-        epi_row8<TC>(C, cbase, ep, roff, row, col0, z, M, N, v, o);
+        epi_row8<TC, (VAR & 1024) != 0>(C, cbase, ep, roff, row, col0, z, M, N, v, o);
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
           gs_s[e] += o[e];
@@ -1237,7 +1390,7 @@ __global__ __launch_bounds__(512, 1) void gemm_8ph(const bf16* __restrict__ A, c
             red[((wid * C8 + lane) * 8 + e) * 2 + 1] = gs_q[e];
           }
         }
-        if constexpr (VAR & 64) epi_lds_barrier(); else __syncthreads();
+        if constexpr (VAR & 64) __syncthreads(); else epi_lds_barrier();
         const int gsz = N / 32;
         const int ngroups = min(BN, N - n0) / gsz;
         if ((int)threadIdx.x < ngroups && m0 + chunk * EPI8_ROWS < M) {
@@ -1254,7 +1407,9 @@ __global__ __launch_bounds__(512, 1) void gemm_8ph(const bf16* __restrict__ A, c
         }
       }
     }
-    if constexpr (VAR & 64) epi_lds_barrier(); else __syncthreads();
+    // LDS-only: the stores of this chunk stay in flight (a __syncthreads() would drain them), and
+    // after the last chunk nothing reads T again
+    if constexpr (VAR & 64) __syncthreads(); else if (chunk == 0) epi_lds_barrier();
   }
   if constexpr (VAR & 32) {
     unsigned long long st_end;
@@ -1456,6 +1611,15 @@ static int launch_8ph(int ta, int tb, const void* A, const void* B, void* C, int
       case 32: G8V(32); break;
       case 96: G8V(96); break;
       case 160: G8V(160); break;
+      case 256: G8V(256); break;
+      case 288: G8V(288); break;
+      case 416: G8V(416); break;
+      case 768: G8V(768); break;
+      case 800: G8V(800); break;
+      case 320: G8V(320); break;
+      case 1280: G8V(1280); break;
+      case 1344: G8V(1344); break;
+      case 2304: G8V(2304); break;
       default: return -(int)hipErrorInvalidValue;
     }
   } else
