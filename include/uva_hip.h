@@ -80,6 +80,10 @@ int uva_debug_conv_stamps(unsigned long long* host);
 int uva_debug_conv_occupancy(int tr, int gn);
 long long uva_gemm_plan(int in_dtype, int ta, int tb, int M, int N, int K, int batch, int gn_prologue,
                         long long ws_floats);
+/* Route full-tile bf16 GEMMs with an alpha (+ bias) epilogue and >= 4 K-tiles through the
+ * persistent 8-phase kernel gemm_8pp (on != 0) or the per-tile gemm_8ph (0, the default;
+ * UVA_8PP=1 sets the initial value).  Test / tuning switch; same results within fp32 rounding. */
+int uva_gemm_set_8pp(int on);
 int uva_conv2d(int dtype, const void* in, const void* w, void* out, const float* bias, const void* residual, int Nimg,
                int Hin, int Win, int Ci, int Co, int ks, int stride, int pad_t, int pad_l, int Hout, int Wout,
                const float* gn_scale, const float* gn_shift, int gn_silu, int act, float* gn_part,

@@ -286,3 +286,18 @@ def policy_variant_kwargs(variant):
                 use_proprioception=v["use_proprioception"], action_mask_ratio=0.5,
                 different_history_freq=v["different_history_freq"], predict_wrist_img=False,
                 predict_proprioception=v["predict_proprioception"])
+
+
+GRAD_SKETCH_K = 4
+
+
+def grad_sketch(name, a):
+    """GRAD_SKETCH_K random +-1 projections of a flattened gradient (float64 numpy), signs drawn
+    from the parameter's name.  Unlike the plain sum, a projection's error under per-element
+    noise has the random-walk size rms(err) * sqrt(n) whatever the gradient's mean, so
+    |sketch - ref| / (rms * sqrt(n)) is a well-conditioned relative error of the whole gradient."""
+    import zlib
+    a = np.asarray(a, np.float64).reshape(-1)
+    rng = np.random.default_rng(zlib.crc32(name.encode()))
+    r = rng.integers(0, 2, size=(GRAD_SKETCH_K, a.size), dtype=np.int8).astype(np.float64) * 2 - 1
+    return r @ a

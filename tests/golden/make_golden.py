@@ -40,6 +40,27 @@ def checksum(t):
     return np.array([a.sum().item(), (a * a).sum().item(), a.abs().max().item()], np.float64)
 
 
+_CAPTURE = None    # gen_bf16_extras: collect the arrays a generator would save instead of writing
+_AUTOCAST = False  # gen_bf16_extras: run the reference's loss under CPU bf16 autocast
+
+
+def _save(path, **d):
+    if _CAPTURE is not None:
+        _CAPTURE[path] = d
+    else:
+        np.savez(path, **d)
+
+
+def _amp():
+    return torch.autocast("cpu", dtype=torch.bfloat16) if _AUTOCAST else contextlib.nullcontext()
+
+
+def sketch_table(module):
+    """cases.grad_sketch of every parameter gradient, in grad_table's order."""
+    return np.stack([cases.grad_sketch(n, p.grad.detach().double().reshape(-1).numpy())
+                     for n, p in module.named_parameters() if p.grad is not None])
+
+
 def grad_table(module):
     names, sums, heads = [], [], []
     for n, p in module.named_parameters():
@@ -121,15 +142,46 @@ def gen_mar():
             rng = cases.mar_rng(variant, mode)
             m.mask_ratio_generator = type("G", (), {"rvs": staticmethod(
                 lambda n, r=rng["mask_rate"]: np.array([r]))})()
-            with injected(rng):
+            with injected(rng), _amp():
                 loss, lv, la = mar_call(m, variant, mode, inp)
-            loss.backward()
+            loss.float().backward()
             names, sums, heads = grad_table(m)
-            np.savez(os.path.join(OUT, f"g2_mar_{variant}_{mode}.npz"),
-                     loss=np.array([loss.item(), lv.item(), la.item()], np.float64),
-                     grad_names=names, grad_sums=sums, grad_heads=heads)
+            _save(os.path.join(OUT, f"g2_mar_{variant}_{mode}.npz"),
+                  loss=np.array([loss.item(), lv.item(), la.item()], np.float64),
+                  grad_names=names, grad_sums=sums, grad_heads=heads, grad_sketch=sketch_table(m))
             print(f"mar {variant} {mode}: loss={loss.item():.6f} Lv={lv.item():.6f} "
                   f"La={la.item():.6f} ngrads={len(names)}")
+
+
+def gen_bf16_extras():
+    """The reference's own bf16 error on every MAR case and policy mode: each generator re-run in
+    fp32 (must reproduce its stored fixture; adds the gradient sketches) and under CPU bf16 autocast
+    (bf16 linear / matmul / conv operands, fp32 norms and losses -- the reference's
+    mixed_precision=bf16 training); the bf16 loss, gradient checksums and sketches are stored
+    beside the fp32 ones ("<key>_bf16"), so the bf16 tests hold this build to the reference's own
+    bf16 deviation."""
+    global _CAPTURE, _AUTOCAST
+    for gen in (gen_mar, gen_policy, gen_policy_variants):
+        _CAPTURE, _AUTOCAST = {}, False
+        gen()
+        fp = _CAPTURE
+        _CAPTURE, _AUTOCAST = {}, True
+        try:
+            gen()
+        finally:
+            bf, _CAPTURE, _AUTOCAST = _CAPTURE, None, False
+        for path, d in fp.items():
+            old = dict(np.load(path))
+            for k, v in d.items():
+                if "sketch" not in k and k in old and np.asarray(v).dtype.kind == "f":
+                    np.testing.assert_allclose(v, old[k], rtol=1e-9, atol=0, err_msg=f"{path} {k}")
+            new = {k: v for k, v in old.items() if not k.endswith("_bf16")}
+            new.update({k: v for k, v in d.items() if "sketch" in k})
+            for k, v in bf[path].items():
+                if k.endswith(("loss", "sums", "sketch")):
+                    new[k + "_bf16"] = v
+            np.savez(path, **new)
+            print(f"bf16 extras -> {os.path.basename(path)}")
 
 
 def gen_indexing():
@@ -331,18 +383,19 @@ def gen_policy():
         rng["task_mode"] = mode
         pol.model.mask_ratio_generator = type("G", (), {"rvs": staticmethod(
             lambda n, r=rng["mask_rate"]: np.array([r]))})()
-        with injected(rng):
+        with injected(rng), _amp():
             loss, (lv, la) = pol.compute_loss(batch)
-        loss.backward()
+        loss.float().backward()
         names, sums, heads = grad_table(pol.model)
         out[f"{mode}_loss"] = np.array([loss.item(), lv.item(), la.item()], np.float64)
         out[f"{mode}_gnames"], out[f"{mode}_gsums"], out[f"{mode}_gheads"] = names, sums, heads
+        out[f"{mode}_gsketch"] = sketch_table(pol.model)
         dec, nod = pol.add_weight_decay(pol.model, 0.02)[1], None
         print(f"policy {mode}: loss={loss.item():.6f} Lv={lv.item():.6f} La={la.item():.6f}")
     decay_names = [n for n, p in pol.model.named_parameters()
                    if p.requires_grad and not (len(p.shape) == 1 or n.endswith(".bias"))]
     out["decay_names"] = np.array(decay_names)
-    np.savez(os.path.join(OUT, "g2_policy_pusht.npz"), **out)
+    _save(os.path.join(OUT, "g2_policy_pusht.npz"), **out)
 
 
 def gen_sample():
@@ -523,13 +576,14 @@ def gen_policy_variants():
             rng = cases.policy_variant_rng(variant, mode)
             pol.model.mask_ratio_generator = type("G", (), {"rvs": staticmethod(
                 lambda n, r=rng["mask_rate"]: np.array([r]))})()
-            with injected(rng):
+            with injected(rng), _amp():
                 loss, (lv, la) = pol.compute_loss(batch)
-            loss.backward()
+            loss.float().backward()
             names, sums, heads = grad_table(pol.model)
             out[f"{variant}_{mode}_loss"] = np.array([loss.item(), float(lv), float(la)], np.float64)
             out[f"{variant}_{mode}_gnames"], out[f"{variant}_{mode}_gsums"], out[f"{variant}_{mode}_gheads"] = \
                 names, sums, heads
+            out[f"{variant}_{mode}_gsketch"] = sketch_table(pol.model)
             print(f"policy {variant} {mode}: loss={loss.item():.6f} Lv={float(lv):.6f} La={float(la):.6f}")
     # process_data's UMI gather (data_utils.py:214-219, 291-360), train and eval
     b = cases.policy_variant_batch("umi", B=3)
@@ -543,7 +597,7 @@ def gen_policy_variants():
         for k, v in prop.items():
             if v is not None:
                 out[f"umi_gather_{tag}_{k}"] = v.numpy()
-    np.savez(os.path.join(OUT, "g2_policy_variants.npz"), **out)
+    _save(os.path.join(OUT, "g2_policy_variants.npz"), **out)
 
 
 def gen_workspace_trace():

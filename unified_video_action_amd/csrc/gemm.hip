@@ -1427,6 +1427,300 @@ __global__ __launch_bounds__(512, 1) void gemm_8ph(const bf16* __restrict__ A, c
   }
 }
 
+// =====================================================================================
+// Persistent 8-phase GEMM (gemm_8pp): full 256x256 tiles, K a multiple of 64 with >= 4 K-tiles,
+// alpha * acc (+ bias) epilogue. One workgroup per CU walks its tiles as ONE stream of K-tiles:
+//  * the next tile's first two K-tiles are DMAed inside this tile's last two K-tile iterations,
+//    like any other prefetch -- there is no per-tile prologue;
+//  * the MFMAs run with the operands swapped (B fragment first), so a lane holds C^T fragments =
+//    4 consecutive columns of one row; one v_permlane32_swap + one v_permlane16_swap per dword give
+//    every lane 8 consecutive columns and the epilogue stores straight from registers: no LDS
+//    staging, no barrier, the K pipeline's LDS buffers keep filling underneath it;
+//  * the stores of tile i drain while tile i+1 computes: the first phase-2 wait after an epilogue
+//    lets its NS stores stay outstanding (the vector-memory counter retires in issue order);
+//  * each tile's bias is DMAed into LDS with its first K-tile and read with ds_read (no wait on the
+//    vector-memory counter).
+// =====================================================================================
+template <int NW>
+__device__ __forceinline__ void vm_wait() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NW) : "memory");
+}
+
+template <int TA, int TB, typename TC>
+__global__ __launch_bounds__(512, 1) void gemm_8pp(const bf16* __restrict__ A, const bf16* __restrict__ B,
+                                                   TC* __restrict__ C, int M, int N, int K, long long lda,
+                                                   long long ldb, long long ldc, float alpha,
+                                                   const float* __restrict__ bias) {
+  using G = Gemm8Cfg<256>;
+  constexpr int BN = 256;
+  constexpr int NS = (sizeof(TC) == 2 ? 1 : 2) * G::FM * G::FN / 2;  // epilogue stores per lane
+  constexpr int WBASE = G::GA + 2 * G::GB;  // DMAs younger than K-tile u+1 at the phase-2 wait
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  bf16* lds = (bf16*)smem;
+  float* bias_lds = (float*)(smem + 2 * G::STAGE * 2);  // [tile parity][copy][256]
+  const int tm = M / 256, tn = N / BN, nblk = tm * tn, nt = K / 64;
+  const int ntile = (nblk - (int)blockIdx.x + (int)gridDim.x - 1) / (int)gridDim.x;
+  const int nstream = ntile * nt;
+  const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int wr = wid / G::WN, wc = wid % G::WN;
+  const int w8 = __builtin_amdgcn_readfirstlane(wid);
+  const bool has_bias = bias != nullptr;
+
+  // tile j of this workgroup -> (m0, n0): XCD-contiguous logical ids, grouped along M
+  auto tile_of = [&](int j, int& m0, int& n0) {
+    const int pid = xcd_remap((int)blockIdx.x + j * (int)gridDim.x, nblk);
+    constexpr int GROUP = 8;
+    const int group = pid / (GROUP * tn), first_m = group * GROUP;
+    const int gsz = min(tm - first_m, GROUP);
+    m0 = (first_m + (pid % (GROUP * tn)) % gsz) * 256;
+    n0 = ((pid % (GROUP * tn)) / gsz) * BN;
+  };
+
+  // per-lane byte offsets of tile (0, 0), K-tile 0; a tile / K-tile moves them by a uniform amount
+  ConvParams cp{};
+  ConvRows cr{};
+  unsigned offA[2][G::GA], offB[2][G::GB];
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+#pragma unroll
+    for (int i = 0; i < G::GA; ++i)
+      offA[h][i] = (unsigned)((const char*)dma8_addr<TA, G::RWA, G::WA, G::GA>(A, lda, 0, M, 0, K, h, i, cp, cr) -
+                              (const char*)A);
+#pragma unroll
+    for (int i = 0; i < G::GB; ++i)
+      offB[h][i] = (unsigned)((const char*)dma8_addr<TB, G::RWB, G::WB, G::GB>(B, ldb, 0, N, 0, K, h, i, cp, cr) -
+                              (const char*)B);
+  }
+  const unsigned stepA = (unsigned)((TA == 1 ? 64 * lda : 64) * 2), stepB = (unsigned)((TB == 1 ? 64 * ldb : 64) * 2);
+  const unsigned rowA = (unsigned)(TA == 0 ? lda * 2 : 2), rowB = (unsigned)(TB == 0 ? ldb * 2 : 2);
+  const int nrA = __builtin_amdgcn_readfirstlane(
+      (int)(unsigned)min(2ull * (unsigned long long)(TA == 1 ? K : M) * (unsigned long long)lda, 0xffffffffull));
+  const int nrB = __builtin_amdgcn_readfirstlane(
+      (int)(unsigned)min(2ull * (unsigned long long)(TB == 1 ? K : N) * (unsigned long long)ldb, 0xffffffffull));
+  const auto rsA = __builtin_amdgcn_make_buffer_rsrc((void*)A, 0, nrA, 0x00020000);
+  const auto rsB = __builtin_amdgcn_make_buffer_rsrc((void*)B, 0, nrB, 0x00020000);
+  const auto rsBias = __builtin_amdgcn_make_buffer_rsrc((void*)(has_bias ? (const void*)bias : (const void*)A), 0,
+                                                        has_bias ? N * 4 : 0, 0x00020000);
+
+  f32x4 acc[G::FM][G::FN];
+#pragma unroll
+  for (int i = 0; i < G::FM; ++i)
+#pragma unroll
+    for (int j = 0; j < G::FN; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+  auto img_a = [&](int buf, int h) { return lds + buf * G::STAGE + h * G::A_HALF; };
+  auto img_b = [&](int buf, int h) { return lds + buf * G::STAGE + 2 * G::A_HALF + h * G::B_HALF; };
+  // half-tile q (A-h0, B-h0, B-h1, A-h1) of a K-tile: so* = tile delta + k-tile step (bytes)
+  auto stage = [&](auto qc, int buf, unsigned soA, unsigned soB) {
+    constexpr int q = decltype(qc)::value;
+    if constexpr (q == 0 || q == 3) {
+      constexpr int h = q == 0 ? 0 : 1;
+      bf16* img = img_a(buf, h);
+#pragma unroll
+      for (int i = 0; i < G::GA; ++i)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rsA, (__attribute__((address_space(3))) void*)(img + (w8 * G::GA + i) * 512),
+                                                 16, (int)offA[h][i], (int)soA, 0, 0);
+    } else {
+      constexpr int h = q - 1;
+      bf16* img = img_b(buf, h);
+#pragma unroll
+      for (int i = 0; i < G::GB; ++i)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rsB, (__attribute__((address_space(3))) void*)(img + (w8 * G::GB + i) * 512),
+                                                 16, (int)offB[h][i], (int)soB, 0, 0);
+    }
+  };
+  // one 256-B DMA per wave (4 B per lane): waves 0-3 land the tile's 256 bias values, waves 4-7 a
+  // second copy -- every wave issues exactly one, so the counted waits stay uniform
+  auto stage_bias = [&](int par, int n0) {
+    float* dst = bias_lds + (par * 2 + (w8 >> 2)) * 256 + (w8 & 3) * 64;
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rsBias, (__attribute__((address_space(3))) void*)dst, 4,
+                                             lane * 4 + (w8 & 3) * 256, n0 * 4, 0, 0);
+  };
+  using Q0 = std::integral_constant<int, 0>;
+  using Q1 = std::integral_constant<int, 1>;
+  using Q2 = std::integral_constant<int, 2>;
+  using Q3 = std::integral_constant<int, 3>;
+
+  int cj = 0, ct = 0, cm0, cn0;
+  tile_of(0, cm0, cn0);
+  // prologue: the bias and K-tiles 0, 1 of tile 0 (nt >= 4)
+  if (has_bias) stage_bias(0, cn0);
+  {
+    const unsigned a0 = cm0 * rowA, b0 = cn0 * rowB;
+    stage(Q1{}, 0, a0, b0);
+    stage(Q0{}, 0, a0, b0);
+    stage(Q2{}, 0, a0, b0);
+    stage(Q3{}, 0, a0, b0);
+    stage(Q1{}, 1, a0 + stepA, b0 + stepB);
+    stage(Q0{}, 1, a0 + stepA, b0 + stepB);
+    stage(Q2{}, 1, a0 + stepA, b0 + stepB);
+    stage(Q3{}, 1, a0 + stepA, b0 + stepB);
+    vm_wait<2 * G::GA + 2 * G::GB>();
+  }
+  // prefetch position: stream position u + 2 = (tile pj, K-tile pt)
+  int pj = 0, pt = 2, pm0 = cm0, pn0 = cn0;
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+  bf16x8 fa[G::HA][2], fb0[G::HB][2], fb1[G::HB][2];
+#pragma unroll
+  for (int g = 0; g < G::HB; ++g)
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) fb0[g][ks] = frag8<TB, G::WB>(img_b(0, 0), wc * (G::RWB / 2) + g * 16, ks);
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+  // stagger: waves 4-7 run one barrier behind waves 0-3 (see gemm_8ph); the epilogue has no barrier,
+  // so the stagger carries across tiles
+  const int grp = __builtin_amdgcn_readfirstlane(wid >> 2);
+  if (grp == 1) __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+
+#define G8P_QUAD(AH, BH, FB)                                                                              \
+  __builtin_amdgcn_s_setprio(1);                                                                          \
+  _Pragma("unroll") for (int f = 0; f < G::HA; ++f)                                                       \
+  _Pragma("unroll") for (int g = 0; g < G::HB; ++g)                                                       \
+  _Pragma("unroll") for (int ks = 0; ks < 2; ++ks)                                                        \
+    acc[AH * G::HA + f][BH * G::HB + g] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(                       \
+        FB[g][ks], fa[f][ks], acc[AH * G::HA + f][BH * G::HB + g], 0, 0, 0);                              \
+  __builtin_amdgcn_s_setprio(0)
+#define G8P_BEGIN()                                                                                       \
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");                                                      \
+  asm volatile("" ::: "memory");                                                                          \
+  __builtin_amdgcn_s_barrier();                                                                           \
+  __builtin_amdgcn_sched_barrier(0)
+#define G8P_END()                                                                                         \
+  __builtin_amdgcn_s_barrier();                                                                           \
+  asm volatile("" ::: "memory")
+
+  const int g4 = lane >> 4, lr = lane & 15;
+  for (int u = 0; u < nstream; ++u) {
+    const int buf = u & 1;
+    const bool pf = u + 2 < nstream;
+    const bool pbias = pf && pt == 0 && has_bias;
+    const bool after_epi = ct == 0 && u > 0;
+    const unsigned pa = pm0 * rowA + pt * stepA, pb = pn0 * rowB + pt * stepB;
+    // ---- phase 0: read A-h0 ; DMA [bias] B-h0(u+2) ; MFMA (A0, B0)
+#pragma unroll
+    for (int f = 0; f < G::HA; ++f)
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) fa[f][ks] = frag8<TA, G::WA>(img_a(buf, 0), wr * (G::RWA / 2) + f * 16, ks);
+    if (pf) {
+      if (pbias) stage_bias(pj & 1, pn0);
+      stage(Q1{}, buf, pa, pb);
+    }
+    G8P_BEGIN();
+    G8P_QUAD(0, 0, fb0);
+    G8P_END();
+    // ---- phase 1: read B-h1 ; DMA A-h0(u+2) ; MFMA (A0, B1)
+#pragma unroll
+    for (int g = 0; g < G::HB; ++g)
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) fb1[g][ks] = frag8<TB, G::WB>(img_b(buf, 1), wc * (G::RWB / 2) + g * 16, ks);
+    if (pf) stage(Q0{}, buf, pa, pb);
+    G8P_BEGIN();
+    G8P_QUAD(0, 1, fb1);
+    G8P_END();
+    // ---- phase 2: read A-h1 ; DMA B-h1(u+2) ; retire K-tile u+1 ; MFMA (A1, B0)
+#pragma unroll
+    for (int f = 0; f < G::HA; ++f)
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) fa[f][ks] = frag8<TA, G::WA>(img_a(buf, 1), wr * (G::RWA / 2) + f * 16, ks);
+    if (pf) {
+      stage(Q2{}, buf, pa, pb);
+      // younger than K-tile u+1: [the epilogue's stores] [the bias DMA] B-h0, A-h0, B-h1 of u+2
+      if (after_epi) {
+        if (pbias) vm_wait<WBASE + 1 + NS>(); else vm_wait<WBASE + NS>();
+      } else {
+        if (pbias) vm_wait<WBASE + 1>(); else vm_wait<WBASE>();
+      }
+    } else {
+      vm_wait<0>();
+    }
+    G8P_BEGIN();
+    G8P_QUAD(1, 0, fb0);
+    G8P_END();
+    // ---- phase 3: read B-h0 of u+1 (retired in phase 2) ; DMA A-h1(u+2) ; MFMA (A1, B1)
+    if (u + 1 < nstream) {
+#pragma unroll
+      for (int g = 0; g < G::HB; ++g)
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks)
+          fb0[g][ks] = frag8<TB, G::WB>(img_b(buf ^ 1, 0), wc * (G::RWB / 2) + g * 16, ks);
+    }
+    if (pf) stage(Q3{}, buf, pa, pb);
+    G8P_BEGIN();
+    G8P_QUAD(1, 1, fb1);
+    G8P_END();
+    if (pf && ++pt == nt) {
+      pt = 0;
+      if (++pj < ntile) tile_of(pj, pm0, pn0);
+    }
+    if (++ct == nt) {
+      // ---- epilogue of tile cj from registers
+      float bvs[G::FN / 2][8];
+#pragma unroll
+      for (int jp = 0; jp < G::FN / 2; ++jp) {
+        if (has_bias) {
+          // inline asm: the compiler would first wait for every outstanding LDS DMA
+          const float* bp = bias_lds + (cj & 1) * 512 + wc * G::RWB + jp * 32 + g4 * 8;
+          f32x4 b0, b1;
+          asm volatile("ds_read_b128 %0, %2\n\tds_read_b128 %1, %2 offset:16\n\ts_waitcnt lgkmcnt(0)"
+                       : "=&v"(b0), "=&v"(b1)
+                       : "v"((unsigned)(size_t)LDS_PTR(char, bp))
+                       : "memory");
+          bvs[jp][0] = b0[0]; bvs[jp][1] = b0[1]; bvs[jp][2] = b0[2]; bvs[jp][3] = b0[3];
+          bvs[jp][4] = b1[0]; bvs[jp][5] = b1[1]; bvs[jp][6] = b1[2]; bvs[jp][7] = b1[3];
+        } else {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) bvs[jp][e] = 0.f;
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < G::FM; ++i) {
+        const long long row = cm0 + wr * G::RWA + i * 16 + lr;
+#pragma unroll
+        for (int jp = 0; jp < G::FN / 2; ++jp) {
+          float v[8];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            // lane group g holds columns 4g + r of fragments 2jp / 2jp+1; after the two swaps it
+            // holds columns 8g + r and 8g + 4 + r of the pair's 32
+            const auto p = __builtin_amdgcn_permlane32_swap(__float_as_uint(acc[i][2 * jp][r]),
+                                                            __float_as_uint(acc[i][2 * jp + 1][r]), false, false);
+            const auto s = __builtin_amdgcn_permlane16_swap(p[0], p[1], false, false);
+            v[r] = __uint_as_float(s[0]);
+            v[4 + r] = __uint_as_float(s[1]);
+          }
+          TC* dst = C + row * ldc + cn0 + wc * G::RWB + jp * 32 + g4 * 8;
+          if constexpr (sizeof(TC) == 2) {
+            bf16x8 ov;
+#pragma unroll
+            for (int e = 0; e < 8; ++e) ov[e] = (bf16)(alpha * v[e] + bvs[jp][e]);
+            *(bf16x8*)dst = ov;
+          } else {
+            *(float4*)dst = make_float4(alpha * v[0] + bvs[jp][0], alpha * v[1] + bvs[jp][1],
+                                        alpha * v[2] + bvs[jp][2], alpha * v[3] + bvs[jp][3]);
+            *(float4*)(dst + 4) = make_float4(alpha * v[4] + bvs[jp][4], alpha * v[5] + bvs[jp][5],
+                                              alpha * v[6] + bvs[jp][6], alpha * v[7] + bvs[jp][7]);
+          }
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < G::FM; ++i)
+#pragma unroll
+        for (int j = 0; j < G::FN; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+      ct = 0;
+      if (++cj < ntile) tile_of(cj, cm0, cn0);
+    }
+  }
+#undef G8P_QUAD
+#undef G8P_BEGIN
+#undef G8P_END
+  if (grp == 0) __builtin_amdgcn_s_barrier();  // re-align the barrier counts before exit
+}
+
 template <typename TC>
 __global__ __launch_bounds__(256) void splitk_reduce(const float* __restrict__ part, int splits, TC* __restrict__ C,
                                                      int M, int N, long long ldc, EpiParams ep) {
@@ -1555,6 +1849,13 @@ static Plan8 plan_8ph(int ta, int M, int N, int K, int batch, bool gn_prologue, 
   return p;
 }
 
+// gemm_8pp routing: -1 = from UVA_8PP (default 0), 0 off, 1 on (uva_gemm_set_8pp)
+static int g_8pp_mode = -1;
+extern "C" int uva_gemm_set_8pp(int on) {
+  g_8pp_mode = on ? 1 : 0;
+  return 0;
+}
+
 // 8-phase 256-row kernel: returns 1 if launched, 0 if the shape is not for it, <0 on error
 template <typename TC>
 static int launch_8ph(int ta, int tb, const void* A, const void* B, void* C, int M, int N, int K, long long lda,
@@ -1584,6 +1885,38 @@ static int launch_8ph(int ta, int tb, const void* A, const void* B, void* C, int
   };
   const bool fast = fast_env && ta != 2 && M % 256 == 0 && N % bn == 0 && K % 64 == 0 && batch == 1 &&
                     span(ta, M, K, lda) < 4.0e9 && span(tb, N, K, ldb) < 4.0e9;
+  // persistent variant (gemm_8pp): fast-path shapes with an alpha (+ bias) epilogue, >= 4 K-tiles
+  if (g_8pp_mode < 0) g_8pp_mode = env_int("UVA_8PP", 0);
+  const int pp_env = g_8pp_mode;  // opt-in: measured equal to gemm_8ph (the stores of all CUs still burst together)
+  const bool plain_epi = !ep.residual && !ep.gate && !ep.aux && ep.act == 0 && ep.drop_thresh == 0 && ep.beta == 0.f;
+  if (pp_env && fast && bn == 256 && splits == 1 && K >= 256 && plain_epi && ldc % 8 == 0 &&
+      ((uintptr_t)C % 16) == 0 && ((uintptr_t)ep.bias % 16) == 0) {
+    static int ncu = 0;
+    if (!ncu) {
+      int dev = 0;
+      (void)hipGetDevice(&dev);
+      if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0) ncu = 256;
+    }
+    const int lb = 2 * Gemm8Cfg<256>::STAGE * 2 + 4 * 256 * 4;
+    const dim3 pgrid((unsigned)(nblk < ncu ? nblk : ncu));
+#define GPP(a, b)                                                                                           \
+  do {                                                                                                      \
+    static bool attr = false;                                                                               \
+    if (!attr) {                                                                                            \
+      (void)hipFuncSetAttribute((const void*)gemm_8pp<a, b, TC>, hipFuncAttributeMaxDynamicSharedMemorySize, lb); \
+      attr = true;                                                                                          \
+    }                                                                                                       \
+    gemm_8pp<a, b, TC><<<pgrid, 512, lb, s>>>((const bf16*)A, (const bf16*)B, (TC*)C, M, N, K, lda, ldb, ldc, \
+                                              ep.alpha, ep.bias);                                           \
+  } while (0)
+    if (ta == 0 && tb == 0) GPP(0, 0);
+    else if (ta == 0 && tb == 1) GPP(0, 1);
+    else if (ta == 1 && tb == 0) GPP(1, 0);
+    else GPP(1, 1);
+#undef GPP
+    UVA_LAUNCH_CHECK();
+    return 1;
+  }
 #define G8(a, b, BNV) do { if (fast) G8X(a, b, BNV, 256); else G8X(a, b, BNV, 0); } while (0)
 #define G8B(a, b) do { if (bn == 256) G8(a, b, 256); else G8(a, b, 128); } while (0)
   static const int var = env_int("UVA_8PH_VAR", 0);
