@@ -25,3 +25,11 @@ for kw in ({}, dict(bias=bias, residual=res, gn_part=part)):
     st = buf.reshape(16, 8, 4).astype(np.float64)
     print(f"{'plain' if not kw else 'bias+res+gnstats'} {H}x{H} Ci{Ci} Co{Co}: prologue {st[..., 0].mean():.0f}  "
           f"loop {st[..., 1].mean():.0f}  epilogue {st[..., 2].mean():.0f} ticks")
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(10):
+        ops.conv2d(x, w, out, n, H, H, Ci, Co, 3, 1, 1, 1, H, H, **kw)
+    e1.record()
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / 10
+    print(f"   {ms:.3f} ms/launch  {2 * n * H * H * 9 * Ci * Co / ms / 1e9:.0f} TF", flush=True)

@@ -36,7 +36,7 @@
 // TR = tile rows: 16 (512 threads, 1 workgroup / CU) or 8 (256 threads, 2 workgroups / CU: the two
 // co-resident tiles drift apart, so one tile's prologue / epilogue HBM traffic runs under the
 // other's MFMA loop instead of every CU loading and storing in lockstep)
-template <int BN, int TR>
+template <int BN, int TR, bool R3 = false, bool HD = false>
 struct ConvHCfg {
   static constexpr int NTH = TR * 32, NW = NTH / 64;
   static constexpr int WN = 2, WM = NW / WN;    // BN = 128: waves of 64 px x 64 co
@@ -44,11 +44,18 @@ struct ConvHCfg {
   static constexpr int FN = BN / WN / 16;       // 16-channel fragments per wave
   static constexpr int HR = TR + 2;             // halo rows
   static constexpr int HPIX = HR * CH_W;
-  static constexpr int HALO_ELEMS = HPIX * 64;
+  // HD: the halo is staged by LDS-DMA, HD_I wave-instructions (8 pixels x 128 B each) per wave,
+  // the image padded to HPIX_P pixels
+  static constexpr int HD_I = ((HPIX + 7) / 8 + NW - 1) / NW;
+  static constexpr int HPIX_P = HD_I * NW * 8;
+  static constexpr int HALO_ELEMS = (HD ? HPIX_P : HPIX) * 64;
   static constexpr int ROUNDS = (HPIX * 8 + NTH - 1) / NTH;
   static constexpr int BT = BN * 64;            // weight tile elements
   static constexpr int NI = BT / (NW * 512);    // DMA instructions per thread per weight tile
-  static constexpr int MAIN_BYTES = (2 * HALO_ELEMS + 2 * BT) * 2;
+  // R3: one halo buffer (restaged between chunks) and a 3-slot weight ring (DMA two steps ahead);
+  // otherwise two halo buffers and a 2-slot ring
+  static constexpr int NHB = R3 ? 1 : 2, NWB = R3 ? 3 : 2;
+  static constexpr int MAIN_BYTES = (NHB * HALO_ELEMS + NWB * BT) * 2;
   static constexpr int TP = BN + 4;             // epilogue fp32 pitch
   static constexpr int EPI_BYTES = 128 * TP * 4 + NW * (BN / 8) * 8 * 2 * 4;
   static constexpr int LDS_BYTES = MAIN_BYTES > EPI_BYTES ? MAIN_BYTES : EPI_BYTES;
@@ -80,8 +87,33 @@ __device__ __forceinline__ int ch_xcd_remap(int bid, int nblk) {
   return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + bid / 8;
 }
 
-// VAR (diagnostic builds only, 0 = production): 1 per-tile prologue / main-loop / epilogue s_memtime
-// stamps of the first 16 blocks (uva_debug_conv_stamps)
+// 16-B LDS read hidden from hipcc's wait insertion; the caller orders completion with explicit
+// s_waitcnt lgkmcnt + sched_barrier before the consumer
+__device__ __forceinline__ bf16x8 lds_read16(const bf16* p) {
+  bf16x8 v;
+  asm volatile("ds_read_b128 %0, %1" : "=v"(v) : "v"((unsigned)(size_t)LDS_PTR(char, p)) : "memory");
+  return v;
+}
+
+// s_waitcnt vmcnt(n) for the few counts the 3-slot ring can need (the immediate is compile-time);
+// an unlisted count falls back to vmcnt(0) (over-waiting is always safe)
+template <int NI, int NR, int NP>
+__device__ __forceinline__ void conv_vm_wait(int n) {
+#define CVW(V) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(V) : "memory")
+  if (n == NI + NR) CVW(NI + NR);
+  else if (n == NI + NP) CVW(NI + NP);
+  else if (n == NI) CVW(NI);
+  else if (n == NR) CVW(NR);
+  else if (n == NP) CVW(NP);
+  else CVW(0);
+#undef CVW
+}
+
+// VAR bits (UVA_CONV_VAR; production non-GN = 12, GN = 0): 1 per-tile prologue / main-loop /
+// epilogue s_memtime stamps of the first 16 blocks (uva_debug_conv_stamps); 2 one halo buffer + a
+// 3-slot weight ring (measured slower); 4 both k-halves' fragment reads issued before the MFMAs
+// (inline-asm reads, counted lgkmcnt); 8 halo staged by LDS-DMA (non-GN; no register staging,
+// zeros from the buffer descriptor's range check)
 __device__ unsigned long long g_uva_conv_stamps[16 * 8 * 4];
 template <int BN, bool GN, int VAR, int TR>
 __global__ __launch_bounds__(TR * 32, 16 / TR) void conv3x3_halo(const bf16* __restrict__ in, const bf16* __restrict__ wt,
@@ -91,12 +123,14 @@ __global__ __launch_bounds__(TR * 32, 16 / TR) void conv3x3_halo(const bf16* __r
                                                        const float* __restrict__ gn_shift, int gn_silu,
                                                        float* __restrict__ gn_part, int Nimg, int H, int W, int Ci,
                                                        int Co) {
-  using G = ConvHCfg<BN, TR>;
+  constexpr bool R3 = (VAR & 2) != 0;
+  constexpr bool HD = (VAR & 8) != 0 && !GN && !R3;
+  using G = ConvHCfg<BN, TR, R3, HD>;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   unsigned long long st0 = 0, st1 = 0, st2 = 0;
   if constexpr (VAR & 1) asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(st0)::"memory");
   bf16* halo = (bf16*)smem;
-  bf16* bimg = halo + 2 * G::HALO_ELEMS;
+  bf16* bimg = halo + G::NHB * G::HALO_ELEMS;
   const int tiles_x = W / CH_T, tiles_y = H / TR, ncb = Co / BN;
   const int nblk = Nimg * tiles_y * tiles_x * ncb;
   const int pid = ch_xcd_remap(blockIdx.x, nblk);
@@ -178,16 +212,48 @@ __global__ __launch_bounds__(TR * 32, 16 / TR) void conv3x3_halo(const bf16* __r
     }
   };
 
+  // ---- HD: halo by LDS-DMA through a per-image buffer descriptor. LDS pixel block b (8 pixels)
+  //      is wave-instruction b; lane l writes pixel 8b + l/8, slot l%8 = channel chunk
+  //      (l%8) ^ (p & 7) (the swizzle goes on the source). Pixels outside the image (and the
+  //      padding past HPIX) get an offset beyond the descriptor's range: the DMA writes zeros.
+  unsigned hoff[HD ? G::HD_I : 1];
+  __amdgpu_buffer_rsrc_t rs_in;
+  if constexpr (HD) {
+    const int img_bytes = __builtin_amdgcn_readfirstlane(H * W * Ci * 2);
+    rs_in = __builtin_amdgcn_make_buffer_rsrc((void*)(in + (long long)n * H * W * Ci), 0, img_bytes, 0x00020000);
+#pragma unroll
+    for (int i = 0; i < G::HD_I; ++i) {
+      const int p = (wid * G::HD_I + i) * 8 + (lane >> 3);
+      const int c = (lane & 7) ^ (p & 7);
+      const int hy = p / CH_W, hx = p - hy * CH_W;
+      const int ih = oh0 - 1 + hy, iw = ow0 - 1 + hx;
+      const bool ok = p < G::HPIX && ih >= 0 && ih < H && iw >= 0 && iw < W;
+      hoff[i] = ok ? (unsigned)(((ih * W + iw) * Ci + c * 8) * 2) : 0x80000000u;
+    }
+  }
+  auto halo_dma = [&](int cc, int hb) {
+    bf16* img = halo + hb * G::HALO_ELEMS;
+#pragma unroll
+    for (int i = 0; i < G::HD_I; ++i)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs_in, (__attribute__((address_space(3))) void*)(img + (wid * G::HD_I + i) * 512),
+                                               16, (int)hoff[i], cc * 128, 0, 0);
+  };
+
   f32x4 acc[G::FM][G::FN];
 #pragma unroll
   for (int i = 0; i < G::FM; ++i)
 #pragma unroll
     for (int j = 0; j < G::FN; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
 
-  // ---- prologue: weight tile 0 + halo of chunk 0
+  // ---- prologue: weight tile 0 (and 1 with the 3-slot ring) + halo of chunk 0
   dma_w(0, 0);
-  halo_load(0);
-  halo_store(0);
+  if (R3 && S > 1) dma_w(1, 1);
+  if constexpr (HD) {
+    halo_dma(0, 0);
+  } else {
+    halo_load(0);
+    halo_store(0);
+  }
   asm volatile("s_waitcnt vmcnt(0)\n\ts_waitcnt lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();
   asm volatile("" ::: "memory");
@@ -213,18 +279,70 @@ __global__ __launch_bounds__(TR * 32, 16 / TR) void conv3x3_halo(const bf16* __r
     for (int i = 0; i < NPRE; ++i) hreg[i] = *res_ptr(i);
   };
   if constexpr (VAR & 1) asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(st1)::"memory");
+  int prev_loads = 0;  // R3: global loads the previous step issued after its weight DMA
   for (int cc = 0; cc < nch; ++cc) {
-    const bf16* hcur = halo + (cc & 1) * G::HALO_ELEMS;
+    const bf16* hcur = halo + (R3 ? 0 : (cc & 1)) * G::HALO_ELEMS;
     const bool more = cc + 1 < nch;
 #pragma unroll 1
     for (int tap = 0; tap < 9; ++tap) {
       const int s = cc * 9 + tap;
-      // ring slot (s+1)&1 was last read in step s-1; every wave passed the barrier that ended it
-      if (s + 1 < S) dma_w(s + 1, (s + 1) & 1);
-      if (tap == 0 && more) halo_load(cc + 1);
-      if (tap == 0 && !more && residual) res_load();
-      const bf16* bcur = bimg + (s & 1) * G::BT;
+      int cur_loads = 0;
+      if constexpr (R3) {
+        // ring slot (s+2)%3 was last read in step s-1; every wave passed the barrier that ended it
+        if (s + 2 < S) dma_w(s + 2, (s + 2) % 3);
+      } else {
+        // ring slot (s+1)&1 was last read in step s-1; every wave passed the barrier that ended it
+        if (s + 1 < S) dma_w(s + 1, (s + 1) & 1);
+      }
+      if (tap == 0 && more) {
+        if constexpr (HD) {
+          halo_dma(cc + 1, (cc + 1) & 1);  // buffer last read in chunk cc-1
+          cur_loads = G::HD_I;
+        } else {
+          halo_load(cc + 1);
+          cur_loads = G::ROUNDS;
+        }
+      }
+      if (tap == 0 && !more && residual) {
+        res_load();
+        cur_loads = NPRE;
+      }
+      const bf16* bcur = bimg + (R3 ? s % 3 : (s & 1)) * G::BT;
       const int kh = tap / 3, kw = tap % 3;
+      if constexpr ((VAR & 4) != 0) {
+        // both k-halves' fragments issued up front: the second half's LDS reads run under the
+        // first half's MFMAs
+        // inline-asm reads (hipcc drains lgkmcnt(0) before the first MFMA otherwise): the k-half
+        // 0 MFMAs wait for the first 8 reads only, completion ordered by asm waits + sched_barrier
+        bf16x8 fa[2][G::FM], fb[2][G::FN];
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {
+          const int c = ks * 4 + fk;
+#pragma unroll
+          for (int f = 0; f < G::FM; ++f) {
+            const int p = (wm * G::FM + f + kh) * CH_W + frow + kw;
+            fa[ks][f] = lds_read16(hcur + p * 64 + ((c ^ (p & 7)) << 3));
+          }
+#pragma unroll
+          for (int g = 0; g < G::FN; ++g) {
+            const int r = wn * (G::FN * 16) + g * 16 + frow;
+            fb[ks][g] = lds_read16(bcur + r * 64 + ((c ^ (r & 7)) << 3));
+          }
+        }
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {
+          if (ks == 0) asm volatile("s_waitcnt lgkmcnt(%0)" ::"n"(G::FM + G::FN) : "memory");
+          else asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+          __builtin_amdgcn_sched_barrier(0);
+          __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+          for (int f = 0; f < G::FM; ++f)
+#pragma unroll
+            for (int g = 0; g < G::FN; ++g)
+              acc[f][g] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[ks][f], fb[ks][g], acc[f][g], 0, 0, 0);
+          __builtin_amdgcn_s_setprio(0);
+        }
+      } else {
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks) {
         const int c = ks * 4 + fk;
@@ -247,10 +365,40 @@ __global__ __launch_bounds__(TR * 32, 16 / TR) void conv3x3_halo(const bf16* __r
             acc[f][g] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[f], fb[g], acc[f][g], 0, 0, 0);
         __builtin_amdgcn_s_setprio(0);
       }
-      if (tap == 8 && more) halo_store((cc + 1) & 1);  // buffer last read in chunk cc-1
-      asm volatile("s_waitcnt vmcnt(0)\n\ts_waitcnt lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_barrier();
-      asm volatile("" ::: "memory");
+      }
+      if constexpr (R3) {
+        // wait for weight tile s+1 only: younger are [this step's W(s+2) DMA] and the global loads
+        // issued after W(s+1) -- by the previous step (after its DMA) and by this one. The halo
+        // loads of tap 0 so stay in flight until the end of tap 2 (the vector-memory counter
+        // retires in issue order); the last step drains everything for the epilogue
+        const int younger = s + 1 < S ? prev_loads + (s + 2 < S ? G::NI : 0) + cur_loads : 0;
+        conv_vm_wait<G::NI, G::ROUNDS, NPRE>(younger);
+        prev_loads = cur_loads;
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        if (tap == 8 && more) {
+          // single halo buffer: every wave is done with chunk cc (barrier above); restage it
+          halo_store(0);
+          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+          __builtin_amdgcn_s_barrier();
+          asm volatile("" ::: "memory");
+        }
+      } else if constexpr (HD) {
+        // weight tile s+1 only: tap 0's halo DMA / residual loads (issued after it) may stay in
+        // flight one more step; every other step drains (its weight DMA is the youngest)
+        if (cur_loads == G::HD_I) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(G::HD_I) : "memory");
+        else if (cur_loads == NPRE) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NPRE) : "memory");
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+      } else {
+        if (tap == 8 && more) halo_store((cc + 1) & 1);  // buffer last read in chunk cc-1
+        asm volatile("s_waitcnt vmcnt(0)\n\ts_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+      }
     }
   }
 
@@ -395,7 +543,7 @@ extern "C" int uva_conv3x3_halo(const void* in, const void* w, void* out, const 
 #define CH_LAUNCH(BNV, GNV, VARV, TRV)                                                                         \
   do {                                                                                                         \
     static bool attr = false;                                                                                  \
-    const int lb = ConvHCfg<BNV, TRV>::LDS_BYTES;                                                              \
+    const int lb = ConvHCfg<BNV, TRV, ((VARV) & 2) != 0, ((VARV) & 8) != 0 && !(GNV) && !((VARV) & 2)>::LDS_BYTES; \
     if (!attr) {                                                                                               \
       (void)hipFuncSetAttribute((const void*)conv3x3_halo<BNV, GNV, VARV, TRV>,                               \
                                 hipFuncAttributeMaxDynamicSharedMemorySize, lb);                               \
@@ -405,15 +553,25 @@ extern "C" int uva_conv3x3_halo(const void* in, const void* w, void* out, const 
         (const bf16*)in, (const bf16*)w, (bf16*)out, bias, (const bf16*)residual, gn_scale, gn_shift, gn_silu, \
         gn_part, Nimg, H, W, Ci, Co);                                                                          \
   } while (0)
-  static const int var = getenv("UVA_CONV_VAR") ? atoi(getenv("UVA_CONV_VAR")) : 0;
+  // production (non-GN): 12 = halo by LDS-DMA (8) + both k-halves' fragment reads issued up front (4)
+  static const int var = getenv("UVA_CONV_VAR") ? atoi(getenv("UVA_CONV_VAR")) : 12;
   if (tr == 16) {
     if (gn_scale) CH_LAUNCH(128, true, 0, 16);
     else if (var == 1) CH_LAUNCH(128, false, 1, 16);
-    else CH_LAUNCH(128, false, 0, 16);
+    else if (var == 0) CH_LAUNCH(128, false, 0, 16);
+    else CH_LAUNCH(128, false, 12, 16);
   } else {
     if (gn_scale) CH_LAUNCH(128, true, 0, 8);
     else if (var == 1) CH_LAUNCH(128, false, 1, 8);
-    else CH_LAUNCH(128, false, 0, 8);
+    else if (var == 2) CH_LAUNCH(128, false, 2, 8);
+    else if (var == 3) CH_LAUNCH(128, false, 3, 8);
+    else if (var == 4) CH_LAUNCH(128, false, 4, 8);
+    else if (var == 6) CH_LAUNCH(128, false, 6, 8);
+    else if (var == 8) CH_LAUNCH(128, false, 8, 8);
+    else if (var == 12) CH_LAUNCH(128, false, 12, 8);
+    else if (var == 13) CH_LAUNCH(128, false, 13, 8);
+    else if (var == 0) CH_LAUNCH(128, false, 0, 8);
+    else CH_LAUNCH(128, false, 12, 8);
   }
 #undef CH_LAUNCH
   UVA_LAUNCH_CHECK();
