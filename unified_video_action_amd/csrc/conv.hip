@@ -294,6 +294,7 @@ __global__ __launch_bounds__(TR * 32, 16 / TR) void conv3x3_halo(const bf16* __r
         // ring slot (s+1)&1 was last read in step s-1; every wave passed the barrier that ended it
         if (s + 1 < S) dma_w(s + 1, (s + 1) & 1);
       }
+      __builtin_amdgcn_sched_barrier(0);  // counted waits below: the weight DMA is issued first
       if (tap == 0 && more) {
         if constexpr (HD) {
           halo_dma(cc + 1, (cc + 1) & 1);  // buffer last read in chunk cc-1
