@@ -33,7 +33,9 @@ def _stored(op, t_flag):
 
 CASES = [(5376, 3072, 328, 256), (5000, 3000, 136, 256), (6144, 2048, 200, 256),
          # > 256 tiles: persistent blocks walk 3 tiles each, cross-tile K-tile-0 prefetch (ragged M, K tail)
-         (16296, 3072, 328, 256), (16384, 3072, 256, 256)]
+         (16296, 3072, 328, 256), (16384, 3072, 256, 256),
+         # N = 768: the 128x384 tile (ragged M and K tail; full tiles on the fast path)
+         (32000, 768, 328, 384), (32768, 768, 3072, 384)]
 
 
 @pytest.mark.parametrize("odt", [torch.float32, torch.bfloat16])
@@ -91,11 +93,11 @@ def test_gemm8_splitk_dw_accumulate(M, N, K, splits):
     assert rel_err(g, ref) < 1e-4  # exact bf16 products, fp32 partial sums over 8-16k terms
 
 
-@pytest.mark.parametrize("M", [5376, 16384])  # 16384: 768 tiles -> persistent blocks
-def test_gemm8_epilogues(M):
+@pytest.mark.parametrize("M,N,K,bn", [(5376, 3072, 256, 256), (16384, 3072, 256, 256),
+                                      (32000, 768, 328, 384), (32768, 768, 768, 384)])
+def test_gemm8_epilogues(M, N, K, bn):
     from unified_video_action_amd.native import ops
-    N, K = 3072, 256
-    assert ops.gemm_plan(M, N, K) == (3, 256, 1)
+    assert ops.gemm_plan(M, N, K) == (3, bn, 1)
     x = torch.randn(M, K, device=DEV).to(torch.bfloat16)
     w = (torch.randn(N, K, device=DEV) * 0.1).to(torch.bfloat16)
     bias = torch.randn(N, device=DEV)
@@ -114,7 +116,10 @@ def test_gemm8_epilogues(M):
     assert rel_err(outd[kept], pre[kept] / 0.9) < 5e-3
     dg = torch.empty(M, N, device=DEV)
     ops.act_bwd(None, torch.ones(M, N, device=DEV), dg, "none", drop_p=0.1, seed=77)
-    assert torch.equal(dg != 0, kept)
+    # same keep pattern, except where acc + bias cancelled to exactly 0.0 (a kept zero reads as dropped:
+    # ~1 element in 25M at these sizes)
+    bad = (dg != 0) != kept
+    assert int(bad.sum()) <= 4 and (pre[bad].abs() < 1e-4).all()
     # adaLN gate (bf16, strided) + fp32 residual, fp32 out
     gate_full = torch.randn(M, 3 * N, device=DEV).to(torch.bfloat16)
     gate = gate_full[:, 2 * N:]

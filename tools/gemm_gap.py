@@ -15,10 +15,12 @@ SHAPES = {  # name: (kind, N_out, K_in)
 }
 
 
-def run():
+def run(modes=("kernels", "library", "tuned"), only=None):
     dev = "cuda"
     print(f"{'shape':>8} {'op':>3} {'M':>6} {'N':>6} {'K':>6}  {'plan':>14}  {'own TF':>7} {'lib TF':>7} {'tuned TF':>8}")
     for name, (No, Ki) in SHAPES.items():
+        if only and name not in only:
+            continue
         x = torch.randn(M, Ki, device=dev).to(torch.bfloat16)
         w = torch.randn(No, Ki, device=dev).to(torch.bfloat16)
         b = torch.randn(No, device=dev)
@@ -31,13 +33,18 @@ def run():
                             ("dx", lambda: ops.linear_dx(dy, w, dx), (M, Ki, No, 0, 1)),
                             ("dw", lambda: ops.linear_dw(dy, x, dw), (No, Ki, M, 1, 1))):
             res = {}
-            for mode in ("kernels", "library", "tuned"):
+            for mode in modes:
                 with ops.gemm_library(mode):
                     res[mode] = fl / timeit(fn) / 1e9
             kern, bn, splits = ops.gemm_plan(shp[0], shp[1], shp[2], shp[3], shp[4])
             print(f"{name:>8} {op:>3} {shp[0]:>6} {shp[1]:>6} {shp[2]:>6}  k{kern} bn{bn:>3} s{splits:>2}     "
-                  f"{res['kernels']:7.0f} {res['library']:7.0f} {res['tuned']:8.0f}", flush=True)
+                  " ".join(f"{res[m]:7.0f}" for m in modes), flush=True)
 
 
 if __name__ == "__main__":
-    run()
+    import argparse
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--modes", default="kernels,library,tuned")
+    ap.add_argument("--only", default="")
+    a = ap.parse_args()
+    run(tuple(a.modes.split(",")), set(a.only.split(",")) if a.only else None)

@@ -52,9 +52,18 @@ __device__ __forceinline__ bf16x8 lds_tr_frag(const bf16* lds, int rowA, int row
   return __builtin_bit_cast(bf16x8, v);
 }
 
+// two f32 -> one dword of two bf16 (RNE, as the (bf16) cast): one v_cvt_pk_bf16_f32 per pair.  Plain
+// casts of individually masked values compiled to one cvt per element + a v_perm per pair.
+// (a vector conversion, not inline asm: the result feeds MFMAs, whose operand hazards hipcc only
+// tracks for instructions it emitted itself)
+typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2;
+__device__ __forceinline__ uint32_t cvt_pk_bf16(float lo, float hi) {
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2){lo, hi}, bf16x2));
+}
+typedef __attribute__((ext_vector_type(4))) uint32_t u32x4;
 __device__ __forceinline__ bf16x8 pack_pi(const f32x4& a, const f32x4& b) {
-  bf16x8 r = {(bf16)a[0], (bf16)a[1], (bf16)a[2], (bf16)a[3], (bf16)b[0], (bf16)b[1], (bf16)b[2], (bf16)b[3]};
-  return r;
+  const u32x4 u = {cvt_pk_bf16(a[0], a[1]), cvt_pk_bf16(a[2], a[3]), cvt_pk_bf16(b[0], b[1]), cvt_pk_bf16(b[2], b[3])};
+  return __builtin_bit_cast(bf16x8, u);
 }
 
 __device__ __forceinline__ f32x4 mfma16(const bf16x8& a, const bf16x8& b, const f32x4& c) {
@@ -98,9 +107,25 @@ __device__ __forceinline__ float exp2_fast(float x) { return __builtin_amdgcn_ex
 __device__ __forceinline__ float keep_and(float v, uint32_t w, int b) {
   return __int_as_float(__float_as_int(v) & __builtin_amdgcn_sbfe(w, b, 1));
 }
+// the same as two instructions (v_bfe_i32 + v_and_b32): from the builtin form hipcc derives a bit test
+// + v_cmp + v_cndmask (three) in the forward and dQ loops
+__device__ __forceinline__ float keep_bfe(float v, uint32_t w, int b) {
+  int m;
+  asm("v_bfe_i32 %0, %1, %2, 1" : "=v"(m) : "v"(w), "s"(b));
+  return __int_as_float(__float_as_int(v) & m);
+}
 // max of two MFMA outputs without the canonicalising v_max hipcc inserts in front of fmaxf
 // (med3(a, b, +inf) == max(a, b); the compiler fuses chains of it into v_max3_f32)
 __device__ __forceinline__ float fmax_nc(float a, float b) { return __builtin_amdgcn_fmed3f(a, b, INFINITY); }
+// max over lanes l, l^16, l^32, l^48 by v_permlane16/32_swap (VALU) instead of two ds_bpermute.
+// Builtins only: an inline-asm producer is invisible to hipcc's permlane / trans / MFMA hazard
+// wait-state insertion (an asm v_max feeding the second swap read a stale register).
+__device__ __forceinline__ float quad_max(float v) {
+  auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  v = fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+  r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
 // position of element k (0..63) of a 64-wide tile inside an MQ / MK word (an involution)
 __host__ __device__ constexpr int mask_pos(int k) { return ((k >> 2) & 3) * 16 + (k >> 4) * 4 + (k & 3); }
 
@@ -251,13 +276,15 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(const bf16* __restrict
     bool need = false;
 #pragma unroll
     for (int qt = 0; qt < 2; ++qt) {
+      // (the lane's scores come straight from the MFMAs: inline-asm VALU on them would bypass the
+      // compiler's MFMA-result hazard wait states, so this chain stays on builtins -- hipcc fuses it
+      // into v_max3_f32)
       float a = fmax_nc(s[0][qt][0], s[0][qt][1]);
 #pragma unroll
       for (int kt = 0; kt < NKT; ++kt)
 #pragma unroll
         for (int r = (kt == 0 ? 2 : 0); r < 4; ++r) a = fmax_nc(a, s[kt][qt][r]);
-      a = fmaxf(a, __shfl_xor(a, 16, 64));
-      a = fmaxf(a, __shfl_xor(a, 32, 64));
+      a = quad_max(a);
       mx[qt] = a * c;
       need |= mx[qt] > m[qt] + 8.0f;
     }
@@ -276,14 +303,16 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(const bf16* __restrict
 #pragma unroll
     for (int qt = 0; qt < 2; ++qt) {
       const float nm = -m[qt];
+      float ps[4] = {0.f, 0.f, 0.f, 0.f};  // four independent partial row sums
 #pragma unroll
       for (int kt = 0; kt < NKT; ++kt)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const float p = exp2_fast(fmaf(s[kt][qt][r], c, nm));
-          rs[qt] += p;
-          s[kt][qt][r] = DROP ? keep_and(p, mw[qt][kt >> 2], (kt & 3) * 4 + r) : p;
+          ps[r] += p;
+          s[kt][qt][r] = DROP ? keep_bfe(p, mw[qt][kt >> 2], (kt & 3) * 4 + r) : p;
         }
+      rs[qt] += (ps[0] + ps[1]) + (ps[2] + ps[3]);
     }
 #pragma unroll
     for (int ks = 0; ks < KT / 32; ++ks) {
@@ -614,7 +643,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(const bf16* __restr
         for (int r = 0; r < 4; ++r) {
           const float p = exp2_fast(fmaf(s[kt][qt][r], c, -L[qt]));
           float dpt = dp[kt][qt][r];
-          if (DROP) dpt = keep_and(dpt, mw[qt], kt * 4 + r);
+          if (DROP) dpt = keep_bfe(dpt, mw[qt], kt * 4 + r);
           s[kt][qt][r] = p * (dpt - Dq[qt]);
         }
 #pragma unroll

@@ -48,7 +48,7 @@ LtState& lt_state(int dev) {
 
 constexpr size_t kLtWorkspace = 64ull << 20;
 
-int g_lt_mode = -1;  // -1: from UVA_GEMM_LIB (default 1)
+int g_lt_mode = -1;  // -1: from UVA_GEMM_LIB (default 0: the hand-written kernels only)
 
 LtKey key_of(const LtShape& s) {
   return LtKey{s.out_dtype, s.ta, s.tb, s.M, s.N, s.K, s.lda, s.ldb, s.ldc, s.beta_nonzero, s.bias};
@@ -146,7 +146,7 @@ extern "C" int uva_lt_mode(int mode) {
 extern "C" int uva_lt_enabled() {
   if (g_lt_mode < 0) {
     const char* e = getenv("UVA_GEMM_LIB");
-    g_lt_mode = e ? atoi(e) : 1;
+    g_lt_mode = e ? atoi(e) : 0;
   }
   return g_lt_mode;
 }

@@ -109,7 +109,8 @@ __device__ __forceinline__ void conv_vm_wait(int n) {
 #undef CVW
 }
 
-// VAR bits (UVA_CONV_VAR; production non-GN = 12, GN = 0): 1 per-tile prologue / main-loop /
+// VAR bits (UVA_CONV_VAR / UVA_CONV_GN_VAR; production non-GN = 12, GN = 0): 16 the next chunk's
+// halo staging spread over taps 1..ROUNDS (one round per step); 1 per-tile prologue / main-loop /
 // epilogue s_memtime stamps of the first 16 blocks (uva_debug_conv_stamps); 2 one halo buffer + a
 // 3-slot weight ring (measured slower); 4 both k-halves' fragment reads issued before the MFMAs
 // (inline-asm reads, counted lgkmcnt); 8 halo staged by LDS-DMA (non-GN; no register staging,
@@ -125,6 +126,8 @@ __global__ __launch_bounds__(TR * 32, 16 / TR) void conv3x3_halo(const bf16* __r
                                                        int Co) {
   constexpr bool R3 = (VAR & 2) != 0;
   constexpr bool HD = (VAR & 8) != 0 && !GN && !R3;
+  constexpr bool SPREAD = (VAR & 16) != 0 && !HD && !R3;  // halo staging spread over taps 1..ROUNDS
+  static_assert(!SPREAD || ConvHCfg<BN, TR>::ROUNDS <= 8, "one staging round per tap 1..8");
   using G = ConvHCfg<BN, TR, R3, HD>;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   unsigned long long st0 = 0, st1 = 0, st2 = 0;
@@ -181,10 +184,9 @@ __global__ __launch_bounds__(TR * 32, 16 / TR) void conv3x3_halo(const bf16* __r
       gsh[0] = h0.x; gsh[1] = h0.y; gsh[2] = h0.z; gsh[3] = h0.w; gsh[4] = h1.x; gsh[5] = h1.y; gsh[6] = h1.z; gsh[7] = h1.w;
     }
   };
-  auto halo_store = [&](int hb) {
+  auto halo_store_round = [&](int hb, int i) __attribute__((always_inline)) {
     bf16* img = halo + hb * G::HALO_ELEMS;
-#pragma unroll
-    for (int i = 0; i < G::ROUNDS; ++i) {
+    {
       const int p = (tid + i * G::NTH) >> 3;
       if (p < G::HPIX) {
         const int hy = p / CH_W, hx = p - hy * CH_W;
@@ -210,6 +212,10 @@ __global__ __launch_bounds__(TR * 32, 16 / TR) void conv3x3_halo(const bf16* __r
         *(bf16x8*)(img + p * 64 + ((hc ^ (p & 7)) << 3)) = v;
       }
     }
+  };
+  auto halo_store = [&](int hb) __attribute__((always_inline)) {
+#pragma unroll
+    for (int i = 0; i < G::ROUNDS; ++i) halo_store_round(hb, i);
   };
 
   // ---- HD: halo by LDS-DMA through a per-image buffer descriptor. LDS pixel block b (8 pixels)
@@ -394,6 +400,22 @@ __global__ __launch_bounds__(TR * 32, 16 / TR) void conv3x3_halo(const bf16* __r
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();
         asm volatile("" ::: "memory");
+      } else if constexpr (SPREAD) {
+        // the next chunk's GN + SiLU staging spread over taps 1..ROUNDS, one round per step after
+        // this step's MFMAs.  Measured SLOWER than the one burst at tap 8 (level-0 conv 7.12 vs
+        // 6.85 ms, same box): the co-resident workgroup already runs its MFMAs under the burst.
+        // The halo loads of tap 0 were issued after W(s+1): only they may stay in flight
+        if (more) {
+#pragma unroll
+          for (int i = 0; i < G::ROUNDS; ++i)
+            if (tap == 1 + i) halo_store_round((cc + 1) & 1, i);  // buffer last read in chunk cc-1
+        }
+        if (cur_loads == G::ROUNDS) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(G::ROUNDS) : "memory");
+        else if (cur_loads == NPRE) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NPRE) : "memory");
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
       } else {
         if (tap == 8 && more) halo_store((cc + 1) & 1);  // buffer last read in chunk cc-1
         asm volatile("s_waitcnt vmcnt(0)\n\ts_waitcnt lgkmcnt(0)" ::: "memory");
@@ -556,14 +578,19 @@ extern "C" int uva_conv3x3_halo(const void* in, const void* w, void* out, const 
   } while (0)
   // production (non-GN): 12 = halo by LDS-DMA (8) + both k-halves' fragment reads issued up front (4)
   static const int var = getenv("UVA_CONV_VAR") ? atoi(getenv("UVA_CONV_VAR")) : 12;
+  static const int gvar = getenv("UVA_CONV_GN_VAR") ? atoi(getenv("UVA_CONV_GN_VAR")) : 0;
   if (tr == 16) {
     if (gn_scale) CH_LAUNCH(128, true, 0, 16);
     else if (var == 1) CH_LAUNCH(128, false, 1, 16);
     else if (var == 0) CH_LAUNCH(128, false, 0, 16);
     else CH_LAUNCH(128, false, 12, 16);
   } else {
-    if (gn_scale) CH_LAUNCH(128, true, 0, 8);
-    else if (var == 1) CH_LAUNCH(128, false, 1, 8);
+    if (gn_scale) {
+      if (gvar == 0) CH_LAUNCH(128, true, 0, 8);
+      else if (gvar == 4) CH_LAUNCH(128, true, 4, 8);
+      else if (gvar == 16) CH_LAUNCH(128, true, 16, 8);
+      else CH_LAUNCH(128, true, 20, 8);
+    } else if (var == 1) CH_LAUNCH(128, false, 1, 8);
     else if (var == 2) CH_LAUNCH(128, false, 2, 8);
     else if (var == 3) CH_LAUNCH(128, false, 3, 8);
     else if (var == 4) CH_LAUNCH(128, false, 4, 8);

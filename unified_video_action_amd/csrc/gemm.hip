@@ -950,10 +950,13 @@ __device__ __forceinline__ void conv_rows_init_8(const ConvParams& cp, int row0,
     }
 }
 
-#define EPI8_ROWS 128
+// BN = 384 is the 128 x 384 tile (N = 768 outputs: 2 x 256 row tiles fill exactly two rounds of 256
+// CUs, where 256 x 256 tiles leave the second round half empty)
 template <int BN>
 struct Gemm8Cfg {
-  static constexpr int BM = 256, WM = (BN == 256) ? 2 : 4, WN = 8 / WM;
+  static constexpr int BM = (BN == 384) ? 128 : 256, WM = (BN == 128) ? 4 : 2, WN = 8 / WM;
+  static constexpr int ER = (BN == 384) ? 64 : 128;      // epilogue rows per LDS chunk
+  static constexpr int NCH = BM / ER;                    // epilogue chunks
   static constexpr int RWA = BM / WM, RWB = BN / WN;      // rows (cols) per wave
   static constexpr int FM = RWA / 16, FN = RWB / 16;      // fragments per wave
   static constexpr int HA = FM / 2, HB = FN / 2;          // fragments per half
@@ -962,7 +965,7 @@ struct Gemm8Cfg {
   static constexpr int WA = BM / 2, WB = BN / 2;          // M-major image row widths (elements)
   static constexpr int STAGE = 2 * A_HALF + 2 * B_HALF;   // elements per K-tile stage
   static constexpr int TP = BN + 4;                       // epilogue fp32 pitch
-  static constexpr int EPI_BYTES = EPI8_ROWS * TP * 4 + 8 * 32 * 8 * 2 * 4;
+  static constexpr int EPI_BYTES = ER * TP * 4 + 8 * 32 * 8 * 2 * 4;
   static constexpr int LDS_BYTES = (2 * STAGE * 2 > EPI_BYTES) ? 2 * STAGE * 2 : EPI_BYTES;
 };
 
@@ -985,6 +988,7 @@ __global__ __launch_bounds__(512, 1) void gemm_8ph(const bf16* __restrict__ A, c
                                                    long long ldb, long long ldc, BatchStrides bs, EpiParams ep,
                                                    ConvParams cp, float* __restrict__ part, int k_per_split) {
   using G = Gemm8Cfg<BN>;
+  static_assert(BN != 384 || TA != 2, "the 128x384 tile has no conv / GN-statistics epilogue");
   extern __shared__ __attribute__((aligned(16))) char smem[];
   bf16* lds = (bf16*)smem;
   unsigned long long st_entry = 0, st_after_pro = 0, st_after_loop = 0, st_e1 = 0, st_e2 = 0;
@@ -1237,21 +1241,22 @@ __global__ __launch_bounds__(512, 1) void gemm_8ph(const bf16* __restrict__ A, c
   float* gn_part = (TA == 2) ? cp.gn_part : nullptr;
   const int lane = threadIdx.x & 63;
   constexpr int C8 = BN / 8;             // 8-column chunks per row
-  constexpr int RPP = 512 / C8;          // rows per pass
-  const int c8 = threadIdx.x % C8, rsub = threadIdx.x / C8;
+  constexpr int RPP = 512 / C8;          // rows per pass (BN = 384: 10 rows, the last 32 threads idle)
+  constexpr int ER = G::ER;
+  const int c8 = threadIdx.x % C8, rsub = (threadIdx.x / C8 < RPP) ? (int)threadIdx.x / C8 : ER;
   const int col0 = n0 + c8 * 8;
   const bool full = (col0 + 8 <= N) && (ldc % 8 == 0) && ((coff + col0) % 8 == 0);
   float bv[8];
   if (!pslab && full) epi_load_bias8(ep, col0, bv);
   const bool plain = !ep.residual && !ep.gate && !ep.aux && ep.act == 0 && ep.drop_thresh == 0 && ep.beta == 0.f;
 #pragma unroll
-  for (int chunk = 0; chunk < 2; ++chunk) {
+  for (int chunk = 0; chunk < G::NCH; ++chunk) {
     float gs_s[8], gs_q[8];
 #pragma unroll
     for (int e = 0; e < 8; ++e) gs_s[e] = gs_q[e] = 0.f;
     // waves whose rows fall in [chunk*128, chunk*128+128) write their accumulators
-    if ((wr * G::RWA) / EPI8_ROWS == chunk) {
-      const int rbase = wr * G::RWA - chunk * EPI8_ROWS;
+    if ((wr * G::RWA) / ER == chunk) {
+      const int rbase = wr * G::RWA - chunk * ER;
 #pragma unroll
       for (int i = 0; i < G::FM; ++i)
 #pragma unroll
@@ -1264,15 +1269,16 @@ __global__ __launch_bounds__(512, 1) void gemm_8ph(const bf16* __restrict__ A, c
     if constexpr (VAR & 128) {
       if (chunk == 0) asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(st_e1)::"memory");
     }
-    constexpr int NIT = EPI8_ROWS / RPP;
-    const int rowb = m0 + chunk * EPI8_ROWS + rsub;
+    constexpr int NIT = (ER + RPP - 1) / RPP;
+    const int rowb = m0 + chunk * ER + rsub;
+    const int rowe = min(M, m0 + chunk * ER + ER);  // rows of this chunk (rl < ER)
     // (the conv variant keeps the general loop: the GN statistics leave no registers for these)
     if (TA != 2 && !pslab && full && plain && !(VAR & 512)) {
       // alpha * acc (+ bias): no loads inside the loop, so no store ever waits for an earlier one
 #pragma unroll
       for (int it = 0; it < NIT; ++it) {
         const int row = rowb + it * RPP;
-        if (row < M) {
+        if (row < rowe) {
           const int rl = it * RPP + rsub;
           const float4 a = *(const float4*)(T + rl * G::TP + c8 * 8);
           const float4 b = *(const float4*)(T + rl * G::TP + c8 * 8 + 4);
@@ -1304,13 +1310,13 @@ __global__ __launch_bounds__(512, 1) void gemm_8ph(const bf16* __restrict__ A, c
     } else if (TA != 2 && !pslab && full && !(VAR & 512)) {
       // row it+1's inputs are loaded before row it's store (see EpiRow)
       EpiRow cur, nxt;
-      if (rowb < M) epi_load_row8<TC>(C, coff + (long long)rowb * ldc + col0, ep, roff, rowb, col0, cur);
+      if (rowb < rowe) epi_load_row8<TC>(C, coff + (long long)rowb * ldc + col0, ep, roff, rowb, col0, cur);
 #pragma unroll 1
       for (int it = 0; it < NIT; ++it) {
         const int row = rowb + it * RPP;
-        if (it + 1 < NIT && row + RPP < M)
+        if (it + 1 < NIT && row + RPP < rowe)
           epi_load_row8<TC>(C, coff + (long long)(row + RPP) * ldc + col0, ep, roff, row + RPP, col0, nxt);
-        if (row < M) {
+        if (row < rowe) {
           const int rl = it * RPP + rsub;
           const float4 a = *(const float4*)(T + rl * G::TP + c8 * 8);
           const float4 b = *(const float4*)(T + rl * G::TP + c8 * 8 + 4);
@@ -1327,10 +1333,10 @@ __global__ __launch_bounds__(512, 1) void gemm_8ph(const bf16* __restrict__ A, c
         cur = nxt;
       }
     } else
-    for (int it = 0; it < EPI8_ROWS / RPP; ++it) {
+    for (int it = 0; it < NIT; ++it) {
       const int rl = it * RPP + rsub;
-      const int row = m0 + chunk * EPI8_ROWS + rl;
-      if (row >= M || col0 >= N) break;
+      const int row = m0 + chunk * ER + rl;
+      if (row >= rowe || col0 >= N) break;
       float v[8];
       const float4 a = *(const float4*)(T + rl * G::TP + c8 * 8);
       const float4 b = *(const float4*)(T + rl * G::TP + c8 * 8 + 4);
@@ -1382,7 +1388,7 @@ __global__ __launch_bounds__(512, 1) void gemm_8ph(const bf16* __restrict__ A, c
             gs_q[e] += __shfl_xor(gs_q[e], o, 64);
           }
         }
-        float* red = T + EPI8_ROWS * G::TP;  // [8 waves][C8][8][2]
+        float* red = T + ER * G::TP;  // [8 waves][C8][8][2]
         if (lane < C8) {
 #pragma unroll
           for (int e = 0; e < 8; ++e) {
@@ -1393,7 +1399,7 @@ __global__ __launch_bounds__(512, 1) void gemm_8ph(const bf16* __restrict__ A, c
         if constexpr (VAR & 64) __syncthreads(); else epi_lds_barrier();
         const int gsz = N / 32;
         const int ngroups = min(BN, N - n0) / gsz;
-        if ((int)threadIdx.x < ngroups && m0 + chunk * EPI8_ROWS < M) {
+        if ((int)threadIdx.x < ngroups && m0 + chunk * ER < M) {
           float sum = 0.f, sq = 0.f;
           for (int c = threadIdx.x * gsz; c < ((int)threadIdx.x + 1) * gsz; ++c)
             for (int w = 0; w < 8; ++w) {
@@ -1809,24 +1815,32 @@ struct Plan8 {
 static Plan8 plan_8ph(int ta, int M, int N, int K, int batch, bool gn_prologue, bool have_ws, long long ws_floats) {
   static const int mode = env_int("UVA_GEMM_8PH", 1);          // 0 off, 1 auto, 2 force BN=128, 3 force BN=256
   static const int f128 = env_int("UVA_8PH_BN128_PCT", 90);    // relative per-CU efficiency of BN=128
+  static const int f384 = env_int("UVA_8PH_BN384_PCT", 85);    // ... of the 128x384 tile
   Plan8 p{0, 1, K, 0};
   if (mode == 0 || M < 256 || N < 128 || (ta == 2 && gn_prologue)) return p;
-  auto tiles = [&](int bn) { return (long long)((M + 255) / 256) * ((N + bn - 1) / bn); };
+  auto bm_of = [](int bn) { return bn == 384 ? 128 : 256; };
+  auto tiles = [&](int bn) { return (long long)((M + bm_of(bn) - 1) / bm_of(bn)) * ((N + bn - 1) / bn); };
+  // work per CU-round, relative: tile occupancy of the last round x useful fraction of each tile
   auto score = [&](int bn) {
     long long t = tiles(bn) * batch;
     long long rounds = (t + 255) / 256;
     double occ = (double)t / (double)(rounds * 256);
-    double useful = (double)M * N / ((double)((M + 255) / 256) * 256 * ((N + bn - 1) / bn) * bn);
-    return occ * useful * (bn == 128 ? f128 / 100.0 : 1.0);
+    double useful = (double)M * N / ((double)tiles(bn) * bm_of(bn) * bn);
+    return occ * useful * (bn == 128 ? f128 / 100.0 : bn == 384 ? f384 / 100.0 : 1.0);
   };
   const bool splitk_regime = batch == 1 && have_ws && tiles(128) < 128 && K >= 8 * 64;
   // measured (tools_kbench.py): BN=256 beats the 128x128 LDS-DMA kernel on every UVA shape it is
   // chosen for; BN=128 does not yet, so it is opt-in (UVA_GEMM_8PH=2) and auto mode falls back
   int bn = 128;
+  // the 128x384 tile: plain products (no conv view), N a multiple of 384, off the split-K regime
+  const bool ok384 = ta != 2 && N % 384 == 0 && !splitk_regime && f384 > 0;
   if (mode == 3) bn = 256;
+  else if (mode == 4) bn = ok384 ? 384 : 256;
   else if (mode == 1) {
-    if (N < 256 || !(splitk_regime || score(256) >= score(128))) return p;
-    bn = 256;
+    // (the 128x384 tile measured faster than the 128x128 fallback kernel on every N = 768 shape)
+    if (ok384 && score(384) > score(256)) bn = 384;
+    else if (N < 256 || !(splitk_regime || score(256) >= score(128))) return p;
+    else bn = 256;
   }
   const long long nblk = tiles(bn);
   int splits = 1;
@@ -1883,7 +1897,7 @@ static int launch_8ph(int ta, int tb, const void* A, const void* B, void* C, int
   auto span = [](int t, int rows, int cols, long long ld) {  // bytes an operand's offsets can reach
     return 2.0 * ((t == 1 ? (double)cols : (double)rows) * (double)ld);
   };
-  const bool fast = fast_env && ta != 2 && M % 256 == 0 && N % bn == 0 && K % 64 == 0 && batch == 1 &&
+  const bool fast = fast_env && ta != 2 && M % (bn == 384 ? 128 : 256) == 0 && N % bn == 0 && K % 64 == 0 && batch == 1 &&
                     span(ta, M, K, lda) < 4.0e9 && span(tb, N, K, ldb) < 4.0e9;
   // persistent variant (gemm_8pp): fast-path shapes with an alpha (+ bias) epilogue, >= 4 K-tiles
   if (g_8pp_mode < 0) g_8pp_mode = env_int("UVA_8PP", 0);
@@ -1919,6 +1933,7 @@ static int launch_8ph(int ta, int tb, const void* A, const void* B, void* C, int
   }
 #define G8(a, b, BNV) do { if (fast) G8X(a, b, BNV, 256); else G8X(a, b, BNV, 0); } while (0)
 #define G8B(a, b) do { if (bn == 256) G8(a, b, 256); else G8(a, b, 128); } while (0)
+#define G8C(a, b) do { if (bn == 384) G8(a, b, 384); else G8B(a, b); } while (0)
   static const int var = env_int("UVA_8PH_VAR", 0);
 #define G8V(V)                                                                                              \
   do {                                                                                                      \
@@ -1958,11 +1973,12 @@ static int launch_8ph(int ta, int tb, const void* A, const void* B, void* C, int
   } else
 #undef G8V
   if (ta == 2 && tb == 0) G8B(2, 0);
-  else if (ta == 0 && tb == 0) G8B(0, 0);
-  else if (ta == 0 && tb == 1) G8B(0, 1);
-  else if (ta == 1 && tb == 0) G8B(1, 0);
-  else if (ta == 1 && tb == 1) G8B(1, 1);
+  else if (ta == 0 && tb == 0) G8C(0, 0);
+  else if (ta == 0 && tb == 1) G8C(0, 1);
+  else if (ta == 1 && tb == 0) G8C(1, 0);
+  else if (ta == 1 && tb == 1) G8C(1, 1);
   else return -(int)hipErrorInvalidValue;
+#undef G8C
 #undef G8B
 #undef G8
 #undef G8X

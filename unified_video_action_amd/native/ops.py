@@ -81,9 +81,10 @@ SPLITK_WS_FLOATS = 1 << 25  # 128 MB fp32 partial slabs
 
 
 class gemm_library:
-    """Route of epilogue-free bf16 GEMMs: gemm_library("kernels") -> the hand-written kernels only,
-    "tuned" -> per shape, whichever of them and the hipBLASLt heuristic's algorithms timed fastest
-    (the default), "library" -> hipBLASLt's first algorithm (library tests)."""
+    """Route of epilogue-free bf16 GEMMs: gemm_library("kernels") -> the hand-written kernels only
+    (the default; UVA_GEMM_LIB=1 selects "tuned" process-wide), "tuned" -> per shape, whichever of
+    them and the hipBLASLt heuristic's algorithms timed fastest (an A/B reference: within 1 % of the
+    kernels-only step since the 128x384 tile), "library" -> hipBLASLt's first algorithm (tests)."""
 
     MODES = {"kernels": 0, "tuned": 1, "library": 2}
 
@@ -95,7 +96,7 @@ class gemm_library:
         return self
 
     def __exit__(self, *exc):
-        lib().query("uva_lt_mode", 1 if self.prev < 0 else self.prev)
+        lib().query("uva_lt_mode", 0 if self.prev < 0 else self.prev)
 
 
 def gemm_plan(M, N, K, ta=0, tb=0, batch=1, splitk=True, gn_prologue=False, dtype=torch.bfloat16):
