@@ -1,0 +1,9 @@
+# round-2 profile: kernel trace/stats of the bench + FETCH/WRITE PMC passes + MFMA-busy PMC pass
+set -e
+export TMPDIR=/tmp
+bash tools/tools_profile_round.sh ${1:-r02}
+python3 tools/tools_traffic.py gpurun_out/prof_${1:-r02}/pmc_fetch gpurun_out/prof_${1:-r02}/pmc_write gpurun_out/prof_${1:-r02}/traffic.json > /dev/null
+bash tools/pmc_step.sh
+cp gpurun_out/pmc_mfma/mfma.json gpurun_out/prof_${1:-r02}/mfma_busy.json
+python3 -c "
+import json; d=json.load(open('gpurun_out/prof_${1:-r02}/bench.json')); print(d['value'], d['roofline'])"
