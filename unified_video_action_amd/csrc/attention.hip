@@ -496,13 +496,15 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_kernel(const bf16* __res
 #pragma unroll
         for (int kt = 0; kt < 2; ++kt) {
           const float p = exp2_fast(fmaf(s[qt][kt][r], c, -Lq[r]));
-          float pd = p, dpt = dp[qt][kt][r];
           if (DROP) {
-            pd = keep_and(p, mw[kt], qt * 4 + r);
-            dpt = keep_and(dpt, mw[kt], qt * 4 + r);
+            // dS = P (keep dP' - D) = Pd dP' - P D: one mask op (Pd) instead of two
+            const float pd = keep_bfe(p, mw[kt], qt * 4 + r);
+            s[qt][kt][r] = pd;
+            dp[qt][kt][r] = fmaf(pd, dp[qt][kt][r], -(p * Dq[r]));
+          } else {
+            s[qt][kt][r] = p;
+            dp[qt][kt][r] = p * (dp[qt][kt][r] - Dq[r]);
           }
-          s[qt][kt][r] = pd;
-          dp[qt][kt][r] = p * (dpt - Dq[r]);
         }
     }
     // dV^T[d][key] += dO'^T Pd ; dK^T[d][key] += Q^T dS      (k = q, permuted by pi)
