@@ -193,13 +193,15 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(const bf16* __restrict
   constexpr int NH = KT / 64;    // 64-key mask words per LDS tile
   __shared__ __attribute__((aligned(16))) bf16 sK[2][NH * AT_TILE];
   __shared__ __attribute__((aligned(16))) bf16 sV[2][NH * AT_TILE];
-  const int bh = blockIdx.y, b = bh / H, h = bh % H;
+  int bx, bh;
+  xcd_grid2(bx, bh);
+  const int b = bh / H, h = bh % H;
   const long long ld = 3LL * H * 64;
   const bf16* Qg = qkv + (long long)b * N * ld + h * 64;
   const bf16* Kg = Qg + H * 64;
   const bf16* Vg = Qg + 2 * H * 64;
   const int w = threadIdx.x >> 6, l = threadIdx.x & 63, g = l >> 4, li = l & 15;
-  const int q0 = blockIdx.x * 128 + w * 32;
+  const int q0 = bx * 128 + w * 32;
   const int nkv = N / KT, n64 = N / 64;
   const uint16_t* mq = DROP ? (const uint16_t*)(MQ + (long long)bh * n64 * N) : nullptr;  // [kv64][q][4 x u16]
 
@@ -413,7 +415,9 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_kernel(const bf16* __res
   __shared__ __attribute__((aligned(16))) bf16 sO[2][AT_TILE];
   __shared__ __attribute__((aligned(16))) float sL[2][64];
   __shared__ __attribute__((aligned(16))) float sD[2][64];
-  const int bh = blockIdx.y, b = bh / H, h = bh % H;
+  int bx, bh;
+  xcd_grid2(bx, bh);
+  const int b = bh / H, h = bh % H;
   const long long ld = 3LL * H * 64, ldo = (long long)H * 64;
   const bf16* Qg = qkv + (long long)b * N * ld + h * 64;
   const bf16* Kg = Qg + H * 64;
@@ -422,7 +426,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_kernel(const bf16* __res
   const float* Lg = lse2 + (long long)bh * N;
   const float* Dg = Dvec + (long long)bh * N;
   const int w = threadIdx.x >> 6, l = threadIdx.x & 63, g = l >> 4, li = l & 15;
-  const int k0 = blockIdx.x * 128 + w * 32;
+  const int k0 = bx * 128 + w * 32;
   const int nq = N / 64;
   const uint16_t* mk = DROP ? (const uint16_t*)(MK + (long long)bh * nq * N) : nullptr;  // [qb][key][4 x u16]
 
@@ -567,14 +571,16 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(const bf16* __restr
                                                              int N, int H, float scale, float c) {
   __shared__ __attribute__((aligned(16))) bf16 sK[2][AT_TILE];
   __shared__ __attribute__((aligned(16))) bf16 sV[2][AT_TILE];
-  const int bh = blockIdx.y, b = bh / H, h = bh % H;
+  int bx, bh;
+  xcd_grid2(bx, bh);
+  const int b = bh / H, h = bh % H;
   const long long ld = 3LL * H * 64, ldo = (long long)H * 64;
   const bf16* Qg = qkv + (long long)b * N * ld + h * 64;
   const bf16* Kg = Qg + H * 64;
   const bf16* Vg = Qg + 2 * H * 64;
   const bf16* dOg = dOs + (long long)b * N * ldo + h * 64;
   const int w = threadIdx.x >> 6, l = threadIdx.x & 63, g = l >> 4, li = l & 15;
-  const int q0 = blockIdx.x * 128 + w * 32;
+  const int q0 = bx * 128 + w * 32;
   const int nkv = N / 64;
   const uint16_t* mq = DROP ? (const uint16_t*)(MQ + (long long)bh * nkv * N) : nullptr;  // [kv][q][4 x u16]
 

@@ -159,7 +159,9 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_fp8_kernel(const uint8_t* __r
   __shared__ __attribute__((aligned(1024))) uint8_t smem[2 * 2 * KT * 64];
   auto sK = [&](int b) { return smem + b * 2 * KT * 64; };
   auto sV = [&](int b) { return smem + b * 2 * KT * 64 + KT * 64; };
-  const int bh = blockIdx.y, b = bh / H, h = bh % H;
+  int bx, bh;
+  xcd_grid2(bx, bh);
+  const int b = bh / H, h = bh % H;
   const int nt64 = N / 64;
   const long long ldq = 2LL * H * 64;
   const uint8_t* Qg = qk8 + (long long)b * N * ldq + h * 64;
@@ -169,7 +171,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_fp8_kernel(const uint8_t* __r
   const float* sk_ = sc + ((long long)(b * 3 + 1) * H + h) * nt64;
   const float* sv_ = sc + ((long long)(b * 3 + 2) * H + h) * nt64;
   const int tid = threadIdx.x, w = tid >> 6, l = tid & 63, g = l >> 4, li = l & 15;
-  const int q0 = blockIdx.x * 128 + w * 32;
+  const int q0 = bx * 128 + w * 32;
   const int nkv = N / KT;
   const uint16_t* mq = DROP ? (const uint16_t*)(MQ + (long long)bh * nt64 * N) : nullptr;
 

@@ -152,5 +152,18 @@ __device__ __forceinline__ float act_grad(int act, float x) {
 }
 
 // ---- launch error plumbing -----------------------------------------------------------
+// XCD-aware (x, y) of a 2-D grid.  The hardware deals linear workgroup ids (x fastest) round-robin
+// over the 8 XCDs, so the gridDim.x blocks of one y (one attention head: its K/V or Q/dO rows are
+// re-read by every one of them) would land on 8 different L2s.  The remap gives each XCD a
+// contiguous range of logical ids, so one head's blocks run back to back on one XCD's L2.
+__device__ __forceinline__ void xcd_grid2(int& bx, int& by) {
+  const int gx = gridDim.x, T = gx * gridDim.y;
+  const int L = blockIdx.y * gx + blockIdx.x;
+  const int q = T / 8, r = T % 8, x = L % 8;
+  const int Lp = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + L / 8;
+  bx = Lp % gx;
+  by = Lp / gx;
+}
+
 #define UVA_LAUNCH_CHECK() \
   do { hipError_t _e = hipGetLastError(); if (_e != hipSuccess) return (int)_e; } while (0)
