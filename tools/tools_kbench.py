@@ -117,3 +117,28 @@ def square_bench():
 
 if __name__ == "__main__" and len(sys.argv) > 1 and sys.argv[1] == "square":
     square_bench()
+
+
+def rowk_bench():
+    """HBM-bound row kernels at the Block shapes: LN fwd / bwd (fp32 residual stream, bf16 dy)."""
+    dev = "cuda"
+    M, D = 32768, 768
+    x = torch.randn(M, D, device=dev)
+    w = torch.randn(D, device=dev)
+    b = torch.randn(D, device=dev)
+    yb = torch.empty(M, D, device=dev, dtype=torch.bfloat16)
+    mean = torch.empty(M, device=dev)
+    rstd = torch.empty(M, device=dev)
+    t = timeit(lambda: ops.layernorm_fwd(x, w, b, yb, mean, rstd))
+    print(f"ln_fwd f32->bf16 [{M},{D}]: {t*1e3:.1f} us, {M*D*6/t/1e6:.0f} GB/s")
+    dy = torch.randn(M, D, device=dev).to(torch.bfloat16)
+    dxb = torch.randn(M, D, device=dev)
+    dx = torch.empty(M, D, device=dev)
+    dw = torch.zeros(D, device=dev)
+    db = torch.zeros(D, device=dev)
+    t = timeit(lambda: ops.layernorm_bwd(x, w, dy, mean, rstd, dx, False, dw=dw, db=db, dx_base=dxb, b=b))
+    print(f"ln_bwd x f32 dy bf16 +dx_base [{M},{D}] dw/db: {t*1e3:.1f} us, {M*D*14/t/1e6:.0f} GB/s")
+
+
+if __name__ == "__main__" and len(sys.argv) > 1 and sys.argv[1] == "rowk":
+    rowk_bench()

@@ -121,6 +121,31 @@ __global__ __launch_bounds__(256) void ln_fwd(const TI* __restrict__ x, const fl
 //   modulated: dscale = dy*xhat, dshift = dy  (TO, ld = ldm)
 //   affine: per-block partial sums dw_part[blk][D] = sum dy*xhat, db_part = sum dy
 // ------------------------------------------------------------------------------------
+// raw (unconverted) VEC-element vector of T: loads are issued into these and converted at first use,
+// so a row's loads can be in flight while the previous row is computed
+template <int VEC, typename T>
+struct RawVec {
+  T v[VEC];
+};
+template <int VEC, typename T>
+__device__ __forceinline__ RawVec<VEC, T> ldraw(const T* p) {
+  RawVec<VEC, T> r;
+  if constexpr (VEC == 4 && sizeof(T) == 4) {
+    *(float4*)r.v = *(const float4*)p;
+  } else if constexpr (VEC == 4 && sizeof(T) == 2) {
+    *(bf16x4*)r.v = *(const bf16x4*)p;
+  } else {
+#pragma unroll
+    for (int i = 0; i < VEC; ++i) r.v[i] = p[i];
+  }
+  return r;
+}
+
+// One wave per row, rows r0 + wid, r0 + wid + 4, ... of the block.  Software-pipelined: the next
+// row's x / dy / dx-base loads (and its mean / rstd) are issued before the current row's reductions,
+// so a wave keeps two rows of loads in flight and each row costs one memory latency, not two (the
+// dx-base read used to wait for the row's reductions).  HBM-bound: per row D * (sizeof(TI) +
+// sizeof(TD) + 4 [+ 4 dx base]) bytes read, D * 4 written.
 template <typename TI, typename TO, int VEC, int NC, typename TD>
 __global__ __launch_bounds__(256) void ln_bwd(const TI* __restrict__ x, const float* __restrict__ w,
                                               const float* __restrict__ b, const TO* __restrict__ scale, long long ldm,
@@ -138,10 +163,44 @@ __global__ __launch_bounds__(256) void ln_bwd(const TI* __restrict__ x, const fl
   for (int c = 0; c < NC; ++c)
 #pragma unroll
     for (int i = 0; i < VEC; ++i) pw[c][i] = pb[c][i] = 0.f;
+  // per-column constants of the lane (w, b) once per block
+  float wv[NC][VEC], bv[NC][VEC];
+#pragma unroll
+  for (int c = 0; c < NC; ++c) {
+    const int col0 = col_of<VEC>(c, lane, 0);
+#pragma unroll
+    for (int i = 0; i < VEC; ++i) wv[c][i] = bv[c][i] = 0.f;
+    if (col0 < D) {
+      if (w) ldv<VEC>(w + col0, wv[c]);
+      if (b) ldv<VEC>(b + col0, bv[c]);
+    }
+  }
+  const float* addsrc = dx_base ? dx_base : (accum ? dx : nullptr);  // row source added to the result
   const int r0 = blockIdx.x * rows_per_block;
   const int r1 = min(rows, r0 + rows_per_block);
-  for (int row = r0 + wid; row < r1; row += 4) {
-    const float mean = mean_in[row], rstd = rstd_in[row];
+  struct Row {
+    RawVec<VEC, TI> x[NC];
+    RawVec<VEC, TD> d[NC];
+    RawVec<VEC, float> a[NC];
+    float mean, rstd;
+  };
+  auto load_row = [&](int row, Row& R) __attribute__((always_inline)) {
+    R.mean = mean_in[row];
+    R.rstd = rstd_in[row];
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+      const int col0 = col_of<VEC>(c, lane, 0);
+      if (col0 < D) {
+        R.x[c] = ldraw<VEC>(x + (long long)row * D + col0);
+        R.d[c] = ldraw<VEC>(dy + (long long)row * D + col0);
+        if (addsrc) R.a[c] = ldraw<VEC>(addsrc + (long long)row * D + col0);
+      }
+    }
+  };
+  // one row: its loads were issued one row earlier into R; the row after next is loaded into L
+  auto process = [&](int row, const Row& R, Row& L) __attribute__((always_inline)) {
+    if (row + 4 < r1) load_row(row + 4, L);
+    const float mean = R.mean, rstd = R.rstd;
     float xh[NC][VEC], g[NC][VEC];
     float s1 = 0.f, s2 = 0.f;
 #pragma unroll
@@ -152,28 +211,25 @@ __global__ __launch_bounds__(256) void ln_bwd(const TI* __restrict__ x, const fl
         for (int i = 0; i < VEC; ++i) xh[c][i] = g[c][i] = 0.f;
         continue;
       }
-      float xv[VEC], dv[VEC], sc[VEC], wv[VEC], bv[VEC];
-      ldv<VEC>(x + (long long)row * D + col0, xv);
-      ldv<VEC>(dy + (long long)row * D + col0, dv);
+      float sc[VEC];
       if (scale) ldv<VEC>(scale + (long long)row * ldm + col0, sc);
-      if (w) ldv<VEC>(w + col0, wv);
-      if (b) ldv<VEC>(b + col0, bv);
       float ds[VEC], dsh[VEC];
 #pragma unroll
       for (int i = 0; i < VEC; ++i) {
-        xh[c][i] = (xv[i] - mean) * rstd;
+        xh[c][i] = (to_f32(R.x[c].v[i]) - mean) * rstd;
+        const float dv = to_f32(R.d[c].v[i]);
         // y_aff = xhat*w + b ; h = y_aff*(1+scale) + shift (modulated) or h = y_aff
-        float da = dv[i];
+        float da = dv;
         if (scale) {
-          float ya = w ? xh[c][i] * wv[i] + (b ? bv[i] : 0.f) : xh[c][i];
-          da = dv[i] * (1.0f + sc[i]);
-          ds[i] = dv[i] * ya;
-          dsh[i] = dv[i];
+          float ya = w ? xh[c][i] * wv[c][i] + (b ? bv[c][i] : 0.f) : xh[c][i];
+          da = dv * (1.0f + sc[i]);
+          ds[i] = dv * ya;
+          dsh[i] = dv;
         }
         if (w) {
           pw[c][i] += da * xh[c][i];
           pb[c][i] += da;
-          g[c][i] = da * wv[i];
+          g[c][i] = da * wv[c][i];
         } else {
           g[c][i] = da;
         }
@@ -191,17 +247,21 @@ __global__ __launch_bounds__(256) void ln_bwd(const TI* __restrict__ x, const fl
       int col0 = col_of<VEC>(c, lane, 0);
       if (col0 >= D) continue;
       float o[VEC];
-      float* dxr = dx + (long long)row * D + col0;
-      const bool add = accum || dx_base;
-      if (dx_base) ldv<VEC>(dx_base + (long long)row * D + col0, o);
-      else if (accum) ldv<VEC>(dxr, o);
 #pragma unroll
       for (int i = 0; i < VEC; ++i) {
         float d = rstd * (g[c][i] - m1 - xh[c][i] * m2);
-        o[i] = add ? o[i] + d : d;
+        o[i] = addsrc ? R.a[c].v[i] + d : d;
       }
-      stv<VEC>(dxr, o);
+      stv<VEC>(dx + (long long)row * D + col0, o);
     }
+  };
+  // two register sets used in turn (no copies between rows)
+  Row ra, rb;
+  int row = r0 + wid;
+  if (row < r1) load_row(row, ra);
+  for (; row < r1; row += 8) {
+    process(row, ra, rb);
+    if (row + 4 < r1) process(row + 4, rb, ra);
   }
   if (dw_part) {
 #pragma unroll
@@ -358,7 +418,9 @@ __global__ __launch_bounds__(256) void softmax_bwd_kernel(const T* __restrict__ 
 // =====================================================================================
 #define DISPATCH_LNB(TI, TO, TD, ...)                                                       \
   do {                                                                                       \
-    if (D % 256 == 0 && D <= 1024) {                                                         \
+    if (D == 768) {                                                                          \
+      ln_bwd<TI, TO, 4, 3, TD><<<grid, 256, 0, stream>>>(__VA_ARGS__);                       \
+    } else if (D % 256 == 0 && D <= 1024) {                                                  \
       ln_bwd<TI, TO, 4, 4, TD><<<grid, 256, 0, stream>>>(__VA_ARGS__);                       \
     } else if (D <= 1024) {                                                                  \
       ln_bwd<TI, TO, 1, 16, TD><<<grid, 256, 0, stream>>>(__VA_ARGS__);                      \
