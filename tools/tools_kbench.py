@@ -138,6 +138,14 @@ def rowk_bench():
     db = torch.zeros(D, device=dev)
     t = timeit(lambda: ops.layernorm_bwd(x, w, dy, mean, rstd, dx, False, dw=dw, db=db, dx_base=dxb, b=b))
     print(f"ln_bwd x f32 dy bf16 +dx_base [{M},{D}] dw/db: {t*1e3:.1f} us, {M*D*14/t/1e6:.0f} GB/s")
+    # fc1 GELU + dropout backward with the fc1 bias gradient (bf16 pre-activation, bf16 dy / dx)
+    F = 3072
+    pre = torch.randn(M, F, device=dev).to(torch.bfloat16)
+    g = torch.randn(M, F, device=dev).to(torch.bfloat16)
+    gx = torch.empty(M, F, device=dev, dtype=torch.bfloat16)
+    dbias = torch.zeros(F, device=dev)
+    t = timeit(lambda: ops.act_bwd_bias(pre, g, gx, dbias, "gelu", drop_p=0.1, seed=3))
+    print(f"act_bwd_bias gelu+dropout bf16 [{M},{F}]: {t*1e3:.1f} us, {M*F*6/t/1e6:.0f} GB/s")
 
 
 if __name__ == "__main__" and len(sys.argv) > 1 and sys.argv[1] == "rowk":
