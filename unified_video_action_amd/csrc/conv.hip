@@ -36,10 +36,12 @@
 // TR = tile rows: 16 (512 threads, 1 workgroup / CU) or 8 (256 threads, 2 workgroups / CU: the two
 // co-resident tiles drift apart, so one tile's prologue / epilogue HBM traffic runs under the
 // other's MFMA loop instead of every CU loading and storing in lockstep)
-template <int BN, int TR, bool R3 = false, bool HD = false>
+template <int BN, int TR, bool R3 = false, bool HD = false, bool RB = false>
 struct ConvHCfg {
   static constexpr int NTH = TR * 32, NW = NTH / 64;
-  static constexpr int WN = 2, WM = NW / WN;    // BN = 128: waves of 64 px x 64 co
+  // BN = 128: waves of 64 px x 64 co; RB: waves of 128 px x 32 co (each wave streams only its
+  // own 32 weight columns from L2, so the workgroup's B traffic equals the LDS ring's)
+  static constexpr int WN = RB ? NW : 2, WM = NW / WN;
   static constexpr int FM = TR / WM;            // tile rows (16-pixel fragments) per wave
   static constexpr int FN = BN / WN / 16;       // 16-channel fragments per wave
   static constexpr int HR = TR + 2;             // halo rows
@@ -48,14 +50,18 @@ struct ConvHCfg {
   // the image padded to HPIX_P pixels
   static constexpr int HD_I = ((HPIX + 7) / 8 + NW - 1) / NW;
   static constexpr int HPIX_P = HD_I * NW * 8;
-  static constexpr int HALO_ELEMS = (HD ? HPIX_P : HPIX) * 64;
+  // RB: padded pixel pitch of 72 elements (144 B = 36 dwords: 16 consecutive pixels hit 16
+  // distinct 4-bank groups, so the A reads need no swizzle and every fragment offset is the lane's
+  // base + a compile-time constant)
+  static constexpr int PP = RB ? 72 : 64;
+  static constexpr int HALO_ELEMS = (HD ? HPIX_P : HPIX) * PP;
   static constexpr int ROUNDS = (HPIX * 8 + NTH - 1) / NTH;
   static constexpr int BT = BN * 64;            // weight tile elements
   static constexpr int NI = BT / (NW * 512);    // DMA instructions per thread per weight tile
   // R3: one halo buffer (restaged between chunks) and a 3-slot weight ring (DMA two steps ahead);
   // otherwise two halo buffers and a 2-slot ring
   static constexpr int NHB = R3 ? 1 : 2, NWB = R3 ? 3 : 2;
-  static constexpr int MAIN_BYTES = (NHB * HALO_ELEMS + NWB * BT) * 2;
+  static constexpr int MAIN_BYTES = (NHB * HALO_ELEMS + (RB ? 0 : NWB * BT)) * 2;  // RB: weights in VGPRs
   static constexpr int TP = BN + 4;             // epilogue fp32 pitch
   static constexpr int EPI_BYTES = 128 * TP * 4 + NW * (BN / 8) * 8 * 2 * 4;
   static constexpr int LDS_BYTES = MAIN_BYTES > EPI_BYTES ? MAIN_BYTES : EPI_BYTES;
@@ -109,7 +115,8 @@ __device__ __forceinline__ void conv_vm_wait(int n) {
 #undef CVW
 }
 
-// VAR bits (UVA_CONV_VAR / UVA_CONV_GN_VAR; production non-GN = 12, GN = 0): 16 the next chunk's
+// VAR bits (UVA_CONV_VAR / UVA_CONV_GN_VAR; production non-GN = 12, GN = 64): 64 weights in VGPRs
+// (RB below; A reads pipelined by k-half across taps measured slower: 5.75 -> 6.16 ms); 16 the next chunk's
 // halo staging spread over taps 1..ROUNDS (one round per step); 1 per-tile prologue / main-loop /
 // epilogue s_memtime stamps of the first 16 blocks (uva_debug_conv_stamps); 2 one halo buffer + a
 // 3-slot weight ring (measured slower); 4 both k-halves' fragment reads issued before the MFMAs
@@ -127,8 +134,13 @@ __global__ __launch_bounds__(TR * 32, 16 / TR) void conv3x3_halo(const bf16* __r
   constexpr bool R3 = (VAR & 2) != 0;
   constexpr bool HD = (VAR & 8) != 0 && !GN && !R3;
   constexpr bool SPREAD = (VAR & 16) != 0 && !HD && !R3;  // halo staging spread over taps 1..ROUNDS
+  // RB (GN only): weight fragments straight from L2 into VGPRs one tap ahead (buffer loads, the
+  // K offset in the SGPR soffset) instead of an LDS ring, so the taps need no barrier (one per
+  // 64-channel chunk, for the halo swap); padded halo pitch, taps unrolled: every A-fragment read is
+  // base + immediate offset (no per-step address VALU)
+  constexpr bool RB = (VAR & 64) != 0 && GN && !R3 && !SPREAD;
   static_assert(!SPREAD || ConvHCfg<BN, TR>::ROUNDS <= 8, "one staging round per tap 1..8");
-  using G = ConvHCfg<BN, TR, R3, HD>;
+  using G = ConvHCfg<BN, TR, R3, HD, RB>;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   unsigned long long st0 = 0, st1 = 0, st2 = 0;
   if constexpr (VAR & 1) asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(st0)::"memory");
@@ -209,7 +221,8 @@ __global__ __launch_bounds__(TR * 32, 16 / TR) void conv3x3_halo(const bf16* __r
             v[j + 1] = (bf16)u.y;
           }
         }
-        *(bf16x8*)(img + p * 64 + ((hc ^ (p & 7)) << 3)) = v;
+        if constexpr (RB) *(bf16x8*)(img + p * G::PP + hc * 8) = v;
+        else *(bf16x8*)(img + p * 64 + ((hc ^ (p & 7)) << 3)) = v;
       }
     }
   };
@@ -252,7 +265,7 @@ __global__ __launch_bounds__(TR * 32, 16 / TR) void conv3x3_halo(const bf16* __r
     for (int j = 0; j < G::FN; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
 
   // ---- prologue: weight tile 0 (and 1 with the 3-slot ring) + halo of chunk 0
-  dma_w(0, 0);
+  if (!RB) dma_w(0, 0);
   if (R3 && S > 1) dma_w(1, 1);
   if constexpr (HD) {
     halo_dma(0, 0);
@@ -286,6 +299,69 @@ __global__ __launch_bounds__(TR * 32, 16 / TR) void conv3x3_halo(const bf16* __r
   };
   if constexpr (VAR & 1) asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(st1)::"memory");
   int prev_loads = 0;  // R3: global loads the previous step issued after its weight DMA
+  if constexpr (RB) {
+    // B fragment (ks, g) of step s for this lane: 16 B at wt[(n0 + wn*64 + g*16 + frow) * K +
+    // tap*Ci + cc*64 + ks*32 + fk*8]; per-lane part in vb[g] (+ ks*64 B immediate), step part in soffset
+    const __amdgpu_buffer_rsrc_t rs_w = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)wt, 0, __builtin_amdgcn_readfirstlane(Co * K * 2), 0x00020000);
+    int vb[G::FN];
+#pragma unroll
+    for (int g = 0; g < G::FN; ++g) vb[g] = ((n0 + wn * (G::FN * 16) + g * 16 + frow) * K + fk * 8) * 2;
+    auto bload = [&](int s, bf16x8 (&dst)[2][G::FN]) __attribute__((always_inline)) {
+      const int cc = s / 9, tap = s - cc * 9;
+      const int soff = __builtin_amdgcn_readfirstlane((tap * Ci + cc * 64) * 2);
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+        for (int g = 0; g < G::FN; ++g)
+          dst[ks][g] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rs_w, vb[g] + ks * 64, soff, 0));
+    };
+    // A fragment (ks, f) of tap (kh, kw): halo pixel (wm*FM + f + kh, frow + kw), channels
+    // (ks*4 + fk)*8.. -> lane base + ((f + kh) * 18 + kw) * PP + ks * 32
+    const int abase = (wm * G::FM * CH_W + frow) * G::PP + fk * 8;
+    bf16x8 bq[2][2][G::FN];  // [register set][ks][g]
+    bload(0, bq[0]);
+    for (int cc = 0; cc < nch; ++cc) {
+      const bf16* hcur = halo + (cc & 1) * G::HALO_ELEMS + abase;
+      const bool more = cc + 1 < nch;
+#pragma unroll
+      for (int tap = 0; tap < 9; ++tap) {
+        const int s = cc * 9 + tap;
+        const int cur = tap & 1, nxt = cur ^ 1;  // tap 8's next set is copied to set 0 below
+        if (s + 1 < S) bload(s + 1, bq[nxt]);
+        if (tap == 0 && more) halo_load(cc + 1);
+        if (tap == 0 && !more && residual) res_load();
+        const int kh = tap / 3, kw = tap % 3;
+        bf16x8 fa[2][G::FM];
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+          for (int f = 0; f < G::FM; ++f)
+            fa[ks][f] = *(const bf16x8*)(hcur + ((f + kh) * CH_W + kw) * G::PP + ks * 32);
+        __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+          for (int f = 0; f < G::FM; ++f)
+#pragma unroll
+            for (int g = 0; g < G::FN; ++g)
+              acc[f][g] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[ks][f], bq[cur][ks][g], acc[f][g], 0, 0, 0);
+        __builtin_amdgcn_s_setprio(0);
+      }
+      // tap 8 loaded step s+1 into set 1; the next chunk's tap 0 reads set 0
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+        for (int g = 0; g < G::FN; ++g) bq[0][ks][g] = bq[1][ks][g];
+      if (more) {
+        // every wave is done with chunk cc-1's buffer since the previous chunk barrier: stage the
+        // next chunk into it, then one barrier orders the staging before chunk cc+1's reads
+        halo_store((cc + 1) & 1);
+        ch_lds_barrier();
+      }
+    }
+    ch_lds_barrier();  // the epilogue's LDS image overlays the halo buffers
+  } else
   for (int cc = 0; cc < nch; ++cc) {
     const bf16* hcur = halo + (R3 ? 0 : (cc & 1)) * G::HALO_ELEMS;
     const bool more = cc + 1 < nch;
@@ -566,7 +642,8 @@ extern "C" int uva_conv3x3_halo(const void* in, const void* w, void* out, const 
 #define CH_LAUNCH(BNV, GNV, VARV, TRV)                                                                         \
   do {                                                                                                         \
     static bool attr = false;                                                                                  \
-    const int lb = ConvHCfg<BNV, TRV, ((VARV) & 2) != 0, ((VARV) & 8) != 0 && !(GNV) && !((VARV) & 2)>::LDS_BYTES; \
+    const int lb = ConvHCfg<BNV, TRV, ((VARV) & 2) != 0, ((VARV) & 8) != 0 && !(GNV) && !((VARV) & 2),          \
+                            ((VARV) & 64) != 0 && (GNV) && !((VARV) & 2) && !((VARV) & 16)>::LDS_BYTES;          \
     if (!attr) {                                                                                               \
       (void)hipFuncSetAttribute((const void*)conv3x3_halo<BNV, GNV, VARV, TRV>,                               \
                                 hipFuncAttributeMaxDynamicSharedMemorySize, lb);                               \
@@ -578,7 +655,9 @@ extern "C" int uva_conv3x3_halo(const void* in, const void* w, void* out, const 
   } while (0)
   // production (non-GN): 12 = halo by LDS-DMA (8) + both k-halves' fragment reads issued up front (4)
   static const int var = getenv("UVA_CONV_VAR") ? atoi(getenv("UVA_CONV_VAR")) : 12;
-  static const int gvar = getenv("UVA_CONV_GN_VAR") ? atoi(getenv("UVA_CONV_GN_VAR")) : 0;
+  // production GN variant: 64 (weights in VGPRs, one barrier per chunk; same-box level-0 conv
+  // 6.61 -> 6.49 ms with the bias + residual + GN-stats epilogue, 7.02 -> 6.79 ms in the bench)
+  static const int gvar = getenv("UVA_CONV_GN_VAR") ? atoi(getenv("UVA_CONV_GN_VAR")) : 64;
   if (tr == 16) {
     if (gn_scale) CH_LAUNCH(128, true, 0, 16);
     else if (var == 1) CH_LAUNCH(128, false, 1, 16);
@@ -587,6 +666,7 @@ extern "C" int uva_conv3x3_halo(const void* in, const void* w, void* out, const 
   } else {
     if (gn_scale) {
       if (gvar == 0) CH_LAUNCH(128, true, 0, 8);
+      else if (gvar == 64) CH_LAUNCH(128, true, 64, 8);
       else if (gvar == 4) CH_LAUNCH(128, true, 4, 8);
       else if (gvar == 16) CH_LAUNCH(128, true, 16, 8);
       else CH_LAUNCH(128, true, 20, 8);
