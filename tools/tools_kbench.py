@@ -95,8 +95,25 @@ def conv_bench():
               f"bias+res+GN-stats epilogue {te:.2f} | all {t2:.2f} ms {fl/t2/1e9:.0f} TF")
 
 
+def conv_s2_bench():
+    """VAE Downsample convs: F.pad(0,1,0,1) + 3x3 / stride 2 (vaekl.py:36-53) at the encoder shapes."""
+    dev = "cuda"
+    for (n, H, C) in ((256, 256, 128), (256, 128, 128), (256, 64, 256), (256, 32, 256)):
+        x = torch.randn(n, H, H, C, device=dev).to(torch.bfloat16)
+        w = (torch.randn(C, 3, 3, C, device=dev) * 0.05).to(torch.bfloat16)
+        Ho = H // 2
+        out = torch.empty(n, Ho, Ho, C, device=dev, dtype=torch.bfloat16)
+        bias = torch.randn(C, device=dev)
+        part = torch.empty(n * Ho * Ho // 128, 32, 2, device=dev)
+        fl = 2 * n * Ho * Ho * C * 9 * C
+        t = timeit(lambda: ops.conv2d(x, w, out, n, H, H, C, C, 3, 2, 0, 0, Ho, Ho, bias=bias, gn_part=part), iters=5)
+        print(f"conv3x3/s2 n{n} {H}x{H} C{C}: {t:.3f} ms {fl/t/1e9:.0f} TF")
+
+
 if __name__ == "__main__" and len(sys.argv) > 1 and sys.argv[1] == "conv":
     conv_bench()
+if __name__ == "__main__" and len(sys.argv) > 1 and sys.argv[1] == "convs2":
+    conv_s2_bench()
 
 
 def square_bench():
