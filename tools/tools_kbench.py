@@ -155,6 +155,18 @@ def rowk_bench():
     db = torch.zeros(D, device=dev)
     t = timeit(lambda: ops.layernorm_bwd(x, w, dy, mean, rstd, dx, False, dw=dw, db=db, dx_base=dxb, b=b))
     print(f"ln_bwd x f32 dy bf16 +dx_base [{M},{D}] dw/db: {t*1e3:.1f} us, {M*D*14/t/1e6:.0f} GB/s")
+    # DiffLoss res-block adaLN LayerNorm backward: D = 1024, fp32 dy, modulation rows of a [M, 3D] bf16 table
+    Wd = 1024
+    x1 = torch.randn(M, Wd, device=dev)
+    mean1 = x1.mean(-1)
+    rstd1 = 1 / x1.var(-1, unbiased=False).add(1e-6).sqrt()
+    mod = (torch.randn(M, 3 * Wd, device=dev) * 0.1).to(torch.bfloat16)
+    dyf = torch.randn(M, Wd, device=dev)
+    dx1 = torch.empty(M, Wd, device=dev)
+    dmod = torch.empty(M, 3 * Wd, device=dev, dtype=torch.bfloat16)
+    t = timeit(lambda: ops.layernorm_bwd(x1, None, dyf, mean1, rstd1, dx1, False, scale=mod[:, Wd:2 * Wd], ldm=3 * Wd,
+                                         dscale=dmod[:, Wd:2 * Wd], dshift=dmod[:, :Wd]))
+    print(f"ln_bwd adaLN x f32 dy f32 [{M},{Wd}]: {t*1e3:.1f} us, {M*Wd*18/t/1e6:.0f} GB/s")
     # fc1 GELU + dropout backward with the fc1 bias gradient (bf16 pre-activation, bf16 dy / dx)
     F = 3072
     pre = torch.randn(M, F, device=dev).to(torch.bfloat16)

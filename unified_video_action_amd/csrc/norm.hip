@@ -198,8 +198,8 @@ __global__ __launch_bounds__(256) void ln_bwd(const TI* __restrict__ x, const fl
     }
   };
   // one row: its loads were issued one row earlier into R; the row after next is loaded into L
-  auto process = [&](int row, const Row& R, Row& L) __attribute__((always_inline)) {
-    if (row + 4 < r1) load_row(row + 4, L);
+  auto process = [&](int row, const Row& R, Row& L, bool pf) __attribute__((always_inline)) {
+    if (pf && row + 4 < r1) load_row(row + 4, L);
     const float mean = R.mean, rstd = R.rstd;
     float xh[NC][VEC], g[NC][VEC];
     float s1 = 0.f, s2 = 0.f;
@@ -255,13 +255,22 @@ __global__ __launch_bounds__(256) void ln_bwd(const TI* __restrict__ x, const fl
       stv<VEC>(dx + (long long)row * D + col0, o);
     }
   };
-  // two register sets used in turn (no copies between rows)
   Row ra, rb;
   int row = r0 + wid;
-  if (row < r1) load_row(row, ra);
-  for (; row < r1; row += 8) {
-    process(row, ra, rb);
-    if (row + 4 < r1) process(row + 4, rb, ra);
+  if constexpr (NC <= 3) {
+    // two register sets used in turn (no copies between rows)
+    if (row < r1) load_row(row, ra);
+    for (; row < r1; row += 8) {
+      process(row, ra, rb, true);
+      if (row + 4 < r1) process(row + 4, rb, ra, true);
+    }
+  } else {
+    // D = 1024 (adaLN trunk): two row sets do not fit beside the modulated path's state (276
+    // VGPRs, one wave per SIMD: 199 -> 283 us), so rows are loaded one at a time
+    for (; row < r1; row += 4) {
+      load_row(row, ra);
+      process(row, ra, rb, false);
+    }
   }
   if (dw_part) {
 #pragma unroll
