@@ -727,19 +727,35 @@ __global__ __launch_bounds__(256) void conv_in_kernel(const bf16* __restrict__ i
   }
   if (tid < 128) sb[tid] = bias ? bias[tid] : 0.f;
   bf16* myslab = slab[wid];
+  // halo of a tile: 324 pixels x 16 B, 2 per thread, loaded into registers one tile AHEAD (the
+  // load of tile t+1 is in flight while tile t computes; loaded at the tile's start, its HBM
+  // latency was exposed once per tile)
+  constexpr int HR = (CH_HPIX + 255) / 256;
+  bf16x8 hv[HR];
+  auto halo_ld = [&](int sp) {
+    const int tx = sp % tiles_x, ty = (sp / tiles_x) % tiles_y, n = sp / (tiles_x * tiles_y);
+#pragma unroll
+    for (int i = 0; i < HR; ++i) {
+      const int p = tid + i * 256;
+      const int hy = p / CH_H, hx = p - hy * CH_H;
+      const int ih = ty * CH_T - 1 + hy, iw = tx * CH_T - 1 + hx;
+      hv[i] = (bf16x8){};
+      if (p < CH_HPIX && ih >= 0 && ih < H && iw >= 0 && iw < W)
+        hv[i] = *(const bf16x8*)(in + (((long long)n * H + ih) * W + iw) * 8);
+    }
+  };
+  const int sp_end = min(ntiles, (int)(blockIdx.x + 1) * CI_TPW);
+  if ((int)blockIdx.x * CI_TPW < sp_end) halo_ld(blockIdx.x * CI_TPW);
 #pragma unroll 1
-  for (int sp = blockIdx.x * CI_TPW; sp < min(ntiles, (int)(blockIdx.x + 1) * CI_TPW); ++sp) {
+  for (int sp = blockIdx.x * CI_TPW; sp < sp_end; ++sp) {
     const int tx = sp % tiles_x, ty = (sp / tiles_x) % tiles_y, n = sp / (tiles_x * tiles_y);
     const int oh0 = ty * CH_T, ow0 = tx * CH_T;
-    // halo: 324 pixels x 16 B (the previous tile's readers passed the barrier ending its iteration)
-    for (int p = tid; p < CH_HPIX; p += 256) {
-      const int hy = p / CH_H, hx = p - hy * CH_H;
-      const int ih = oh0 - 1 + hy, iw = ow0 - 1 + hx;
-      bf16x8 v = (bf16x8){};
-      if (ih >= 0 && ih < H && iw >= 0 && iw < W) v = *(const bf16x8*)(in + (((long long)n * H + ih) * W + iw) * 8);
-      *(bf16x8*)(sx + p * 8) = v;
-    }
+    // (the previous tile's readers passed the barrier ending its iteration)
+#pragma unroll
+    for (int i = 0; i < HR; ++i)
+      if (tid + i * 256 < CH_HPIX) *(bf16x8*)(sx + (tid + i * 256) * 8) = hv[i];
     __syncthreads();
+    if (sp + 1 < sp_end) halo_ld(sp + 1);
     float gs[8], gq[8];
 #pragma unroll
     for (int f = 0; f < 8; ++f) gs[f] = gq[f] = 0.f;
