@@ -264,6 +264,29 @@ __global__ __launch_bounds__(TR * 32, 16 / TR) void conv3x3_halo(const bf16* __r
 #pragma unroll
     for (int j = 0; j < G::FN; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
 
+  const int frow = lane & 15, fk = lane >> 4;
+  // RB: B fragment (ks, g) of step s for this lane: 16 B at wt[(n0 + wn*32 + g*16 + frow) * K +
+  // tap*Ci + cc*64 + ks*32 + fk*8]; per-lane part in vb[g] (+ ks*64 B immediate), step part in
+  // soffset.  Step 0's fragments are issued ahead of the halo so their latency overlaps it.
+  __amdgpu_buffer_rsrc_t rs_w;
+  int vb[G::FN];
+  bf16x8 bq[2][2][G::FN];  // [register set][ks][g]
+  auto bload = [&](int s, bf16x8 (&dst)[2][G::FN]) __attribute__((always_inline)) {
+    const int cc = s / 9, tap = s - cc * 9;
+    const int soff = __builtin_amdgcn_readfirstlane((tap * Ci + cc * 64) * 2);
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int g = 0; g < G::FN; ++g)
+        dst[ks][g] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rs_w, vb[g] + ks * 64, soff, 0));
+  };
+  if constexpr (RB) {
+    rs_w = __builtin_amdgcn_make_buffer_rsrc((void*)wt, 0, __builtin_amdgcn_readfirstlane(Co * K * 2), 0x00020000);
+#pragma unroll
+    for (int g = 0; g < G::FN; ++g) vb[g] = ((n0 + wn * (G::FN * 16) + g * 16 + frow) * K + fk * 8) * 2;
+    bload(0, bq[0]);
+  }
+
   // ---- prologue: weight tile 0 (and 1 with the 3-slot ring) + halo of chunk 0
   if (!RB) dma_w(0, 0);
   if (R3 && S > 1) dma_w(1, 1);
@@ -277,7 +300,6 @@ __global__ __launch_bounds__(TR * 32, 16 / TR) void conv3x3_halo(const bf16* __r
   __builtin_amdgcn_s_barrier();
   asm volatile("" ::: "memory");
 
-  const int frow = lane & 15, fk = lane >> 4;
   // epilogue geometry.  The first ROUNDS of the tile's residual row chunks are loaded at tap 0 of
   // the LAST chunk into hreg (free there: no next halo), so the step barriers cover their HBM
   // latency (loaded at the epilogue's start, ~1.5-3k cycles stayed exposed per tile, +0.7 ms at
@@ -300,27 +322,9 @@ __global__ __launch_bounds__(TR * 32, 16 / TR) void conv3x3_halo(const bf16* __r
   if constexpr (VAR & 1) asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(st1)::"memory");
   int prev_loads = 0;  // R3: global loads the previous step issued after its weight DMA
   if constexpr (RB) {
-    // B fragment (ks, g) of step s for this lane: 16 B at wt[(n0 + wn*64 + g*16 + frow) * K +
-    // tap*Ci + cc*64 + ks*32 + fk*8]; per-lane part in vb[g] (+ ks*64 B immediate), step part in soffset
-    const __amdgpu_buffer_rsrc_t rs_w = __builtin_amdgcn_make_buffer_rsrc(
-        (void*)wt, 0, __builtin_amdgcn_readfirstlane(Co * K * 2), 0x00020000);
-    int vb[G::FN];
-#pragma unroll
-    for (int g = 0; g < G::FN; ++g) vb[g] = ((n0 + wn * (G::FN * 16) + g * 16 + frow) * K + fk * 8) * 2;
-    auto bload = [&](int s, bf16x8 (&dst)[2][G::FN]) __attribute__((always_inline)) {
-      const int cc = s / 9, tap = s - cc * 9;
-      const int soff = __builtin_amdgcn_readfirstlane((tap * Ci + cc * 64) * 2);
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks)
-#pragma unroll
-        for (int g = 0; g < G::FN; ++g)
-          dst[ks][g] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rs_w, vb[g] + ks * 64, soff, 0));
-    };
     // A fragment (ks, f) of tap (kh, kw): halo pixel (wm*FM + f + kh, frow + kw), channels
     // (ks*4 + fk)*8.. -> lane base + ((f + kh) * 18 + kw) * PP + ks * 32
     const int abase = (wm * G::FM * CH_W + frow) * G::PP + fk * 8;
-    bf16x8 bq[2][2][G::FN];  // [register set][ks][g]
-    bload(0, bq[0]);
     for (int cc = 0; cc < nch; ++cc) {
       const bf16* hcur = halo + (cc & 1) * G::HALO_ELEMS + abase;
       const bool more = cc + 1 < nch;
