@@ -50,10 +50,13 @@ struct ConvHCfg {
   // the image padded to HPIX_P pixels
   static constexpr int HD_I = ((HPIX + 7) / 8 + NW - 1) / NW;
   static constexpr int HPIX_P = HD_I * NW * 8;
-  // RB: padded pixel pitch of 72 elements (144 B = 36 dwords: 16 consecutive pixels hit 16
-  // distinct 4-bank groups, so the A reads need no swizzle and every fragment offset is the lane's
-  // base + a compile-time constant)
-  static constexpr int PP = RB ? 72 : 64;
+  // RB: padded pixel pitch of 80 elements (160 B = 10 x 16 B): for a fragment read, lane l reads
+  // 16 B at pixel (l & 15), channel chunk (l >> 4), i.e. 16-B slot ((l & 15) * 10 + (l >> 4)) mod 16
+  // of the 64-bank row -- distinct inside each of ds_read_b128's four 16-lane groups
+  // ({0-3,12-15,20-27}, ...), so the A reads are conflict-free with no swizzle and every fragment
+  // offset is the lane's base + a compile-time constant.  (A 144-B pitch, conflict-free only for 16
+  // CONSECUTIVE lanes, was up to 8-way conflicted in the real lane groups.)
+  static constexpr int PP = RB ? 80 : 64;
   static constexpr int HALO_ELEMS = (HD ? HPIX_P : HPIX) * PP;
   static constexpr int ROUNDS = (HPIX * 8 + NTH - 1) / NTH;
   static constexpr int BT = BN * 64;            // weight tile elements
