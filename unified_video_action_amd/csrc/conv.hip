@@ -674,6 +674,7 @@ extern "C" int uva_conv3x3_halo(const void* in, const void* w, void* out, const 
     if (gn_scale) {
       if (gvar == 0) CH_LAUNCH(128, true, 0, 8);
       else if (gvar == 64) CH_LAUNCH(128, true, 64, 8);
+      else if (gvar == 65) CH_LAUNCH(128, true, 65, 8);  // + per-tile phase stamps
       else if (gvar == 4) CH_LAUNCH(128, true, 4, 8);
       else if (gvar == 16) CH_LAUNCH(128, true, 16, 8);
       else CH_LAUNCH(128, true, 20, 8);
