@@ -260,6 +260,13 @@ int uva_upsample_nearest2x(int dtype, const void* x, void* y, int n, int H, int 
  * crop window crop_size^2 resized back to S^2 (bilinear), then the 5x5 reflect-padded blur. */
 int uva_pusht_augment(const float* img, float* out, const float* params, int B, int T, int C, int S, int crop_size,
                       hipStream_t stream);
+/* Video training augmentation: the UMI chain of config/task/umi_lazy.yaml:50-72 (kornia 0.8
+ * VideoSequential: RandomCrop -> Resize -> ColorJitter -> RandomSharpness -> RandomAutoContrast ->
+ * RandomGrayscale -> RandomGaussianBlur, dataset/base_lazy_dataset.py:365-411) and the Libero ColorJitter of
+ * dataset/libero_replay_image_dataset.py:229-247 (torchvision).  img/out [B,T,3,S,S] fp32 in [0,1];
+ * params [B][24] per video (utils/augment.py); scratch >= B*T*6*S*S floats.  One workgroup per frame. */
+int uva_video_augment(const float* img, float* out, float* scratch, const float* params, int B, int T, int S,
+                      hipStream_t stream);
 int uva_posterior_sample(int mdt, const void* moments, const float* eps, float* z, int Nimg, float scale,
                          hipStream_t stream);
 

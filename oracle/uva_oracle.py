@@ -723,6 +723,154 @@ def pusht_augment(image, params, crop=91):
     return torch.stack(out)
 
 
+# ---- §8f-3: UMI (kornia 0.8 VideoSequential) and Libero (torchvision 0.16 ColorJitter) ----------
+# Parameter row per video (utils/augment.py AUG_NP = 24): 0 crop, 1 top, 2 left, 3 jitter,
+# 4-7 op order (0 brightness, 1 contrast, 2 saturation, 3 hue), 8-11 factors (hue already in the
+# style's unit: radians for kornia, turns for torchvision), 12 sharpness, 13 its factor,
+# 14 autocontrast, 15 grayscale, 16 blur, 17-21 1-D Gaussian taps, 22 style (0 kornia,
+# 1 torchvision), 23 crop size.  kornia and torchvision are absent here: these are restatements
+# of their published algorithms (parity against the libraries themselves: unpinned).
+
+def _gray_k(x):
+    """kornia.color.rgb_to_grayscale (0.299, 0.587, 0.114)."""
+    return 0.299 * x[..., 0:1, :, :] + 0.587 * x[..., 1:2, :, :] + 0.114 * x[..., 2:3, :, :]
+
+
+def _gray_tv(x):
+    """torchvision F_t.rgb_to_grayscale (0.2989, 0.587, 0.114)."""
+    r, g, b = x.unbind(dim=-3)
+    return (0.2989 * r + 0.587 * g + 0.114 * b).unsqueeze(-3)
+
+
+def _k_rgb2hsv(img, eps=1e-8):
+    """kornia.color.rgb_to_hsv: h in [0, 2pi), first channel wins a tie for the max."""
+    max_rgb, argmax_rgb = img.max(-3)
+    min_rgb = img.min(-3).values
+    deltac = max_rgb - min_rgb
+    v = max_rgb
+    s = deltac / (max_rgb + eps)
+    deltac = torch.where(deltac == 0, torch.ones_like(deltac), deltac)
+    rc, gc, bc = torch.unbind(max_rgb.unsqueeze(-3) - img, dim=-3)
+    h = torch.stack((bc - gc, (rc - bc) + 2.0 * deltac, (gc - rc) + 4.0 * deltac), dim=-3) / deltac.unsqueeze(-3)
+    h = torch.gather(h, -3, argmax_rgb.unsqueeze(-3)).squeeze(-3)
+    h = (h / 6.0) % 1.0
+    return torch.stack((2.0 * math.pi * h, s, v), dim=-3)
+
+
+def _k_hsv2rgb(img):
+    """kornia.color.hsv_to_rgb (sector gather over (v,q,p,p,t,v | t,v,v,q,p,p | p,p,t,v,v,q))."""
+    h = img[..., 0, :, :] / (2 * math.pi)
+    s, v = img[..., 1, :, :], img[..., 2, :, :]
+    hi = torch.floor(h * 6) % 6
+    f = ((h * 6) % 6) - hi
+    p, q, t = v * (1 - s), v * (1 - f * s), v * (1 - (1 - f) * s)
+    hi = hi.long()
+    idx = torch.stack([hi, hi + 6, hi + 12], dim=-3)
+    out = torch.stack((v, q, p, p, t, v, t, v, v, q, p, p, p, p, t, v, v, q), dim=-3)
+    return torch.gather(out, -3, idx)
+
+
+def _tv_rgb2hsv(img):
+    """torchvision F_t._rgb2hsv (h in turns)."""
+    r, g, b = img.unbind(dim=-3)
+    maxc, minc = img.max(dim=-3).values, img.min(dim=-3).values
+    eqc = maxc == minc
+    cr = maxc - minc
+    ones = torch.ones_like(maxc)
+    s = cr / torch.where(eqc, ones, maxc)
+    crd = torch.where(eqc, ones, cr)
+    rc, gc, bc = (maxc - r) / crd, (maxc - g) / crd, (maxc - b) / crd
+    hr = (maxc == r) * (bc - gc)
+    hg = ((maxc == g) & (maxc != r)) * (2.0 + rc - bc)
+    hb = ((maxc != g) & (maxc != r)) * (4.0 + gc - rc)
+    h = torch.fmod((hr + hg + hb) / 6.0 + 1.0, 1.0)
+    return torch.stack((h, s, maxc), dim=-3)
+
+
+def _tv_hsv2rgb(img):
+    """torchvision F_t._hsv2rgb (clamped p / q / t, sector select)."""
+    h, s, v = img.unbind(dim=-3)
+    i = torch.floor(h * 6.0)
+    f = h * 6.0 - i
+    i = i.to(torch.int32) % 6
+    p = torch.clamp(v * (1.0 - s), 0.0, 1.0)
+    q = torch.clamp(v * (1.0 - s * f), 0.0, 1.0)
+    t = torch.clamp(v * (1.0 - s * (1.0 - f)), 0.0, 1.0)
+    mask = (i.unsqueeze(-3) == torch.arange(6).view(-1, 1, 1)).to(img.dtype)
+    a4 = torch.stack((torch.stack((v, q, p, p, t, v), -3), torch.stack((t, v, v, q, p, p), -3),
+                      torch.stack((p, p, t, v, v, q), -3)), -4)
+    return torch.einsum("...ijk,...xijk->...xjk", mask, a4)
+
+
+def _jitter_op(x, op, fac, tv):
+    """One ColorJitter op on frames [T, 3, H, W]: kornia 0.8 ColorJitter (brightness_accumulative,
+    contrast_with_mean_subtraction, saturation_with_gray_subtraction, adjust_hue) or torchvision
+    0.16 ColorJitter (_blend forms, adjust_hue)."""
+    gray = _gray_tv if tv else _gray_k
+    if op == 0:
+        return (fac * x).clamp(0.0, 1.0)
+    if op == 1:
+        m = gray(x).mean(dim=(-3, -2, -1), keepdim=True)
+        return (fac * x + (1.0 - fac) * m).clamp(0.0, 1.0)
+    if op == 2:
+        return (fac * x + (1.0 - fac) * gray(x)).clamp(0.0, 1.0)
+    if fac == 0.0:
+        return x  # both libraries skip a zero hue shift
+    if tv:
+        h, s, v = _tv_rgb2hsv(x).unbind(-3)
+        return _tv_hsv2rgb(torch.stack(((h + fac) % 1.0, s, v), -3))
+    h, s, v = _k_rgb2hsv(x).unbind(-3)
+    return _k_hsv2rgb(torch.stack((torch.fmod(h + fac, 2 * math.pi), s, v), -3))
+
+
+def _sharpness_k(x, fac):
+    """kornia.enhance.sharpness: 3x3 (1,1,1;1,5,1;1,1,1)/13 smoothing on the valid interior,
+    clamped, border pixels kept, then blended back: deg + fac * (x - deg), clamped."""
+    C = x.shape[-3]
+    k = torch.tensor([[1.0, 1.0, 1.0], [1.0, 5.0, 1.0], [1.0, 1.0, 1.0]]) / 13
+    deg = F.conv2d(x, k.view(1, 1, 3, 3).repeat(C, 1, 1, 1), groups=C).clamp(0.0, 1.0)
+    res = x.clone()
+    res[..., 1:-1, 1:-1] = deg
+    return (res + (x - res) * fac).clamp(0.0, 1.0)
+
+
+def video_augment(video, params):
+    """video [B, T, 3, S, S] in [0, 1] -> augmented copy, one parameter row per video.
+    kornia style (UMI, base_lazy_dataset.py:365-411 + config/task/umi_lazy.yaml:50-72):
+    RandomCrop(cs) -> Resize(S) (bilinear, upscaling: antialias inert) -> ColorJitter ->
+    RandomSharpness -> RandomAutoContrast (normalize_min_max per frame and channel, eps 1e-6,
+    clipped) -> RandomGrayscale -> RandomGaussianBlur (separable, reflect, x then y).
+    torchvision style (Libero, libero_replay_image_dataset.py:229-247): ColorJitter only."""
+    B, T, C, S, _ = video.shape
+    out = []
+    for b in range(B):
+        x = video[b].float()
+        p = params[b].tolist()
+        tv = p[22] != 0
+        cs = int(p[23])
+        if p[0]:
+            t, l = int(p[1]), int(p[2])
+            x = F.interpolate(x[..., t:t + cs, l:l + cs], size=(S, S), mode="bilinear", align_corners=False)
+        if p[3]:
+            for k in range(4):
+                op = int(p[4 + k])
+                x = _jitter_op(x, op, torch.tensor(p[8 + op], dtype=torch.float32).item(), tv)
+        if p[12]:
+            x = _sharpness_k(x, p[13])
+        if p[14]:
+            mn = x.amin(dim=(-2, -1), keepdim=True)
+            mx = x.amax(dim=(-2, -1), keepdim=True)
+            x = ((x - mn) / (mx - mn + 1e-6)).clamp(0.0, 1.0)
+        if p[15]:
+            x = _gray_k(x).expand(-1, C, -1, -1).contiguous()
+        if p[16]:
+            k = torch.tensor(p[17:22], dtype=torch.float32)
+            x = F.conv2d(F.pad(x, (2, 2, 0, 0), mode="reflect"), k.view(1, 1, 1, 5).repeat(C, 1, 1, 1), groups=C)
+            x = F.conv2d(F.pad(x, (0, 0, 2, 2), mode="reflect"), k.view(1, 1, 5, 1).repeat(C, 1, 1, 1), groups=C)
+        out.append(x)
+    return torch.stack(out)
+
+
 def eval_frame_indices(T=32, k=4):
     """[3, 11, 19, 27] for T=32 (select_frames eval=True, data_utils.py:141-142)."""
     return torch.arange(0, T, T // k) + k - 1

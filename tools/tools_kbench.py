@@ -179,3 +179,25 @@ def rowk_bench():
 
 if __name__ == "__main__" and len(sys.argv) > 1 and sys.argv[1] == "rowk":
     rowk_bench()
+
+
+def aug_bench():
+    """UMI video augmentation (B=56 videos x 8 frames of 224^2, every op on) and Libero ColorJitter
+    (B=32 x 8 x 128^2): time per launch and HBM rate on the algorithmic bytes (frames in + out)."""
+    from unified_video_action_amd.utils.augment import libero_jitter_params, umi_aug_params, video_augment
+    for name, (B, T, S, prm) in {"umi": (56, 8, 224, None), "libero": (32, 8, 128, None)}.items():
+        x = torch.rand(B, T, 3, S, S, device="cuda")
+        if name == "umi":
+            p = umi_aug_params(range(B))
+            p[:, 0], p[:, 1], p[:, 2], p[:, 3], p[:, 12], p[:, 13], p[:, 14], p[:, 16] = 1, 8, 8, 1, 1, 1.5, 1, 1
+            p[:, 17:22] = torch.tensor([0.05, 0.25, 0.4, 0.25, 0.05])
+            p[:, 8:12] = torch.tensor([1.1, 0.9, 1.2, 0.3])
+        else:
+            p = libero_jitter_params(range(B))
+        ms = timeit(lambda: video_augment(x, p))
+        gb = 2 * x.numel() * 4 / 1e9
+        print(f"augment {name:7s} B={B} T={T} S={S}: {ms:.3f} ms  {gb / ms:.2f} TB/s on in+out ({gb:.3f} GB)")
+
+
+if __name__ == "__main__" and len(sys.argv) > 1 and sys.argv[1] == "aug":
+    aug_bench()

@@ -40,6 +40,7 @@ import torch.distributed as dist
 from .. import config as C
 from ..runtime import RT
 from .base_workspace import BaseWorkspace
+from ..utils.augment import augment_batch
 
 
 def dist_env():
@@ -199,6 +200,8 @@ class TrainUnifiedVideoActionWorkspace(BaseWorkspace):
         # a fresh EMAModel after the (optional) resume, as the reference builds it (:190-193)
         self.ema = C.instantiate(cfg.ema, model=self.ema_model) if cfg.training.use_ema else None
         self.model.train()
+        # on-device training augmentation instead of the dataset workers' CPU one
+        self.device_augment = bool(cfg.task.get("device_augment", False))
         return self
 
     # ---- one training step (workspace:279-302) -------------------------------------------------
@@ -238,6 +241,8 @@ class TrainUnifiedVideoActionWorkspace(BaseWorkspace):
             n_batches = len(self.train_dataloader)
             for batch_idx, batch in enumerate(self.train_dataloader):
                 batch = _to_device(batch, self.device)
+                if self.device_augment:
+                    batch = augment_batch(batch)
                 raw, lv, la = self.train_step(batch)
                 meta = {"global_step": self.global_step, "epoch": self.epoch,
                         "lr": self.lr_scheduler.get_last_lr()[0]}
