@@ -57,6 +57,8 @@ def parse(argv=None):
     ap.add_argument("--other-configs", default="pusht_joint:64",
                     help="N=1 only: extra config:batch entries measured after the main line ('' = none)")
     ap.add_argument("--other-steps", type=int, default=20)
+    ap.add_argument("--h2d-steps", type=int, default=10,
+                    help="N=1: steps fed from host batches through the pinned prefetcher (0 = skip)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-batch", type=int, default=2, help="CPU baseline batch (BASELINE configs[0]: 2)")
     ap.add_argument("--cpu-steps", type=int, default=3, help="timed CPU steps (median) after one warm-up step")
@@ -187,6 +189,36 @@ def timed_run(config, batch_size, steps, warmup, precision, device, world, rank)
     return elapsed, per_step, loss.item(), (pol, opt, sched, ema, batch)
 
 
+def h2d_probe(state, device, steps):
+    """PCIe-inclusive numbers beside `value` (which starts from HBM-resident inputs): the pinned
+    host -> device copy of one batch alone, and steps fed through utils.prefetch.PinnedPrefetcher
+    (copy of batch i+1 on a copy stream under step i) from pageable host batches."""
+    import torch
+    from unified_video_action_amd.utils.prefetch import PinnedPrefetcher, _leaves, _map
+    pol, opt, sched, ema, batch = state
+    host = _map(batch, lambda t: t.cpu())
+    nbytes = sum(t.numel() * t.element_size() for t in _leaves(host, []))
+    pinned = _map(host, lambda t: t.pin_memory())
+    for _ in range(2):
+        _map(pinned, lambda t: t.to(device, non_blocking=True))
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(5):
+        _map(pinned, lambda t: t.to(device, non_blocking=True))
+    torch.cuda.synchronize()
+    copy_ms = (time.perf_counter() - t0) / 5 * 1e3
+    step(pol, opt, sched, ema, batch)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for b in PinnedPrefetcher([host] * steps, device, depth=2):
+        step(pol, opt, sched, ema, b)
+    torch.cuda.synchronize()
+    fed_ms = (time.perf_counter() - t0) / steps * 1e3
+    return {"bytes_per_batch": nbytes, "pinned_copy_ms": round(copy_ms, 3),
+            "pinned_copy_GBps": round(nbytes / copy_ms / 1e6, 2), "steps_fed_from_host": steps,
+            "ms_per_step_fed_from_host": round(fed_ms, 2)}
+
+
 def cpu_baseline(args):
     """oracle (PyTorch-CPU fp32 restatement, pinned to the reference) on a bounded sample: the
     same training step at BASELINE configs[0]'s batch (2), one warm-up step, median of a few."""
@@ -255,6 +287,7 @@ def run(args):
         torch.cuda.synchronize()
         trace, ops.TRACE = ops.TRACE, None
         rows = summarize_trace(trace)
+    h2d = h2d_probe(state, device, args.h2d_steps) if (world == 1 and args.h2d_steps > 0) else None
     del state
     others = []
     if world == 1 and args.other_configs:
@@ -306,6 +339,8 @@ def run(args):
         out["top_kernels"] = [{"kernel": t_, "total_ms_per_step": round(a / args.trace_steps, 3),
                                "avg_ms": round(av, 4), "tflops": round(f_ / (av * 1e-3) / 1e12, 1)}
                               for a, t_, n_, av, f_ in rows[:8]]
+    if h2d:
+        out["h2d"] = h2d
     if others:
         out["other_configs"] = others
     if world == 1 and not args.no_cpu_baseline:

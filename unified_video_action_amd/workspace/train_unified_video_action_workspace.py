@@ -41,6 +41,7 @@ from .. import config as C
 from ..runtime import RT
 from .base_workspace import BaseWorkspace
 from ..utils.augment import augment_batch
+from ..utils.prefetch import PinnedPrefetcher
 
 
 def dist_env():
@@ -239,8 +240,8 @@ class TrainUnifiedVideoActionWorkspace(BaseWorkspace):
                 self.train_dataloader.sampler.set_epoch(self.epoch)
             losses = []
             n_batches = len(self.train_dataloader)
-            for batch_idx, batch in enumerate(self.train_dataloader):
-                batch = _to_device(batch, self.device)
+            # H2D of the next batches on a copy stream from pinned staging, overlapped with the step
+            for batch_idx, batch in enumerate(PinnedPrefetcher(self.train_dataloader, self.device)):
                 if self.device_augment:
                     batch = augment_batch(batch)
                 raw, lv, la = self.train_step(batch)
