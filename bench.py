@@ -66,7 +66,7 @@ def parse(argv=None):
     ap.add_argument("--trace-steps", type=int, default=3)
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--trace-out", default="", help="write every traced kernel row (tag, launches, avg ms) here")
-    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r02c.json"))
+    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r02e.json"))
     return ap.parse_args(argv)
 
 

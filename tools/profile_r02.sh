@@ -7,3 +7,8 @@ bash tools/pmc_step.sh
 cp gpurun_out/pmc_mfma/mfma.json gpurun_out/prof_${1:-r02}/mfma_busy.json
 python3 -c "
 import json; d=json.load(open('gpurun_out/prof_${1:-r02}/bench.json')); print(d['value'], d['roofline'])"
+# keep the merge-back under gpurun's 64 MiB cap: drop the raw per-dispatch CSVs (stats, traffic and
+# MFMA summaries above are what profiles/ keeps)
+python3 tools/kt_by_grid.py gpurun_out/prof_${1:-r02}/kt/run_kernel_trace.csv gpurun_out/prof_${1:-r02}/kernel_stats_by_grid.csv || { ls gpurun_out/prof_${1:-r02}/kt; head -2 gpurun_out/prof_${1:-r02}/kt/*trace*.csv; }
+find gpurun_out -name "*.csv" -size +4M -delete
+du -sh gpurun_out
