@@ -264,7 +264,8 @@ int uva_pusht_augment(const float* img, float* out, const float* params, int B, 
  * VideoSequential: RandomCrop -> Resize -> ColorJitter -> RandomSharpness -> RandomAutoContrast ->
  * RandomGrayscale -> RandomGaussianBlur, dataset/base_lazy_dataset.py:365-411) and the Libero ColorJitter of
  * dataset/libero_replay_image_dataset.py:229-247 (torchvision).  img/out [B,T,3,S,S] fp32 in [0,1];
- * params [B][24] per video (utils/augment.py); scratch >= B*T*6*S*S floats.  One workgroup per frame. */
+ * params [B][24] per video (utils/augment.py); scratch >= B*T*(6*S*S + 7*ceil(S/8)) floats; S % 4 == 0, S <= 256.
+ * Three launches over (frame, 8-row band) workgroups. */
 int uva_video_augment(const float* img, float* out, float* scratch, const float* params, int B, int T, int S,
                       hipStream_t stream);
 int uva_posterior_sample(int mdt, const void* moments, const float* eps, float* z, int Nimg, float scale,

@@ -194,7 +194,16 @@ def aug_bench():
             p[:, 8:12] = torch.tensor([1.1, 0.9, 1.2, 0.3])
         else:
             p = libero_jitter_params(range(B))
-        ms = timeit(lambda: video_augment(x, p))
+        from unified_video_action_amd.native.lib import lib
+        out = torch.empty_like(x)
+        from unified_video_action_amd.utils.augment import aug_scratch_floats
+        scratch = torch.empty(aug_scratch_floats(B, T, S), device="cuda")
+        pd = p.cuda()
+        ms_api = timeit(lambda: video_augment(x, p))  # host validation + params H2D included
+        ms = timeit(lambda: lib().call("uva_video_augment", ops.ptr(x), ops.ptr(out), ops.ptr(scratch), ops.ptr(pd),
+                                       B, T, S, ops.stream()))
+        torch.testing.assert_close(out, video_augment(x, p), atol=0, rtol=0)
+        print(f"  ({name}: {ms_api:.3f} ms per video_augment() call incl. host-side checks)")
         gb = 2 * x.numel() * 4 / 1e9
         print(f"augment {name:7s} B={B} T={T} S={S}: {ms:.3f} ms  {gb / ms:.2f} TB/s on in+out ({gb:.3f} GB)")
 

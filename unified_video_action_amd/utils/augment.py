@@ -126,12 +126,18 @@ def libero_jitter_params(seeds, brightness=0.2, contrast=0.2, saturation=0.2, hu
     return out
 
 
+def aug_scratch_floats(B, T, S):
+    """floats of uva_video_augment's scratch: two [B*T, 3, S, S] images + per-band partials."""
+    return B * T * (6 * S * S + 7 * ((S + 7) // 8))
+
+
 def video_augment(video, params):
     """video [B, T, 3, S, S] fp32 in [0, 1] on the GPU, params [B, AUG_NP] -> augmented copy
     (uva_video_augment: one workgroup per frame, whole chain in one launch)."""
     B, T, C, H, W = video.shape
-    if C != 3 or H != W:
-        raise ValueError(f"video augmentation expects [B, T, 3, S, S], got {tuple(video.shape)}")
+    if C != 3 or H != W or H % 4 or H > 256:
+        raise ValueError(f"video augmentation expects [B, T, 3, S, S] with S % 4 == 0 and S <= 256, "
+                         f"got {tuple(video.shape)}")
     if tuple(params.shape) != (B, AUG_NP):
         raise ValueError(f"params must be [{B}, {AUG_NP}], got {tuple(params.shape)}")
     crop = params[:, 0] != 0
@@ -145,7 +151,7 @@ def video_augment(video, params):
     prm = params.to(video.device, torch.float32).contiguous()
     x = video.float().contiguous()
     out = torch.empty_like(x)
-    scratch = torch.empty(B * T * 6 * H * W, device=x.device, dtype=torch.float32)
+    scratch = torch.empty(aug_scratch_floats(B, T, H), device=x.device, dtype=torch.float32)
     lib().call("uva_video_augment", ops.ptr(x), ops.ptr(out), ops.ptr(scratch), ops.ptr(prm), B, T, H, ops.stream())
     return out
 
