@@ -57,6 +57,8 @@ def parse(argv=None):
     ap.add_argument("--other-configs", default="pusht_joint:64",
                     help="N=1 only: extra config:batch entries measured after the main line ('' = none)")
     ap.add_argument("--other-steps", type=int, default=20)
+    ap.add_argument("--launch-check", action="store_true",
+                    help="check the --gpus N process wiring (gloo, no GPU work) and exit")
     ap.add_argument("--h2d-steps", type=int, default=10,
                     help="N=1: steps fed from host batches through the pinned prefetcher (0 = skip)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -269,9 +271,36 @@ def line_for(config, batch, world, steps, elapsed, per_step, loss):
             "final_loss": round(loss, 5)}
 
 
+def launch_check(args):
+    """--launch-check: the N-process wiring of `--gpus N` (spawned workers or an external
+    torchrun environment) without touching a GPU: gloo rendezvous, world size == --gpus, one
+    all-reduce; rank 0 prints one JSON line."""
+    import torch
+    import torch.distributed as dist
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("gloo")
+        t = torch.tensor([float(rank)])
+        dist.all_reduce(t)
+        ok = dist.get_world_size() == args.gpus
+        dist.barrier()
+        dist.destroy_process_group()
+    else:
+        t, ok = torch.tensor([0.0]), args.gpus == 1
+    if rank == 0:
+        print(json.dumps({"launch_check": ok, "world": world, "gpus": args.gpus, "rank_sum": t.item()}), flush=True)
+    if not ok:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but {world} ranks")
+
+
 def run(args):
     import torch
     import torch.distributed as dist
+    if args.launch_check:
+        launch_check(args)
+        return
     world, rank, local = setup_dist(args)
     device = torch.device("cuda", local)
     from unified_video_action_amd.native import ops

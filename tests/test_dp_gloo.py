@@ -161,3 +161,41 @@ def test_mar_base_buckets_cover_every_param_once():
         assert n_store == n_train == 261_079_156, n_store  # PushT joint MAR
         assert n_hooked == 26 and n_with_hook == 26 and n_buckets == 26  # 24 Blocks + 2 diffusion trunks
         assert scale == 0.5
+
+
+def test_bench_gpus_n_spawns_n_ranks():
+    """`bench.py --gpus 2` with no launcher environment spawns two workers that rendezvous on
+    127.0.0.1 and agree on the world size (the driver's N>1 invocation path; gloo, no GPU)."""
+    import json
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    r = subprocess.run([sys.executable, "bench.py", "--gpus", "2", "--launch-check"], cwd=root, env=env,
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    line = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+    assert line == {"launch_check": True, "world": 2, "gpus": 2, "rank_sum": 1.0}
+
+
+def test_bench_under_torchrun_sees_the_launcher_world():
+    """the driver's exact N>1 command line (torch.distributed.run, 127.0.0.1) reaches the same
+    rendezvous check without spawning a second level of workers."""
+    import json
+    import os
+    import socket
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                        "--master-addr", "127.0.0.1", "--master-port", str(port), "bench.py", "--gpus", "2",
+                        "--launch-check"], cwd=root, env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [json.loads(ln) for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert lines == [{"launch_check": True, "world": 2, "gpus": 2, "rank_sum": 1.0}]
