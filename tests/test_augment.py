@@ -185,3 +185,42 @@ def test_augment_batch_dispatch_umi_libero():
     out = augment_batch({"obs": {"agentview_rgb": lib.clone()}}, seeds=[3, 4])
     torch.testing.assert_close(out["obs"]["agentview_rgb"], video_augment(lib, libero_jitter_params([3, 4])),
                                atol=0, rtol=0)
+
+
+def test_oracle_hue_matches_python_colorsys():
+    """Both restated hue paths (kornia radians, torchvision turns) against an independent
+    implementation of the same HSV model: Python's colorsys, per pixel in double precision."""
+    import colorsys
+    g = torch.Generator().manual_seed(5)
+    x = torch.rand(1, 3, 8, 25, generator=g)
+    x[0, :, 0, :5] = 0.25  # gray pixels (undefined hue: s = 0)
+    x[0, 0, 1, :5] = x[0, 1, 1, :5]  # r == g ties
+    for shift in (0.07, -0.31, 0.5):
+        want = torch.empty_like(x)
+        for i in range(8):
+            for j in range(25):
+                h, s, v = colorsys.rgb_to_hsv(*x[0, :, i, j].double().tolist())
+                want[0, :, i, j] = torch.tensor(colorsys.hsv_to_rgb((h + shift) % 1.0, s, v))
+        tv = O._jitter_op(x, 3, shift, tv=True)
+        kn = O._jitter_op(x, 3, float(torch.tensor(shift) * 2 * np.pi), tv=False)
+        torch.testing.assert_close(tv, want, atol=2e-6, rtol=0)
+        torch.testing.assert_close(kn, want, atol=2e-6, rtol=0)
+
+
+def test_oracle_sharpness_matches_pil_enhance():
+    """kornia.enhance.sharpness follows PIL's ImageEnhance.Sharpness (SMOOTH 3x3 kernel
+    (1,1,1;1,5,1;1,1,1)/13 on the interior, border pixels kept, then blended with the image);
+    the restatement against PIL itself on 8-bit images.  PIL rounds the smoothed image to 8 bits
+    and truncates the blend: (1 + |1 - f| / 2) / 255 tolerance; border pixels must match exactly
+    (a wrong kernel or border rule is off by many 8-bit steps)."""
+    from PIL import Image, ImageEnhance
+    g = torch.Generator().manual_seed(6)
+    u8 = (torch.rand(3, 20, 24, generator=g) * 255).round().to(torch.uint8)
+    img = Image.fromarray(u8.permute(1, 2, 0).numpy(), "RGB")
+    x = u8.float().unsqueeze(0) / 255.0
+    for f in (0.0, 0.4, 1.0, 1.7):
+        want = torch.from_numpy(np.array(ImageEnhance.Sharpness(img).enhance(f))).permute(2, 0, 1).float() / 255
+        got = O._sharpness_k(x, f)[0]
+        assert (got - want).abs().max().item() <= (1.0 + 0.5 * abs(1 - f)) / 255 + 1e-6, f
+        for edge in (got[:, 0] - want[:, 0], got[:, -1] - want[:, -1], got[:, :, 0] - want[:, :, 0]):
+            assert edge.abs().max().item() < 1e-6
