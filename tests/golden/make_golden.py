@@ -153,7 +153,13 @@ def gen_mar():
                   f"La={la.item():.6f} ngrads={len(names)}")
 
 
-def gen_bf16_extras():
+def gen_policy_variants_all():
+    """g2_policy_variants.npz from scratch: the fp32 run, then its bf16 extras."""
+    gen_policy_variants()
+    gen_bf16_extras(gens=(gen_policy_variants,))
+
+
+def gen_bf16_extras(gens=None):
     """The reference's own bf16 error on every MAR case and policy mode: each generator re-run in
     fp32 (must reproduce its stored fixture; adds the gradient sketches) and under CPU bf16 autocast
     (bf16 linear / matmul / conv operands, fp32 norms and losses -- the reference's
@@ -161,7 +167,7 @@ def gen_bf16_extras():
     beside the fp32 ones ("<key>_bf16"), so the bf16 tests hold this build to the reference's own
     bf16 deviation."""
     global _CAPTURE, _AUTOCAST
-    for gen in (gen_mar, gen_policy, gen_policy_variants):
+    for gen in gens or (gen_mar, gen_policy, gen_policy_variants):
         _CAPTURE, _AUTOCAST = {}, False
         gen()
         fp = _CAPTURE

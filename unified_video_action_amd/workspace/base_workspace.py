@@ -17,6 +17,25 @@ import torch
 from .checkpoint import _cpu, _loads_primitive, _plain_cfg, safe_load, strip_module
 
 
+_SKIP = object()
+
+
+def _primitive(v):
+    """v as plain Python data (paths as str), or _SKIP when it has no such form."""
+    if v is None or isinstance(v, (bool, int, float, str, bytes)):
+        return v
+    if isinstance(v, os.PathLike):
+        return os.fspath(v)
+    if isinstance(v, (list, tuple)):
+        out = [_primitive(x) for x in v]
+        return _SKIP if any(x is _SKIP for x in out) else type(v)(out)
+    if isinstance(v, dict):
+        out = {k: _primitive(x) for k, x in v.items()}
+        ok = all(isinstance(k, (str, int)) for k in out) and not any(x is _SKIP for x in out.values())
+        return out if ok else _SKIP
+    return _SKIP
+
+
 class BaseWorkspace:
     include_keys = tuple()
     exclude_keys = tuple()
@@ -59,7 +78,9 @@ class BaseWorkspace:
             payload["state_dicts"][key] = _cpu(value.state_dict())
         for key in include_keys:
             if key in self.__dict__:
-                payload["pickles"][key] = pickle.dumps(self.__dict__[key])
+                value = _primitive(self.__dict__[key])
+                if value is not _SKIP:  # only what load_payload's global-free unpickler can read back
+                    payload["pickles"][key] = pickle.dumps(value)
         self.wait_for_save()
         if use_thread:
             self._saving_thread = threading.Thread(target=torch.save, args=(payload, str(path)))

@@ -80,6 +80,9 @@ class ParamStore:
                 grad[o:o + k].copy_(p.grad.detach().reshape(-1))
             p.data = flat[o:o + k].view_as(p)
             p.grad = grad[o:o + k].view_as(p)
+            # the fused AdamW kernel rewrites p without bumping _version: any compute shadow built
+            # outside the store (bf16 switched on after binding) keys on RT.param_gen instead
+            p._uva_raw_updated = True
             if shadow is not None:
                 p._uva_shadow = shadow[o:o + k].view_as(p)
                 p._uva_shadow_owner = id(p)

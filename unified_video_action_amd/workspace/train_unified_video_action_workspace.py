@@ -77,8 +77,20 @@ class TopKCheckpointManager:
         self.path_value_map = {}
 
     def get_ckpt_path(self, data):
-        if self.k == 0 or self.monitor_key not in data:
+        if self.k == 0:
             return None
+        if self.monitor_key not in data:
+            # the reference's monitor keys (test_mean_score, val_action_l2_distances) come from the
+            # env-runner / validation paths this workspace does not run: rank by train_loss instead
+            # (lower is better), with a file name that states it, and say so once
+            if "train_loss" not in data:
+                return None
+            if not getattr(self, "_fallback", False):
+                print(f"TopKCheckpointManager: '{self.monitor_key}' is not logged by this workspace; "
+                      f"ranking top-k checkpoints by train_loss (min)")
+                self._fallback = True
+                self.monitor_key, self.mode = "train_loss", "min"
+                self.format_str = "epoch={epoch:04d}-train_loss={train_loss:.3f}.ckpt"
         value = data[self.monitor_key]
         path = os.path.join(self.save_dir, self.format_str.format(**data))
         if len(self.path_value_map) < self.k:
@@ -160,14 +172,6 @@ class TrainUnifiedVideoActionWorkspace(BaseWorkspace):
         self.world, self.rank, local = init_distributed("cuda" if torch.cuda.is_available() else "cpu")
         self.device = torch.device(device) if device is not None else (
             torch.device("cuda", local) if torch.cuda.is_available() else torch.device("cpu"))
-        if cfg.training.debug:
-            cfg.training.num_epochs = 2
-            cfg.training.max_train_steps = 3
-            cfg.training.max_val_steps = 3
-            cfg.training.rollout_every = 1
-            cfg.training.checkpoint_every = 1
-            cfg.training.val_every = 1
-            cfg.training.sample_every = 1
         self.dataset = C.instantiate(cfg.task.dataset)
         sampler = None
         dl_kw = dict(cfg.dataloader)
@@ -200,6 +204,16 @@ class TrainUnifiedVideoActionWorkspace(BaseWorkspace):
             self.ema_model.to(self.device)
         # a fresh EMAModel after the (optional) resume, as the reference builds it (:190-193)
         self.ema = C.instantiate(cfg.ema, model=self.ema_model) if cfg.training.use_ema else None
+        # debug overrides AFTER the LR schedule and the resume, in the reference's order
+        # (workspace:172-234): the schedule keeps the full run's num_training_steps
+        if cfg.training.debug:
+            cfg.training.num_epochs = 2
+            cfg.training.max_train_steps = 3
+            cfg.training.max_val_steps = 3
+            cfg.training.rollout_every = 1
+            cfg.training.checkpoint_every = 1
+            cfg.training.val_every = 1
+            cfg.training.sample_every = 1
         self.model.train()
         # on-device training augmentation instead of the dataset workers' CPU one
         self.device_augment = bool(cfg.task.get("device_augment", False))
