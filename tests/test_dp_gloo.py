@@ -1,7 +1,9 @@
 """Data-parallel reducer on the CPU with torch.distributed gloo, world_size 2:
   * the real policy (mar_base, PushT joint, fp32): get_optimizer's flat layout + default_buckets
     cover every trainable parameter exactly once (buckets + tail), every Block / diffusion trunk
-    carries its bucket hook, and the reducer is created lazily once the process group exists;
+    carries its bucket hook, and the reducer is created lazily once the process group exists; the
+    26 real hooks fired in reverse order from inside a backward pass issue ONE collective each (the
+    no-decay ranges reduce in the tail) and the reduced flat gradient equals the sum over ranks;
   * the reducer protocol on a small torch model: async per-bucket launches from backward, the
     end-of-backward completion callback, the tail bucket, 1/world averaging -- equal to a
     single-process run on the concatenated batch."""
@@ -67,8 +69,9 @@ def _tiny_worker(rank, world, port, q):
     torch.manual_seed(0)
     m = Tiny()
     store = ParamStore(_named_groups(m))
-    red = GradReducer(store, [(b, b) for b in m.blocks])
-    assert len(red.buckets) == 3 and all(len(r) <= 2 for r in red.buckets)
+    # the 8x8 weights (64 elements) are bucketed, the bias / LayerNorm ranges go to the tail
+    red = GradReducer(store, [(b, b) for b in m.blocks], min_bucket_elems=32)
+    assert len(red.buckets) == 3 and all(len(r) == 1 for r in red.buckets)
     assert int(red.coverage().min()) == 1 and int(red.coverage().max()) == 1
     g = torch.Generator().manual_seed(123)
     x = torch.randn(8, 4, generator=g)[rank * 4:(rank + 1) * 4]
@@ -139,9 +142,40 @@ def _policy_worker(rank, world, port, q):
         inside[o:o + k] = True
     n_trainable = sum(p.numel() for p in pol.model.parameters() if p.requires_grad)
     hooked = [m for m in pol.model.modules() if isinstance(m, (Block, SimpleMLPAdaLN))]
+    # the real hooks of the 26 modules fired from inside a backward pass in reverse order (as the
+    # fused BlockFn / AdaLNTrunkFn backwards fire them), each launching ONE collective; the
+    # end-of-backward callback reduces the tail (all no-decay ranges + the rest) and waits
+    calls = []
+    real_all_reduce = dist.all_reduce
+
+    def counting_all_reduce(t, *a, **k):
+        calls.append(t.numel())
+        return real_all_reduce(t, *a, **k)
+
+    dist.all_reduce = counting_all_reduce
+    idx = torch.arange(st.total, dtype=torch.float32)
+    st.grad.copy_((rank + 1) * torch.remainder(idx, 977.0))
+
+    class FireHooks(torch.autograd.Function):
+        @staticmethod
+        def forward(ctx, x):
+            return x.clone()
+
+        @staticmethod
+        def backward(ctx, g):
+            for m in reversed(hooked):
+                m._uva_bucket_hook()
+            return g
+
+    red.arm()
+    FireHooks.apply(torch.zeros(1, requires_grad=True)).sum().backward()
+    dist.all_reduce = real_all_reduce
+    ok = bool(torch.equal(st.grad[inside], 3.0 * torch.remainder(idx, 977.0)[inside]))
+    n_bucket_calls = sum(1 for n in calls if n >= red.MIN_BUCKET_ELEMS)
     q.put((rank, int(cov[inside].min()), int(cov[inside].max()), int(cov.max()), st.n_params, n_trainable,
            len(hooked), sum(callable(getattr(m, "_uva_bucket_hook", None)) for m in hooked), opt.grad_scale,
-           len(red.buckets)))
+           len(red.buckets), ok, len(calls), len(red.tail), sum(len(b) for b in red.buckets), n_bucket_calls,
+           red.pending))
     dist.destroy_process_group()
 
 
@@ -156,11 +190,16 @@ def test_mar_base_buckets_cover_every_param_once():
     res = [q.get(timeout=280) for _ in range(world)]
     for p in procs:
         p.join(timeout=30)
-    for rank, cmin, cmax, call, n_store, n_train, n_hooked, n_with_hook, scale, n_buckets in res:
+    for (rank, cmin, cmax, call, n_store, n_train, n_hooked, n_with_hook, scale, n_buckets, ok, n_calls, n_tail,
+         n_ranges, n_bucket_calls, pending) in res:
         assert cmin == 1 and cmax == 1 and call == 1, (cmin, cmax, call)
         assert n_store == n_train == 261_079_156, n_store  # PushT joint MAR
         assert n_hooked == 26 and n_with_hook == 26 and n_buckets == 26  # 24 Blocks + 2 diffusion trunks
         assert scale == 0.5
+        assert ok, "reduced flat gradient != sum over ranks"
+        assert n_ranges == 26 and n_bucket_calls >= 26, (n_ranges, n_bucket_calls)  # one collective per bucket
+        assert n_calls == 26 + n_tail and n_tail <= 4, (n_calls, n_tail)  # + the few contiguous tail ranges
+        assert not pending
 
 
 def test_bench_gpus_n_spawns_n_ranks():

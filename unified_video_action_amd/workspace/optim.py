@@ -303,8 +303,12 @@ class GradReducer:
     several backward passes is not supported: the reference configs all use
     gradient_accumulate_every = 1)."""
 
-    def __init__(self, store, buckets, group=None):
+    MIN_BUCKET_ELEMS = 1 << 16  # ranges below 256 KB of fp32 gradients join the tail collective
+
+    def __init__(self, store, buckets, group=None, min_bucket_elems=None):
         """buckets: [(module whose params form the bucket, module whose fused backward fires the hook)]"""
+        if min_bucket_elems is not None:
+            self.MIN_BUCKET_ELEMS = min_bucket_elems
         self.store = store
         self.group = group
         self.world = dist.get_world_size(group) if dist.is_available() and dist.is_initialized() else 1
@@ -315,7 +319,11 @@ class GradReducer:
         self._queued = False
         covered = []
         for i, (m, owner) in enumerate(buckets):
-            rs = store.ranges_of(m)
+            # one collective per bucket: a module's params sit in two group regions of the flat
+            # buffer (weight decay, then none); its small no-decay range (LayerNorm / bias, ~40 KB
+            # per Block) goes to the tail, where the no-decay ranges of all modules are contiguous
+            # and reduce as ONE collective after backward
+            rs = [r for r in store.ranges_of(m) if r[1] >= self.MIN_BUCKET_ELEMS]
             self.buckets.append(rs)
             covered += rs
             if self.world > 1:
