@@ -49,19 +49,8 @@ int uva_gemm(int in_dtype, int out_dtype, int ta, int tb, const void* A, const v
 /* res_dtype: dtype of `residual`; gate (dtype gate_dtype, ld ldg) multiplies the value after
  * dropout and before the residual add (adaLN: x + gate * mlp(h), diffusion_loss.py:163-167). */
 /* workspace (fp32, ws_floats) enables deterministic split-K for few-tile / long-K products
- * (the dW GEMMs, K = tokens); pass NULL/0 to disable.
- * Epilogue-free bf16 products (no bias / residual / aux / act / dropout / gate, batch 1, alpha 1,
- * beta 0 or 1: the backward's dX and dW GEMMs) are routed to hipBLASLt when uva_lt_enabled(). */
-
-/* ---- hipBLASLt route for plain bf16 GEMMs (blaslt.hip) ---------------------------------
- * Same operand convention as uva_gemm (bf16 A/B, fp32 accumulate, out_dtype bf16 or fp32,
- * C = alpha * op(A) op(B) + beta * C).  Returns 0, -1 when the library has no algorithm for
- * the shape (uva_gemm then uses its own kernels), or an error code.  uva_lt_mode(0/1) switches
- * the route off/on (default from UVA_GEMM_LIB, on) and returns the previous mode (-1 = unset). */
-int uva_lt_gemm(int out_dtype, int ta, int tb, const void* A, const void* B, void* C, int M, int N, int K,
-                long long lda, long long ldb, long long ldc, float alpha, float beta, hipStream_t stream);
-int uva_lt_mode(int mode);
-int uva_lt_enabled();
+ * (the dW GEMMs, K = tokens); pass NULL/0 to disable.  Every product runs on this library's own
+ * kernels (no vendor BLAS is linked). */
 
 /* ---- convolution as implicit GEMM over NHWC (bf16: MFMA, fp32: VALU) -----------------
  * out[n,oh,ow,co] = bias[co] + residual + sum_{kh,kw,ci} act(in[n,ih,iw,ci]) w[co][kh][kw][ci]
@@ -72,18 +61,9 @@ int uva_lt_enabled();
  * (vae/vaekl.py:36-113,116-159,162-273,469) and DiffActLoss.conv (diffusion_action_loss.py:42-46). */
 /* Which kernel a bf16 GEMM of this shape runs on (test / tuning introspection; no device work):
  * kernel | BN << 4 | splits << 16; kernel 0 = VALU, 1 = MFMA register-staged 128x128,
- * 2 = MFMA LDS-DMA 128x128, 3 = MFMA 8-phase 256-row (BN 128/256), splits = split-K slices. */
-/* Diagnostic: per-wave s_memtime segment sums of the last stamped 8-phase GEMM (UVA_8PH_VAR odd):
- * [16 blocks][8 waves][read+issue, barrier-1, mfma issue, barrier-2, loop total]. */
-int uva_debug_gemm8_stamps(unsigned long long* host);
-int uva_debug_conv_stamps(unsigned long long* host);
-int uva_debug_conv_occupancy(int tr, int gn);
+ * 2 = MFMA LDS-DMA 128x128, 3 = MFMA 8-phase (256x256 or 128x384 tiles), splits = split-K slices. */
 long long uva_gemm_plan(int in_dtype, int ta, int tb, int M, int N, int K, int batch, int gn_prologue,
                         long long ws_floats);
-/* Route full-tile bf16 GEMMs with an alpha (+ bias) epilogue and >= 4 K-tiles through the
- * persistent 8-phase kernel gemm_8pp (on != 0) or the per-tile gemm_8ph (0, the default;
- * UVA_8PP=1 sets the initial value).  Test / tuning switch; same results within fp32 rounding. */
-int uva_gemm_set_8pp(int on);
 int uva_conv2d(int dtype, const void* in, const void* w, void* out, const float* bias, const void* residual, int Nimg,
                int Hin, int Win, int Ci, int Co, int ks, int stride, int pad_t, int pad_l, int Hout, int Wout,
                const float* gn_scale, const float* gn_shift, int gn_silu, int act, float* gn_part,

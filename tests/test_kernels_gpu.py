@@ -29,52 +29,44 @@ def _stored(op, t_flag):
     return op.t().contiguous() if t_flag else op.contiguous()
 
 
-@pytest.mark.parametrize("route", ["kernels", "hipblaslt"])
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("ta,tb", [(0, 0), (0, 1), (1, 0), (1, 1)])
 @pytest.mark.parametrize("M,N,K", [(256, 384, 192), (300, 200, 72), (130, 136, 520), (64, 48, 2)])
-def test_gemm_layouts(route, dtype, ta, tb, M, N, K):
-    """Every operand layout against fp32 torch, on the hand-written kernels and (bf16, epilogue-free)
-    on the hipBLASLt route of blaslt.hip; fp32 and bf16 outputs."""
+def test_gemm_layouts(dtype, ta, tb, M, N, K):
+    """Every operand layout against fp32 torch; fp32 and bf16 outputs."""
     from unified_video_action_amd.native import ops
     if dtype == torch.bfloat16 and ((ta and M % 8) or (tb and N % 8)):
         pytest.skip("m-contiguous bf16 operands need 8-aligned dims (host pads these)")
-    if route == "hipblaslt" and dtype != torch.bfloat16:
-        pytest.skip("library route is bf16-only")
     a = torch.randn(M, K, device=DEV).to(dtype)
     b = torch.randn(N, K, device=DEV).to(dtype)
     A, B = _stored(a, ta), _stored(b, tb)
     ref = a.float() @ b.float().t()
-    with ops.gemm_library("library" if route == "hipblaslt" else "kernels"):
-        for odt in ((torch.float32, torch.bfloat16) if dtype == torch.bfloat16 else (torch.float32,)):
-            C = torch.empty(M, N, device=DEV, dtype=odt)
-            ops.gemm(A, B, C, M, N, K, A.stride(0), B.stride(0), C.stride(0), ta, tb)
-            tol = 1e-5 if dtype == torch.float32 else (5e-3 if odt == torch.float32 else 1e-2)
-            assert rel_err(C, ref) < tol
+    for odt in ((torch.float32, torch.bfloat16) if dtype == torch.bfloat16 else (torch.float32,)):
+        C = torch.empty(M, N, device=DEV, dtype=odt)
+        ops.gemm(A, B, C, M, N, K, A.stride(0), B.stride(0), C.stride(0), ta, tb)
+        tol = 1e-5 if dtype == torch.float32 else (5e-3 if odt == torch.float32 else 1e-2)
+        assert rel_err(C, ref) < tol
 
 
-@pytest.mark.parametrize("route", ["kernels", "library", "tuned"])
 @pytest.mark.parametrize("M,N,K", [(768, 768, 16384), (3072, 768, 8192), (32768, 768, 3072)])
-def test_gemm_backward_shapes_accumulate(route, M, N, K):
+def test_gemm_backward_shapes_accumulate(M, N, K):
     """The backward's products at MAR shapes: dW += dY^T X (ta = tb = 1, fp32 grad, beta = 1) and
-    dX = dY W (tb = 1); kernel, library and tuned (timed pick; the real output untouched by the
-    timing runs) routes agree with fp32 torch."""
+    dX = dY W (tb = 1) agree with fp32 torch."""
     from unified_video_action_amd.native import ops
     torch.manual_seed(M + N + K)
-    with ops.gemm_library(route):
-        if K >= 8192:  # dW: A = dY stored [K tokens][M], B = X stored [K tokens][N]
-            dy = torch.randn(K, M, device=DEV).to(torch.bfloat16)
-            x = torch.randn(K, N, device=DEV).to(torch.bfloat16)
-            C = torch.randn(M, N, device=DEV)
-            ref = C.double() + dy.double().t() @ x.double()
-            ops.gemm(dy, x, C, M, N, K, M, N, N, 1, 1, beta=1.0)
-        else:  # dX: A = dY [M][K], B = W stored [K][N]
-            dy = torch.randn(M, K, device=DEV).to(torch.bfloat16)
-            w = (torch.randn(K, N, device=DEV) * 0.05).to(torch.bfloat16)
-            C = torch.empty(M, N, device=DEV)
-            ref = dy.double() @ w.double()
-            ops.gemm(dy, w, C, M, N, K, K, N, N, 0, 1)
-        assert rel_err(C, ref) < 2e-3
+    if K >= 8192:  # dW: A = dY stored [K tokens][M], B = X stored [K tokens][N]
+        dy = torch.randn(K, M, device=DEV).to(torch.bfloat16)
+        x = torch.randn(K, N, device=DEV).to(torch.bfloat16)
+        C = torch.randn(M, N, device=DEV)
+        ref = C.double() + dy.double().t() @ x.double()
+        ops.gemm(dy, x, C, M, N, K, M, N, N, 1, 1, beta=1.0)
+    else:  # dX: A = dY [M][K], B = W stored [K][N]
+        dy = torch.randn(M, K, device=DEV).to(torch.bfloat16)
+        w = (torch.randn(K, N, device=DEV) * 0.05).to(torch.bfloat16)
+        C = torch.empty(M, N, device=DEV)
+        ref = dy.double() @ w.double()
+        ops.gemm(dy, w, C, M, N, K, K, N, N, 0, 1)
+    assert rel_err(C, ref) < 2e-3
 
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])

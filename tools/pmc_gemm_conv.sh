@@ -9,7 +9,7 @@ P2="SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS
 i=0
 for P in "$P1" "$P2"; do
   i=$((i+1))
-  UVA_GEMM_LIB=0 timeout -s KILL 90 rocprofv3 --pmc $P --output-format csv -d $O/g$i -o run -- python3 tools/tools_gemm_one.py 8192 8192 8192 0 0 3 > $O/g$i.log 2>&1 || { echo "gemm pass $i failed"; tail -3 $O/g$i.log; exit 1; }
+  timeout -s KILL 90 rocprofv3 --pmc $P --output-format csv -d $O/g$i -o run -- python3 tools/tools_gemm_one.py 8192 8192 8192 0 0 3 > $O/g$i.log 2>&1 || { echo "gemm pass $i failed"; tail -3 $O/g$i.log; exit 1; }
   timeout -s KILL 90 rocprofv3 --pmc $P --output-format csv -d $O/c$i -o run -- python3 tools/tools_conv_phase.py > $O/c$i.log 2>&1 || { echo "conv pass $i failed"; tail -3 $O/c$i.log; exit 1; }
 done
 echo done

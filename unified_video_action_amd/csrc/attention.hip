@@ -32,7 +32,6 @@
 // dO' = dO / (1 - p) is prepared by the pre kernel (with D = rowsum(dO * O)), so the dropout
 // scale costs nothing inside the loops.
 #include "common.h"
-#include <stdlib.h>
 
 #define AT_LD 72
 #define AT_TILE (64 * AT_LD)
@@ -183,7 +182,7 @@ __global__ __launch_bounds__(256) void attn_mask_kernel(uint64_t* __restrict__ M
 // =====================================================================================
 // forward
 // =====================================================================================
-// KT = keys per LDS tile (64 or 128).  Default 64 at three waves per SIMD (168 VGPRs, 36.9 KB of
+// KT = keys per LDS tile: 64 at three waves per SIMD (168 VGPRs, 36.9 KB of
 // LDS per workgroup): the loop is latency-bound (PMC: 0.39 of wave-cycles issue-stalled, MFMA busy
 // 0.20, VALU active 0.33 at two waves per SIMD), so the third wave buys more than the 128-key tile's
 // longer compute rounds (0.167 vs 0.174 ms at B32 N1024 H12 p0.1, same box).  A 32x32x16 variant
@@ -730,15 +729,9 @@ extern "C" int uva_attn_fwd(const void* qkv, void* out, float* lse2, const void*
   uva_drop_params(drop_p, &th, &ds);
   dim3 grid((N + 127) / 128, B * H);
   const float c = scale * 1.4426950408889634f;
-  static const int kt_env = getenv("UVA_ATTN_FWD_KT") ? atoi(getenv("UVA_ATTN_FWD_KT")) : 64;
-  const bool k128 = kt_env == 128 && N % 128 == 0;
   const uint64_t* MQ = drop ? (const uint64_t*)mask : nullptr;
-  if (drop && k128)
-    attn_fwd_kernel<true, 128, 2><<<grid, 256, 0, s>>>((const bf16*)qkv, (bf16*)out, lse2, MQ, N, H, c, ds);
-  else if (drop)
+  if (drop)
     attn_fwd_kernel<true, 64, 3><<<grid, 256, 0, s>>>((const bf16*)qkv, (bf16*)out, lse2, MQ, N, H, c, ds);
-  else if (k128)
-    attn_fwd_kernel<false, 128, 2><<<grid, 256, 0, s>>>((const bf16*)qkv, (bf16*)out, lse2, nullptr, N, H, c, 1.0f);
   else
     attn_fwd_kernel<false, 64, 3><<<grid, 256, 0, s>>>((const bf16*)qkv, (bf16*)out, lse2, nullptr, N, H, c, 1.0f);
   UVA_LAUNCH_CHECK();

@@ -118,14 +118,12 @@ __device__ __forceinline__ void conv_vm_wait(int n) {
 #undef CVW
 }
 
-// VAR bits (UVA_CONV_VAR / UVA_CONV_GN_VAR; production non-GN = 12, GN = 64): 64 weights in VGPRs
-// (RB below; A reads pipelined by k-half across taps measured slower: 5.75 -> 6.16 ms); 16 the next chunk's
-// halo staging spread over taps 1..ROUNDS (one round per step); 1 per-tile prologue / main-loop /
-// epilogue s_memtime stamps of the first 16 blocks (uva_debug_conv_stamps); 2 one halo buffer + a
-// 3-slot weight ring (measured slower); 4 both k-halves' fragment reads issued before the MFMAs
-// (inline-asm reads, counted lgkmcnt); 8 halo staged by LDS-DMA (non-GN; no register staging,
-// zeros from the buffer descriptor's range check)
-__device__ unsigned long long g_uva_conv_stamps[16 * 8 * 4];
+// VAR bits (the library builds non-GN = 12 and GN = 64 only): 64 weights in VGPRs (RB below; A
+// reads pipelined by k-half across taps measured slower: 5.75 -> 6.16 ms); 4 both k-halves' fragment
+// reads issued before the MFMAs (inline-asm reads, counted lgkmcnt); 8 halo staged by LDS-DMA
+// (non-GN; no register staging, zeros from the buffer descriptor's range check).  Compile-time
+// alternatives measured slower and not built: 16 the next chunk's halo staging spread over taps
+// 1..ROUNDS; 2 one halo buffer + a 3-slot weight ring.
 template <int BN, bool GN, int VAR, int TR>
 __global__ __launch_bounds__(TR * 32, 16 / TR) void conv3x3_halo(const bf16* __restrict__ in, const bf16* __restrict__ wt,
                                                        bf16* __restrict__ out, const float* __restrict__ bias,
@@ -145,8 +143,6 @@ __global__ __launch_bounds__(TR * 32, 16 / TR) void conv3x3_halo(const bf16* __r
   static_assert(!SPREAD || ConvHCfg<BN, TR>::ROUNDS <= 8, "one staging round per tap 1..8");
   using G = ConvHCfg<BN, TR, R3, HD, RB>;
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  unsigned long long st0 = 0, st1 = 0, st2 = 0;
-  if constexpr (VAR & 1) asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(st0)::"memory");
   bf16* halo = (bf16*)smem;
   bf16* bimg = halo + G::NHB * G::HALO_ELEMS;
   const int tiles_x = W / CH_T, tiles_y = H / TR, ncb = Co / BN;
@@ -322,7 +318,6 @@ __global__ __launch_bounds__(TR * 32, 16 / TR) void conv3x3_halo(const bf16* __r
 #pragma unroll
     for (int i = 0; i < NPRE; ++i) hreg[i] = *res_ptr(i);
   };
-  if constexpr (VAR & 1) asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(st1)::"memory");
   int prev_loads = 0;  // R3: global loads the previous step issued after its weight DMA
   if constexpr (RB) {
     // A fragment (ks, f) of tap (kh, kw): halo pixel (wm*FM + f + kh, frow + kw), channels
@@ -508,7 +503,6 @@ __global__ __launch_bounds__(TR * 32, 16 / TR) void conv3x3_halo(const bf16* __r
     }
   }
 
-  if constexpr (VAR & 1) asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(st2)::"memory");
   // ---- epilogue: 128-pixel halves (tile rows 0-7 [, 8-15]) staged through LDS as fp32
   float* T = (float*)smem;
   float bv[8];
@@ -613,14 +607,6 @@ __global__ __launch_bounds__(TR * 32, 16 / TR) void conv3x3_halo(const bf16* __r
     }
     ch_lds_barrier();
   }
-  if constexpr (VAR & 1) {
-    unsigned long long st3;
-    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(st3)::"memory");
-    if (lane == 0 && blockIdx.x < 16) {
-      unsigned long long* o = g_uva_conv_stamps + (blockIdx.x * 8 + wid) * 4;
-      o[0] = st1 - st0; o[1] = st2 - st1; o[2] = st3 - st2; o[3] = st3;
-    }
-  }
 }
 
 // eligibility of the halo kernel (host side mirror: native/ops.py conv_halo_ok)
@@ -641,9 +627,9 @@ extern "C" int uva_conv3x3_halo(const void* in, const void* w, void* out, const 
   const int bn = halo_bn(Nimg, H, W, Ci, Co);
   if (!bn || (((uintptr_t)in | (uintptr_t)w | (uintptr_t)out | (uintptr_t)residual) % 16)) return (int)hipErrorInvalidValue;
   if ((gn_scale == nullptr) != (gn_shift == nullptr)) return (int)hipErrorInvalidValue;
-  // TR = 8 (two co-resident 256-thread workgroups per CU) unless UVA_CONV_TR=16
-  static const int tr_env = getenv("UVA_CONV_TR") ? atoi(getenv("UVA_CONV_TR")) : 8;
-  const int tr = tr_env == 16 ? 16 : 8;
+  // 8-row tiles: two co-resident 256-thread workgroups per CU (16-row tiles at one 512-thread
+  // workgroup per CU measured slower: level-0 7.54 vs 6.77 ms)
+  constexpr int tr = 8;
   const long long nblk = (long long)Nimg * (H / tr) * (W / CH_T) * (Co / bn);
   if (nblk >= (1ll << 31)) return (int)hipErrorInvalidValue;
 #define CH_LAUNCH(BNV, GNV, VARV, TRV)                                                                         \
@@ -660,35 +646,12 @@ extern "C" int uva_conv3x3_halo(const void* in, const void* w, void* out, const 
         (const bf16*)in, (const bf16*)w, (bf16*)out, bias, (const bf16*)residual, gn_scale, gn_shift, gn_silu, \
         gn_part, Nimg, H, W, Ci, Co);                                                                          \
   } while (0)
-  // production (non-GN): 12 = halo by LDS-DMA (8) + both k-halves' fragment reads issued up front (4)
-  static const int var = getenv("UVA_CONV_VAR") ? atoi(getenv("UVA_CONV_VAR")) : 12;
-  // production GN variant: 64 (weights in VGPRs, one barrier per chunk; same-box level-0 conv
-  // 6.61 -> 6.49 ms with the bias + residual + GN-stats epilogue, 7.02 -> 6.79 ms in the bench)
-  static const int gvar = getenv("UVA_CONV_GN_VAR") ? atoi(getenv("UVA_CONV_GN_VAR")) : 64;
-  if (tr == 16) {
-    if (gn_scale) CH_LAUNCH(128, true, 0, 16);
-    else if (var == 1) CH_LAUNCH(128, false, 1, 16);
-    else if (var == 0) CH_LAUNCH(128, false, 0, 16);
-    else CH_LAUNCH(128, false, 12, 16);
-  } else {
-    if (gn_scale) {
-      if (gvar == 0) CH_LAUNCH(128, true, 0, 8);
-      else if (gvar == 64) CH_LAUNCH(128, true, 64, 8);
-      else if (gvar == 65) CH_LAUNCH(128, true, 65, 8);  // + per-tile phase stamps
-      else if (gvar == 4) CH_LAUNCH(128, true, 4, 8);
-      else if (gvar == 16) CH_LAUNCH(128, true, 16, 8);
-      else CH_LAUNCH(128, true, 20, 8);
-    } else if (var == 1) CH_LAUNCH(128, false, 1, 8);
-    else if (var == 2) CH_LAUNCH(128, false, 2, 8);
-    else if (var == 3) CH_LAUNCH(128, false, 3, 8);
-    else if (var == 4) CH_LAUNCH(128, false, 4, 8);
-    else if (var == 6) CH_LAUNCH(128, false, 6, 8);
-    else if (var == 8) CH_LAUNCH(128, false, 8, 8);
-    else if (var == 12) CH_LAUNCH(128, false, 12, 8);
-    else if (var == 13) CH_LAUNCH(128, false, 13, 8);
-    else if (var == 0) CH_LAUNCH(128, false, 0, 8);
-    else CH_LAUNCH(128, false, 12, 8);
-  }
+  // non-GN: 12 = halo by LDS-DMA (8) + both k-halves' fragment reads issued up front (4);
+  // GN: 64 = weights in VGPRs, one barrier per chunk (same-box level-0 conv 6.61 -> 6.49 ms with the
+  // bias + residual + GN-stats epilogue, 7.02 -> 6.79 ms in the bench).  The other VAR bits are the
+  // measured-slower alternatives, compile-time only and not built.
+  if (gn_scale) CH_LAUNCH(128, true, 64, 8);
+  else CH_LAUNCH(128, false, 12, 8);
 #undef CH_LAUNCH
   UVA_LAUNCH_CHECK();
   return 0;
@@ -860,23 +823,3 @@ extern "C" int uva_conv_in8(const void* in, const void* w, void* out, const floa
   return 0;
 }
 
-extern "C" int uva_debug_conv_stamps(unsigned long long* host) {
-  return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_uva_conv_stamps), sizeof(g_uva_conv_stamps));
-}
-
-// resident workgroups per CU of the halo conv variant (tile rows tr, with/without GN prologue)
-extern "C" int uva_debug_conv_occupancy(int tr, int gn) {
-  int nb = -1;
-#define CH_OCC(GNV, TRV)                                                                                       \
-  do {                                                                                                         \
-    const int lb = ConvHCfg<128, TRV>::LDS_BYTES;                                                              \
-    (void)hipFuncSetAttribute((const void*)conv3x3_halo<128, GNV, 0, TRV>,                                     \
-                              hipFuncAttributeMaxDynamicSharedMemorySize, lb);                                 \
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, (const void*)conv3x3_halo<128, GNV, 0, TRV>, TRV * 32, \
-                                                     lb) != hipSuccess) nb = -1;                               \
-  } while (0)
-  if (tr == 16) { if (gn) CH_OCC(true, 16); else CH_OCC(false, 16); }
-  else { if (gn) CH_OCC(true, 8); else CH_OCC(false, 8); }
-#undef CH_OCC
-  return nb;
-}

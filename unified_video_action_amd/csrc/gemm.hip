@@ -16,10 +16,6 @@
 //  * gemm_generic    -- fp32 FMA on the VALU, any shape / dtype; the fp32 parity
 //    path and the tiny-K/N projections (K = 2, 4, 10 ...).
 #include "common.h"
-#include "blaslt.h"
-#include <map>
-#include <mutex>
-#include <tuple>
 #include <stdio.h>
 #include <stdlib.h>
 
@@ -969,18 +965,17 @@ struct Gemm8Cfg {
   static constexpr int LDS_BYTES = (2 * STAGE * 2 > EPI_BYTES) ? 2 * STAGE * 2 : EPI_BYTES;
 };
 
-// VAR: diagnostic build bits (0 = production): 1 s_memtime stamps per phase segment, 2 no wave-group
-// stagger, 4 no compiler memory fences around barriers, 8 lgkmcnt after the barrier (timing only:
-// breaks the WAR order), 16 no s_setprio, 32 per-tile prologue / K-loop / epilogue stamps,
-// 64 __syncthreads() epilogue barriers (drain the stores; the default orders LDS only), 128 (with 32) epilogue chunk-0 staging / store split, 256 the fast-path
-// DMA (full tiles), 512 no output stores (timing only), 1024 non-temporal output stores
-// (tools_gemm8_phase.py: the epilogue of a 256x256 bf16 tile is ~29k ticks at K=768, mostly the
-// output stores of all CUs landing at once)
+// VAR: 0 = the general path, 256 = the fast path (full tiles, K a multiple of 64: per-lane DMA
+// sources precomputed once).  Only these two are built into the library.  The other bits name
+// the structural alternatives that were measured against them and lost (same-box A/B, DESIGN.md
+// §5); they stay as compile-time switches of this template for re-measurement, never selected at
+// run time: 2 no wave-group stagger, 4 no compiler memory fences around barriers, 8 lgkmcnt after
+// the barrier (timing only: breaks the WAR order), 16 no s_setprio, 64 __syncthreads() epilogue
+// barriers, 512 no output stores (timing only), 1024 non-temporal output stores.
 #define GEMM8_SYNC()                                     \
   do {                                                   \
     if constexpr (!(VAR & 4)) asm volatile("" ::: "memory"); \
   } while (0)
-__device__ unsigned long long g_uva_stamps[16 * 8 * 5];
 
 template <int TA, int TB, int BN, typename TC, int VAR = 0>
 __global__ __launch_bounds__(512, 1) void gemm_8ph(const bf16* __restrict__ A, const bf16* __restrict__ B,
@@ -991,14 +986,6 @@ __global__ __launch_bounds__(512, 1) void gemm_8ph(const bf16* __restrict__ A, c
   static_assert(BN != 384 || TA != 2, "the 128x384 tile has no conv / GN-statistics epilogue");
   extern __shared__ __attribute__((aligned(16))) char smem[];
   bf16* lds = (bf16*)smem;
-  unsigned long long st_entry = 0, st_after_pro = 0, st_after_loop = 0, st_e1 = 0, st_e2 = 0;
-  if constexpr (VAR & 32) asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(st_entry)::"memory");
-  if constexpr ((VAR & 2048) != 0) {  // experiment: stagger the first round of blocks in 4 groups
-    if (blockIdx.x < 256) {
-      const int n = (blockIdx.x & 3) * 2;
-      for (int i = 0; i < n; ++i) __builtin_amdgcn_s_sleep(127);
-    }
-  }
   const int z = blockIdx.z, zo = z / bs.binner, zi = z % bs.binner;
   A += zo * bs.sAo + zi * bs.sAi;
   B += zo * bs.sBo + zi * bs.sBi;
@@ -1126,18 +1113,6 @@ __global__ __launch_bounds__(512, 1) void gemm_8ph(const bf16* __restrict__ A, c
   const int grp = __builtin_amdgcn_readfirstlane(wid >> 2);
   if (!(VAR & 2) && grp == 1) __builtin_amdgcn_s_barrier();
   GEMM8_SYNC();
-  unsigned long long st_sum[4] = {0, 0, 0, 0}, st_t0 = 0, st_t1 = 0, st_loop0 = 0;
-#define GEMM8_STAMP(dst)                                                                                  \
-  do {                                                                                                    \
-    if constexpr (VAR & 1) {                                                                              \
-      __builtin_amdgcn_sched_barrier(0);                                                                  \
-      asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(dst)::"memory");                         \
-      __builtin_amdgcn_sched_barrier(0);                                                                  \
-    }                                                                                                     \
-  } while (0)
-  GEMM8_STAMP(st_loop0);
-  st_t0 = st_loop0;
-  if constexpr (VAR & 32) asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(st_after_pro)::"memory");
 
 #define GEMM8_QUAD(AH, BH, FB)                                                                            \
   if constexpr (!(VAR & 16)) __builtin_amdgcn_s_setprio(1);                                               \
@@ -1146,30 +1121,18 @@ __global__ __launch_bounds__(512, 1) void gemm_8ph(const bf16* __restrict__ A, c
   _Pragma("unroll") for (int ks = 0; ks < 2; ++ks)                                                        \
     acc[AH * G::HA + f][BH * G::HB + g] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(                       \
         fa[f][ks], FB[g][ks], acc[AH * G::HA + f][BH * G::HB + g], 0, 0, 0);                              \
-  if constexpr (!(VAR & 16)) __builtin_amdgcn_s_setprio(0);                                               \
-  GEMM8_STAMP(st_t1);                                                                                     \
-  st_sum[2] += st_t1 - st_t0;                                                                             \
-  st_t0 = st_t1
+  if constexpr (!(VAR & 16)) __builtin_amdgcn_s_setprio(0)
 
 #define GEMM8_SYNC_MFMA_BEGIN()                                                                           \
   if constexpr (!(VAR & 8)) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); /* retire reads BEFORE the barrier */ \
-  GEMM8_STAMP(st_t1);                                                                                     \
-  st_sum[0] += st_t1 - st_t0;                                                                             \
-  st_t0 = st_t1;                                                                                          \
   GEMM8_SYNC();                                                                                           \
   __builtin_amdgcn_s_barrier();                                                                           \
   if constexpr (VAR & 8) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");                              \
-  GEMM8_STAMP(st_t1);                                                                                     \
-  st_sum[1] += st_t1 - st_t0;                                                                             \
-  st_t0 = st_t1;                                                                                          \
   __builtin_amdgcn_sched_barrier(0)
 
 #define GEMM8_SYNC_MFMA_END()                                                                             \
   __builtin_amdgcn_s_barrier();                                                                           \
-  GEMM8_SYNC();                                                                                           \
-  GEMM8_STAMP(st_t1);                                                                                     \
-  st_sum[3] += st_t1 - st_t0;                                                                             \
-  st_t0 = st_t1
+  GEMM8_SYNC()
 
   for (int t = 0; t < nt; ++t) {
     const int buf = t & 1;
@@ -1222,16 +1185,6 @@ __global__ __launch_bounds__(512, 1) void gemm_8ph(const bf16* __restrict__ A, c
 #undef GEMM8_QUAD
 #undef GEMM8_SYNC_MFMA_BEGIN
 #undef GEMM8_SYNC_MFMA_END
-  if constexpr (VAR & 1) {
-    // [read+issue, barrier-1, mfma issue, barrier-2, whole loop] per wave, first 16 blocks
-    GEMM8_STAMP(st_t1);
-    if ((threadIdx.x & 63) == 0 && blockIdx.x < 16 && blockIdx.y == 0 && blockIdx.z == 0) {
-      unsigned long long* o = g_uva_stamps + (blockIdx.x * 8 + wid) * 5;
-      o[0] = st_sum[0]; o[1] = st_sum[1]; o[2] = st_sum[2]; o[3] = st_sum[3]; o[4] = st_t1 - st_loop0;
-    }
-  }
-#undef GEMM8_STAMP
-  if constexpr (VAR & 32) asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(st_after_loop)::"memory");
   if (!(VAR & 2) && grp == 0) __builtin_amdgcn_s_barrier();  // re-align barrier counts: every wave is past its last MFMA
   GEMM8_SYNC();
 
@@ -1266,9 +1219,6 @@ __global__ __launch_bounds__(512, 1) void gemm_8ph(const bf16* __restrict__ A, c
             T[(rbase + i * 16 + (lane >> 4) * 4 + r) * G::TP + wc * G::RWB + j * 16 + (lane & 15)] = acc[i][j][r];
     }
     if constexpr (VAR & 64) __syncthreads(); else epi_lds_barrier();
-    if constexpr (VAR & 128) {
-      if (chunk == 0) asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(st_e1)::"memory");
-    }
     constexpr int NIT = (ER + RPP - 1) / RPP;
     const int rowb = m0 + chunk * ER + rsub;
     const int rowe = min(M, m0 + chunk * ER + ER);  // rows of this chunk (rl < ER)
@@ -1374,9 +1324,6 @@ __global__ __launch_bounds__(512, 1) void gemm_8ph(const bf16* __restrict__ A, c
         }
       }
     }
-    if constexpr (VAR & 128) {
-      if (chunk == 0) asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(st_e2)::"memory");
-    }
     if constexpr (TA == 2) {
       if (gn_part) {
         // per-(128-row chunk, group) sums: lanes sharing c8 inside a wave, then the 8 waves via LDS
@@ -1417,314 +1364,6 @@ __global__ __launch_bounds__(512, 1) void gemm_8ph(const bf16* __restrict__ A, c
     // after the last chunk nothing reads T again
     if constexpr (VAR & 64) __syncthreads(); else if (chunk == 0) epi_lds_barrier();
   }
-  if constexpr (VAR & 32) {
-    unsigned long long st_end;
-    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(st_end)::"memory");
-    if ((threadIdx.x & 63) == 0 && blockIdx.x < 16 && blockIdx.y == 0 && blockIdx.z == 0) {
-      unsigned long long* o = g_uva_stamps + (blockIdx.x * 8 + (threadIdx.x >> 6)) * 5;
-      if constexpr (VAR & 128) {  // epilogue split: chunk-0 staging, chunk-0 stores, rest
-        o[0] = st_after_loop - st_entry; o[1] = st_e1 - st_after_loop; o[2] = st_e2 - st_e1; o[3] = st_end - st_e2;
-      } else {
-        o[0] = st_after_pro - st_entry; o[1] = st_after_loop - st_after_pro; o[2] = st_end - st_after_loop;
-        o[3] = st_entry;
-      }
-      o[4] = st_end;
-    }
-  }
-}
-
-// =====================================================================================
-// Persistent 8-phase GEMM (gemm_8pp): full 256x256 tiles, K a multiple of 64 with >= 4 K-tiles,
-// alpha * acc (+ bias) epilogue. One workgroup per CU walks its tiles as ONE stream of K-tiles:
-//  * the next tile's first two K-tiles are DMAed inside this tile's last two K-tile iterations,
-//    like any other prefetch -- there is no per-tile prologue;
-//  * the MFMAs run with the operands swapped (B fragment first), so a lane holds C^T fragments =
-//    4 consecutive columns of one row; one v_permlane32_swap + one v_permlane16_swap per dword give
-//    every lane 8 consecutive columns and the epilogue stores straight from registers: no LDS
-//    staging, no barrier, the K pipeline's LDS buffers keep filling underneath it;
-//  * the stores of tile i drain while tile i+1 computes: the first phase-2 wait after an epilogue
-//    lets its NS stores stay outstanding (the vector-memory counter retires in issue order);
-//  * each tile's bias is DMAed into LDS with its first K-tile and read with ds_read (no wait on the
-//    vector-memory counter).
-// =====================================================================================
-template <int NW>
-__device__ __forceinline__ void vm_wait() {
-  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NW) : "memory");
-}
-
-template <int TA, int TB, typename TC>
-__global__ __launch_bounds__(512, 1) void gemm_8pp(const bf16* __restrict__ A, const bf16* __restrict__ B,
-                                                   TC* __restrict__ C, int M, int N, int K, long long lda,
-                                                   long long ldb, long long ldc, float alpha,
-                                                   const float* __restrict__ bias) {
-  using G = Gemm8Cfg<256>;
-  constexpr int BN = 256;
-  constexpr int NS = (sizeof(TC) == 2 ? 1 : 2) * G::FM * G::FN / 2;  // epilogue stores per lane
-  constexpr int WBASE = G::GA + 2 * G::GB;  // DMAs younger than K-tile u+1 at the phase-2 wait
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  bf16* lds = (bf16*)smem;
-  float* bias_lds = (float*)(smem + 2 * G::STAGE * 2);  // [tile parity][copy][256]
-  const int tm = M / 256, tn = N / BN, nblk = tm * tn, nt = K / 64;
-  const int ntile = (nblk - (int)blockIdx.x + (int)gridDim.x - 1) / (int)gridDim.x;
-  const int nstream = ntile * nt;
-  const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int wr = wid / G::WN, wc = wid % G::WN;
-  const int w8 = __builtin_amdgcn_readfirstlane(wid);
-  const bool has_bias = bias != nullptr;
-
-  // tile j of this workgroup -> (m0, n0): XCD-contiguous logical ids, grouped along M
-  auto tile_of = [&](int j, int& m0, int& n0) {
-    const int pid = xcd_remap((int)blockIdx.x + j * (int)gridDim.x, nblk);
-    constexpr int GROUP = 8;
-    const int group = pid / (GROUP * tn), first_m = group * GROUP;
-    const int gsz = min(tm - first_m, GROUP);
-    m0 = (first_m + (pid % (GROUP * tn)) % gsz) * 256;
-    n0 = ((pid % (GROUP * tn)) / gsz) * BN;
-  };
-
-  // per-lane byte offsets of tile (0, 0), K-tile 0; a tile / K-tile moves them by a uniform amount
-  ConvParams cp{};
-  ConvRows cr{};
-  unsigned offA[2][G::GA], offB[2][G::GB];
-#pragma unroll
-  for (int h = 0; h < 2; ++h) {
-#pragma unroll
-    for (int i = 0; i < G::GA; ++i)
-      offA[h][i] = (unsigned)((const char*)dma8_addr<TA, G::RWA, G::WA, G::GA>(A, lda, 0, M, 0, K, h, i, cp, cr) -
-                              (const char*)A);
-#pragma unroll
-    for (int i = 0; i < G::GB; ++i)
-      offB[h][i] = (unsigned)((const char*)dma8_addr<TB, G::RWB, G::WB, G::GB>(B, ldb, 0, N, 0, K, h, i, cp, cr) -
-                              (const char*)B);
-  }
-  const unsigned stepA = (unsigned)((TA == 1 ? 64 * lda : 64) * 2), stepB = (unsigned)((TB == 1 ? 64 * ldb : 64) * 2);
-  const unsigned rowA = (unsigned)(TA == 0 ? lda * 2 : 2), rowB = (unsigned)(TB == 0 ? ldb * 2 : 2);
-  const int nrA = __builtin_amdgcn_readfirstlane(
-      (int)(unsigned)min(2ull * (unsigned long long)(TA == 1 ? K : M) * (unsigned long long)lda, 0xffffffffull));
-  const int nrB = __builtin_amdgcn_readfirstlane(
-      (int)(unsigned)min(2ull * (unsigned long long)(TB == 1 ? K : N) * (unsigned long long)ldb, 0xffffffffull));
-  const auto rsA = __builtin_amdgcn_make_buffer_rsrc((void*)A, 0, nrA, 0x00020000);
-  const auto rsB = __builtin_amdgcn_make_buffer_rsrc((void*)B, 0, nrB, 0x00020000);
-  const auto rsBias = __builtin_amdgcn_make_buffer_rsrc((void*)(has_bias ? (const void*)bias : (const void*)A), 0,
-                                                        has_bias ? N * 4 : 0, 0x00020000);
-
-  f32x4 acc[G::FM][G::FN];
-#pragma unroll
-  for (int i = 0; i < G::FM; ++i)
-#pragma unroll
-    for (int j = 0; j < G::FN; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
-
-  auto img_a = [&](int buf, int h) { return lds + buf * G::STAGE + h * G::A_HALF; };
-  auto img_b = [&](int buf, int h) { return lds + buf * G::STAGE + 2 * G::A_HALF + h * G::B_HALF; };
-  // half-tile q (A-h0, B-h0, B-h1, A-h1) of a K-tile: so* = tile delta + k-tile step (bytes)
-  auto stage = [&](auto qc, int buf, unsigned soA, unsigned soB) {
-    constexpr int q = decltype(qc)::value;
-    if constexpr (q == 0 || q == 3) {
-      constexpr int h = q == 0 ? 0 : 1;
-      bf16* img = img_a(buf, h);
-#pragma unroll
-      for (int i = 0; i < G::GA; ++i)
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(rsA, (__attribute__((address_space(3))) void*)(img + (w8 * G::GA + i) * 512),
-                                                 16, (int)offA[h][i], (int)soA, 0, 0);
-    } else {
-      constexpr int h = q - 1;
-      bf16* img = img_b(buf, h);
-#pragma unroll
-      for (int i = 0; i < G::GB; ++i)
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(rsB, (__attribute__((address_space(3))) void*)(img + (w8 * G::GB + i) * 512),
-                                                 16, (int)offB[h][i], (int)soB, 0, 0);
-    }
-  };
-  // one 256-B DMA per wave (4 B per lane): waves 0-3 land the tile's 256 bias values, waves 4-7 a
-  // second copy -- every wave issues exactly one, so the counted waits stay uniform
-  auto stage_bias = [&](int par, int n0) {
-    float* dst = bias_lds + (par * 2 + (w8 >> 2)) * 256 + (w8 & 3) * 64;
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(rsBias, (__attribute__((address_space(3))) void*)dst, 4,
-                                             lane * 4 + (w8 & 3) * 256, n0 * 4, 0, 0);
-  };
-  using Q0 = std::integral_constant<int, 0>;
-  using Q1 = std::integral_constant<int, 1>;
-  using Q2 = std::integral_constant<int, 2>;
-  using Q3 = std::integral_constant<int, 3>;
-
-  int cj = 0, ct = 0, cm0, cn0;
-  tile_of(0, cm0, cn0);
-  // prologue: the bias and K-tiles 0, 1 of tile 0 (nt >= 4)
-  if (has_bias) stage_bias(0, cn0);
-  {
-    const unsigned a0 = cm0 * rowA, b0 = cn0 * rowB;
-    stage(Q1{}, 0, a0, b0);
-    stage(Q0{}, 0, a0, b0);
-    stage(Q2{}, 0, a0, b0);
-    stage(Q3{}, 0, a0, b0);
-    stage(Q1{}, 1, a0 + stepA, b0 + stepB);
-    stage(Q0{}, 1, a0 + stepA, b0 + stepB);
-    stage(Q2{}, 1, a0 + stepA, b0 + stepB);
-    stage(Q3{}, 1, a0 + stepA, b0 + stepB);
-    vm_wait<2 * G::GA + 2 * G::GB>();
-  }
-  // prefetch position: stream position u + 2 = (tile pj, K-tile pt)
-  int pj = 0, pt = 2, pm0 = cm0, pn0 = cn0;
-  asm volatile("" ::: "memory");
-  __builtin_amdgcn_s_barrier();
-  asm volatile("" ::: "memory");
-  bf16x8 fa[G::HA][2], fb0[G::HB][2], fb1[G::HB][2];
-#pragma unroll
-  for (int g = 0; g < G::HB; ++g)
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks) fb0[g][ks] = frag8<TB, G::WB>(img_b(0, 0), wc * (G::RWB / 2) + g * 16, ks);
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  asm volatile("" ::: "memory");
-  __builtin_amdgcn_s_barrier();
-  asm volatile("" ::: "memory");
-  // stagger: waves 4-7 run one barrier behind waves 0-3 (see gemm_8ph); the epilogue has no barrier,
-  // so the stagger carries across tiles
-  const int grp = __builtin_amdgcn_readfirstlane(wid >> 2);
-  if (grp == 1) __builtin_amdgcn_s_barrier();
-  asm volatile("" ::: "memory");
-
-#define G8P_QUAD(AH, BH, FB)                                                                              \
-  __builtin_amdgcn_s_setprio(1);                                                                          \
-  _Pragma("unroll") for (int f = 0; f < G::HA; ++f)                                                       \
-  _Pragma("unroll") for (int g = 0; g < G::HB; ++g)                                                       \
-  _Pragma("unroll") for (int ks = 0; ks < 2; ++ks)                                                        \
-    acc[AH * G::HA + f][BH * G::HB + g] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(                       \
-        FB[g][ks], fa[f][ks], acc[AH * G::HA + f][BH * G::HB + g], 0, 0, 0);                              \
-  __builtin_amdgcn_s_setprio(0)
-#define G8P_BEGIN()                                                                                       \
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");                                                      \
-  asm volatile("" ::: "memory");                                                                          \
-  __builtin_amdgcn_s_barrier();                                                                           \
-  __builtin_amdgcn_sched_barrier(0)
-#define G8P_END()                                                                                         \
-  __builtin_amdgcn_s_barrier();                                                                           \
-  asm volatile("" ::: "memory")
-
-  const int g4 = lane >> 4, lr = lane & 15;
-  for (int u = 0; u < nstream; ++u) {
-    const int buf = u & 1;
-    const bool pf = u + 2 < nstream;
-    const bool pbias = pf && pt == 0 && has_bias;
-    const bool after_epi = ct == 0 && u > 0;
-    const unsigned pa = pm0 * rowA + pt * stepA, pb = pn0 * rowB + pt * stepB;
-    // ---- phase 0: read A-h0 ; DMA [bias] B-h0(u+2) ; MFMA (A0, B0)
-#pragma unroll
-    for (int f = 0; f < G::HA; ++f)
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks) fa[f][ks] = frag8<TA, G::WA>(img_a(buf, 0), wr * (G::RWA / 2) + f * 16, ks);
-    if (pf) {
-      if (pbias) stage_bias(pj & 1, pn0);
-      stage(Q1{}, buf, pa, pb);
-    }
-    G8P_BEGIN();
-    G8P_QUAD(0, 0, fb0);
-    G8P_END();
-    // ---- phase 1: read B-h1 ; DMA A-h0(u+2) ; MFMA (A0, B1)
-#pragma unroll
-    for (int g = 0; g < G::HB; ++g)
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks) fb1[g][ks] = frag8<TB, G::WB>(img_b(buf, 1), wc * (G::RWB / 2) + g * 16, ks);
-    if (pf) stage(Q0{}, buf, pa, pb);
-    G8P_BEGIN();
-    G8P_QUAD(0, 1, fb1);
-    G8P_END();
-    // ---- phase 2: read A-h1 ; DMA B-h1(u+2) ; retire K-tile u+1 ; MFMA (A1, B0)
-#pragma unroll
-    for (int f = 0; f < G::HA; ++f)
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks) fa[f][ks] = frag8<TA, G::WA>(img_a(buf, 1), wr * (G::RWA / 2) + f * 16, ks);
-    if (pf) {
-      stage(Q2{}, buf, pa, pb);
-      // younger than K-tile u+1: [the epilogue's stores] [the bias DMA] B-h0, A-h0, B-h1 of u+2
-      if (after_epi) {
-        if (pbias) vm_wait<WBASE + 1 + NS>(); else vm_wait<WBASE + NS>();
-      } else {
-        if (pbias) vm_wait<WBASE + 1>(); else vm_wait<WBASE>();
-      }
-    } else {
-      vm_wait<0>();
-    }
-    G8P_BEGIN();
-    G8P_QUAD(1, 0, fb0);
-    G8P_END();
-    // ---- phase 3: read B-h0 of u+1 (retired in phase 2) ; DMA A-h1(u+2) ; MFMA (A1, B1)
-    if (u + 1 < nstream) {
-#pragma unroll
-      for (int g = 0; g < G::HB; ++g)
-#pragma unroll
-        for (int ks = 0; ks < 2; ++ks)
-          fb0[g][ks] = frag8<TB, G::WB>(img_b(buf ^ 1, 0), wc * (G::RWB / 2) + g * 16, ks);
-    }
-    if (pf) stage(Q3{}, buf, pa, pb);
-    G8P_BEGIN();
-    G8P_QUAD(1, 1, fb1);
-    G8P_END();
-    if (pf && ++pt == nt) {
-      pt = 0;
-      if (++pj < ntile) tile_of(pj, pm0, pn0);
-    }
-    if (++ct == nt) {
-      // ---- epilogue of tile cj from registers
-      float bvs[G::FN / 2][8];
-#pragma unroll
-      for (int jp = 0; jp < G::FN / 2; ++jp) {
-        if (has_bias) {
-          // inline asm: the compiler would first wait for every outstanding LDS DMA
-          const float* bp = bias_lds + (cj & 1) * 512 + wc * G::RWB + jp * 32 + g4 * 8;
-          f32x4 b0, b1;
-          asm volatile("ds_read_b128 %0, %2\n\tds_read_b128 %1, %2 offset:16\n\ts_waitcnt lgkmcnt(0)"
-                       : "=&v"(b0), "=&v"(b1)
-                       : "v"((unsigned)(size_t)LDS_PTR(char, bp))
-                       : "memory");
-          bvs[jp][0] = b0[0]; bvs[jp][1] = b0[1]; bvs[jp][2] = b0[2]; bvs[jp][3] = b0[3];
-          bvs[jp][4] = b1[0]; bvs[jp][5] = b1[1]; bvs[jp][6] = b1[2]; bvs[jp][7] = b1[3];
-        } else {
-#pragma unroll
-          for (int e = 0; e < 8; ++e) bvs[jp][e] = 0.f;
-        }
-      }
-#pragma unroll
-      for (int i = 0; i < G::FM; ++i) {
-        const long long row = cm0 + wr * G::RWA + i * 16 + lr;
-#pragma unroll
-        for (int jp = 0; jp < G::FN / 2; ++jp) {
-          float v[8];
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            // lane group g holds columns 4g + r of fragments 2jp / 2jp+1; after the two swaps it
-            // holds columns 8g + r and 8g + 4 + r of the pair's 32
-            const auto p = __builtin_amdgcn_permlane32_swap(__float_as_uint(acc[i][2 * jp][r]),
-                                                            __float_as_uint(acc[i][2 * jp + 1][r]), false, false);
-            const auto s = __builtin_amdgcn_permlane16_swap(p[0], p[1], false, false);
-            v[r] = __uint_as_float(s[0]);
-            v[4 + r] = __uint_as_float(s[1]);
-          }
-          TC* dst = C + row * ldc + cn0 + wc * G::RWB + jp * 32 + g4 * 8;
-          if constexpr (sizeof(TC) == 2) {
-            bf16x8 ov;
-#pragma unroll
-            for (int e = 0; e < 8; ++e) ov[e] = (bf16)(alpha * v[e] + bvs[jp][e]);
-            *(bf16x8*)dst = ov;
-          } else {
-            *(float4*)dst = make_float4(alpha * v[0] + bvs[jp][0], alpha * v[1] + bvs[jp][1],
-                                        alpha * v[2] + bvs[jp][2], alpha * v[3] + bvs[jp][3]);
-            *(float4*)(dst + 4) = make_float4(alpha * v[4] + bvs[jp][4], alpha * v[5] + bvs[jp][5],
-                                              alpha * v[6] + bvs[jp][6], alpha * v[7] + bvs[jp][7]);
-          }
-        }
-      }
-#pragma unroll
-      for (int i = 0; i < G::FM; ++i)
-#pragma unroll
-        for (int j = 0; j < G::FN; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
-      ct = 0;
-      if (++cj < ntile) tile_of(cj, cm0, cn0);
-    }
-  }
-#undef G8P_QUAD
-#undef G8P_BEGIN
-#undef G8P_END
-  if (grp == 0) __builtin_amdgcn_s_barrier();  // re-align the barrier counts before exit
 }
 
 template <typename TC>
@@ -1801,11 +1440,6 @@ static int launch_generic(int ta, int tb, const void* A, const void* B, void* C,
   return 0;
 }
 
-static int env_int(const char* name, int dflt) {
-  const char* e = getenv(name);
-  return e ? atoi(e) : dflt;
-}
-
 struct Plan8 {
   int bn, splits, kps;
   long long nblk;
@@ -1813,11 +1447,10 @@ struct Plan8 {
 
 // shape -> 8-phase configuration (bn = 0: not for this kernel)
 static Plan8 plan_8ph(int ta, int M, int N, int K, int batch, bool gn_prologue, bool have_ws, long long ws_floats) {
-  static const int mode = env_int("UVA_GEMM_8PH", 1);          // 0 off, 1 auto, 2 force BN=128, 3 force BN=256
-  static const int f128 = env_int("UVA_8PH_BN128_PCT", 90);    // relative per-CU efficiency of BN=128
-  static const int f384 = env_int("UVA_8PH_BN384_PCT", 85);    // ... of the 128x384 tile
+  constexpr int f128 = 90;  // relative per-CU efficiency of BN=128 (measured, % of the 256x256 tile)
+  constexpr int f384 = 85;  // ... of the 128x384 tile
   Plan8 p{0, 1, K, 0};
-  if (mode == 0 || M < 256 || N < 128 || (ta == 2 && gn_prologue)) return p;
+  if (M < 256 || N < 128 || (ta == 2 && gn_prologue)) return p;
   auto bm_of = [](int bn) { return bn == 384 ? 128 : 256; };
   auto tiles = [&](int bn) { return (long long)((M + bm_of(bn) - 1) / bm_of(bn)) * ((N + bn - 1) / bn); };
   // work per CU-round, relative: tile occupancy of the last round x useful fraction of each tile
@@ -1830,18 +1463,14 @@ static Plan8 plan_8ph(int ta, int M, int N, int K, int batch, bool gn_prologue, 
   };
   const bool splitk_regime = batch == 1 && have_ws && tiles(128) < 128 && K >= 8 * 64;
   // measured (tools_kbench.py): BN=256 beats the 128x128 LDS-DMA kernel on every UVA shape it is
-  // chosen for; BN=128 does not yet, so it is opt-in (UVA_GEMM_8PH=2) and auto mode falls back
-  int bn = 128;
+  // chosen for, the 128x384 tile beats the 128x128 fallback on every N = 768 shape; a BN=128 form
+  // of this kernel measured slower than the fallback kernel and is not built
+  int bn;
   // the 128x384 tile: plain products (no conv view), N a multiple of 384, off the split-K regime
-  const bool ok384 = ta != 2 && N % 384 == 0 && !splitk_regime && f384 > 0;
-  if (mode == 3) bn = 256;
-  else if (mode == 4) bn = ok384 ? 384 : 256;
-  else if (mode == 1) {
-    // (the 128x384 tile measured faster than the 128x128 fallback kernel on every N = 768 shape)
-    if (ok384 && score(384) > score(256)) bn = 384;
-    else if (N < 256 || !(splitk_regime || score(256) >= score(128))) return p;
-    else bn = 256;
-  }
+  const bool ok384 = ta != 2 && N % 384 == 0 && !splitk_regime;
+  if (ok384 && score(384) > score(256)) bn = 384;
+  else if (N < 256 || !(splitk_regime || score(256) >= score(128))) return p;
+  else bn = 256;
   const long long nblk = tiles(bn);
   int splits = 1;
   if (batch == 1 && have_ws && nblk < 128 && K >= 8 * 64) {
@@ -1864,12 +1493,6 @@ static Plan8 plan_8ph(int ta, int M, int N, int K, int batch, bool gn_prologue, 
 }
 
 // gemm_8pp routing: -1 = from UVA_8PP (default 0), 0 off, 1 on (uva_gemm_set_8pp)
-static int g_8pp_mode = -1;
-extern "C" int uva_gemm_set_8pp(int on) {
-  g_8pp_mode = on ? 1 : 0;
-  return 0;
-}
-
 // 8-phase 256-row kernel: returns 1 if launched, 0 if the shape is not for it, <0 on error
 template <typename TC>
 static int launch_8ph(int ta, int tb, const void* A, const void* B, void* C, int M, int N, int K, long long lda,
@@ -1893,85 +1516,14 @@ static int launch_8ph(int ta, int tb, const void* A, const void* B, void* C, int
                                                       bs, ep, cp, part, kps);                               \
   } while (0)
   // full tiles + K a multiple of 64 (every K-slice then is one too): the precomputed-source fast path
-  static const int fast_env = env_int("UVA_8PH_FAST", 1);
   auto span = [](int t, int rows, int cols, long long ld) {  // bytes an operand's offsets can reach
     return 2.0 * ((t == 1 ? (double)cols : (double)rows) * (double)ld);
   };
-  const bool fast = fast_env && ta != 2 && M % (bn == 384 ? 128 : 256) == 0 && N % bn == 0 && K % 64 == 0 && batch == 1 &&
+  const bool fast = ta != 2 && M % (bn == 384 ? 128 : 256) == 0 && N % bn == 0 && K % 64 == 0 && batch == 1 &&
                     span(ta, M, K, lda) < 4.0e9 && span(tb, N, K, ldb) < 4.0e9;
-  // persistent variant (gemm_8pp): fast-path shapes with an alpha (+ bias) epilogue, >= 4 K-tiles
-  if (g_8pp_mode < 0) g_8pp_mode = env_int("UVA_8PP", 0);
-  const int pp_env = g_8pp_mode;  // opt-in: measured equal to gemm_8ph (the stores of all CUs still burst together)
-  const bool plain_epi = !ep.residual && !ep.gate && !ep.aux && ep.act == 0 && ep.drop_thresh == 0 && ep.beta == 0.f;
-  if (pp_env && fast && bn == 256 && splits == 1 && K >= 256 && plain_epi && ldc % 8 == 0 &&
-      ((uintptr_t)C % 16) == 0 && ((uintptr_t)ep.bias % 16) == 0) {
-    static int ncu = 0;
-    if (!ncu) {
-      int dev = 0;
-      (void)hipGetDevice(&dev);
-      if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0) ncu = 256;
-    }
-    const int lb = 2 * Gemm8Cfg<256>::STAGE * 2 + 4 * 256 * 4;
-    const dim3 pgrid((unsigned)(nblk < ncu ? nblk : ncu));
-#define GPP(a, b)                                                                                           \
-  do {                                                                                                      \
-    static bool attr = false;                                                                               \
-    if (!attr) {                                                                                            \
-      (void)hipFuncSetAttribute((const void*)gemm_8pp<a, b, TC>, hipFuncAttributeMaxDynamicSharedMemorySize, lb); \
-      attr = true;                                                                                          \
-    }                                                                                                       \
-    gemm_8pp<a, b, TC><<<pgrid, 512, lb, s>>>((const bf16*)A, (const bf16*)B, (TC*)C, M, N, K, lda, ldb, ldc, \
-                                              ep.alpha, ep.bias);                                           \
-  } while (0)
-    if (ta == 0 && tb == 0) GPP(0, 0);
-    else if (ta == 0 && tb == 1) GPP(0, 1);
-    else if (ta == 1 && tb == 0) GPP(1, 0);
-    else GPP(1, 1);
-#undef GPP
-    UVA_LAUNCH_CHECK();
-    return 1;
-  }
 #define G8(a, b, BNV) do { if (fast) G8X(a, b, BNV, 256); else G8X(a, b, BNV, 0); } while (0)
-#define G8B(a, b) do { if (bn == 256) G8(a, b, 256); else G8(a, b, 128); } while (0)
+#define G8B(a, b) G8(a, b, 256)
 #define G8C(a, b) do { if (bn == 384) G8(a, b, 384); else G8B(a, b); } while (0)
-  static const int var = env_int("UVA_8PH_VAR", 0);
-#define G8V(V)                                                                                              \
-  do {                                                                                                      \
-    static bool attr = false;                                                                               \
-    const int lb = Gemm8Cfg<256>::LDS_BYTES;                                                                \
-    if (!attr) {                                                                                            \
-      (void)hipFuncSetAttribute((const void*)gemm_8ph<0, 0, 256, TC, V>, hipFuncAttributeMaxDynamicSharedMemorySize, lb); \
-      attr = true;                                                                                          \
-    }                                                                                                       \
-    gemm_8ph<0, 0, 256, TC, V><<<grid, 512, lb, s>>>((const bf16*)A, (const bf16*)B, (TC*)C, M, N, K, lda, ldb, \
-                                                     ldc, bs, ep, cp, part, kps);                           \
-  } while (0)
-  if (var && ta == 0 && tb == 0 && bn == 256 && sizeof(TC) == 2) {
-    switch (var) {
-      case 1: G8V(1); break;
-      case 2: G8V(2); break;
-      case 3: G8V(3); break;
-      case 4: G8V(4); break;
-      case 8: G8V(8); break;
-      case 9: G8V(9); break;
-      case 16: G8V(16); break;
-      case 12: G8V(12); break;
-      case 32: G8V(32); break;
-      case 96: G8V(96); break;
-      case 160: G8V(160); break;
-      case 256: G8V(256); break;
-      case 288: G8V(288); break;
-      case 416: G8V(416); break;
-      case 768: G8V(768); break;
-      case 800: G8V(800); break;
-      case 320: G8V(320); break;
-      case 1280: G8V(1280); break;
-      case 1344: G8V(1344); break;
-      case 2304: G8V(2304); break;
-      default: return -(int)hipErrorInvalidValue;
-    }
-  } else
-#undef G8V
   if (ta == 2 && tb == 0) G8B(2, 0);
   else if (ta == 0 && tb == 0) G8C(0, 0);
   else if (ta == 0 && tb == 1) G8C(0, 1);
@@ -2004,8 +1556,7 @@ static int launch_mfma(int ta, int tb, const void* A, const void* B, void* C, in
   int splits = 1;
   // K steps (x MB_K) per split, at least: 2 for the long-K training products; 4 for few-row GEMMs
   // (M <= 1024: the inference sampler's 1024x1024 layers, 41 -> 34 ms per 100-step loop at B=32)
-  static const int minks_env = env_int("UVA_SPLITK_MIN_KSTEPS", 0);
-  const int minks = minks_env > 0 ? minks_env : (M <= 1024 ? 4 : 2);
+  const int minks = M <= 1024 ? 4 : 2;
   if (batch == 1 && ws && nblk < 256 && K >= 2 * minks * MB_K) {
     splits = (512 + nblk - 1) / nblk;
     int kmax = K / (minks * MB_K);
@@ -2020,14 +1571,9 @@ static int launch_mfma(int ta, int tb, const void* A, const void* B, void* C, in
   }
   float* part = splits > 1 ? ws : nullptr;
   dim3 grid(nblk, splits, batch);
-  static int use_v1 = -1;
-  if (use_v1 < 0) {
-    const char* e = getenv("UVA_GEMM_V1");
-    use_v1 = (e && e[0] == '1') ? 1 : 0;
-  }
   // LDS-DMA needs 16-B aligned sources for every lane: K-contiguous lds/ld multiples of 8 (checked by
   // the dispatcher) -- and no register-side prologue (GN apply) on the A operand
-  const bool v2 = !use_v1 && !(ta == 2 && cp.gn_scale);
+  const bool v2 = !(ta == 2 && cp.gn_scale);
   if (v2) {
     size_t lds2 = EPI_LDS_BYTES;  // >= 4 x 8192 bf16 staging images
     static bool attr2 = false;
@@ -2122,79 +1668,6 @@ static int gemm_dispatch(int in_dtype, int out_dtype, int ta, int tb, const void
   return launch_generic<float, bf16>(ta, tb, A, B, C, M, N, K, lda, ldb, ldc, batch, bs, ep, cp, stream);
 }
 
-extern "C" int uva_lt_enabled();
-
-// Epilogue-free bf16 products: once per shape, time this file's kernel against the hipBLASLt
-// heuristic's first algorithms (blaslt.hip) on a scratch output and keep the fastest (the library
-// wins the dX products by 10-40 %, its first pick loses the long-K dW products by 1.5-3x).
-// Returns 0 when the library ran, -1 when this file's kernels are the choice, or an error code.
-static int plain_gemm_tuned(int out_dtype, int ta, int tb, const void* A, const void* B, void* C, int M, int N,
-                            int K, long long lda, long long ldb, long long ldc, float beta, const BatchStrides& bs,
-                            const EpiParams& ep, float* ws, long long ws_floats, hipStream_t stream) {
-  const LtShape sh{out_dtype, ta, tb, M, N, K, lda, ldb, ldc, beta != 0.f, ep.bias != nullptr};
-  using Key = std::tuple<int, int, int, int, int, int, long long, long long, long long, int, int, int, int>;
-  static std::map<Key, int> choice;
-  static std::mutex mu;
-  int dev = 0;
-  (void)hipGetDevice(&dev);
-  const Key key{out_dtype, ta, tb, M, N, K, lda, ldb, ldc, beta != 0.f, dev, uva_lt_enabled(), ep.bias != nullptr};
-  int pick;
-  {
-    std::lock_guard<std::mutex> lock(mu);
-    auto it = choice.find(key);
-    pick = it == choice.end() ? -2 : it->second;
-  }
-  if (pick == -2) {
-    const int n = lt_prepare(sh, 8);
-    pick = -1;
-    if (n > 0 && uva_lt_enabled() == 2) {
-      pick = 0;  // heuristic only
-    } else if (n > 0) {
-      const size_t esz = out_dtype == UVA_DT_BF16 ? 2 : 4;
-      const size_t bytes = (size_t)ldc * M * esz;
-      void* scratch = nullptr;
-      if (hipMalloc(&scratch, bytes) != hipSuccess) return (int)hipErrorOutOfMemory;
-      (void)hipMemsetAsync(scratch, 0, bytes, stream);
-      hipEvent_t e0, e1;
-      (void)hipEventCreate(&e0);
-      (void)hipEventCreate(&e1);
-      auto time_it = [&](auto&& run) -> float {
-        if (run() != 0) return 1e30f;  // warm (first use loads the code object)
-        (void)hipEventRecord(e0, stream);
-        for (int i = 0; i < 3; ++i) run();
-        (void)hipEventRecord(e1, stream);
-        (void)hipEventSynchronize(e1);
-        float ms = 0.f;
-        (void)hipEventElapsedTime(&ms, e0, e1);
-        return ms / 3.f;
-      };
-      ConvParams cp{};
-      float best = time_it([&]() {
-        return gemm_dispatch(UVA_DT_BF16, out_dtype, ta, tb, A, B, scratch, M, N, K, lda, ldb, ldc, 1, bs, ep, cp, 0,
-                             ws, ws_floats, stream);
-      });
-      const float own = best;
-      for (int i = 0; i < n; ++i) {
-        const float t = time_it([&]() { return lt_run(sh, i, A, B, scratch, scratch, 1.f, beta, ep.bias, stream); });
-        if (t < best) {
-          best = t;
-          pick = i;
-        }
-      }
-      (void)hipEventDestroy(e0);
-      (void)hipEventDestroy(e1);
-      (void)hipFree(scratch);
-      if (getenv("UVA_GEMM_TUNE_LOG"))
-        fprintf(stderr, "[uva gemm tune] ta%d tb%d M%d N%d K%d out%d beta%d: own %.1f us, pick %d (%.1f us)\n", ta,
-                tb, M, N, K, out_dtype, beta != 0.f, own * 1e3f, pick, best * 1e3f);
-    }
-    std::lock_guard<std::mutex> lock(mu);
-    choice[key] = pick;
-  }
-  if (pick < 0) return -1;
-  return lt_run(sh, pick, A, B, C, C, 1.f, beta, ep.bias, stream);
-}
-
 extern "C" int uva_gemm(int in_dtype, int out_dtype, int ta, int tb, const void* A, const void* B, void* C, int M,
                         int N, int K, long long lda, long long ldb, long long ldc, int batch, int batch_inner,
                         long long sAo, long long sAi, long long sBo, long long sBi, long long sCo, long long sCi,
@@ -2210,21 +1683,9 @@ extern "C" int uva_gemm(int in_dtype, int out_dtype, int ta, int tb, const void*
   ep.gate = gate;
   ep.ldg = ldg;
   ep.gate_dt = gate_dtype;
-  // epilogue-free (or bias-only) bf16 products -- the backward's dX / dW, the forward's qkv / fc1 /
-  // fc2: this file's kernel or hipBLASLt, whichever timed faster for the shape (plain_gemm_tuned)
-  if (in_dtype == UVA_DT_BF16 && batch == 1 && !force_generic && !residual && !aux && act == 0 &&
-      !(drop_p > 0.f) && !gate && alpha == 1.f && (beta == 0.f || (beta == 1.f && !bias)) && uva_lt_enabled()) {
-    const int r = plain_gemm_tuned(out_dtype, ta, tb, A, B, C, M, N, K, lda, ldb, ldc, beta, bs, ep, workspace,
-                                   ws_floats, stream);
-    if (r >= 0) return r;
-  }
   ConvParams cp{};
   return gemm_dispatch(in_dtype, out_dtype, ta, tb, A, B, C, M, N, K, lda, ldb, ldc, batch, bs, ep, cp, force_generic,
                        workspace, ws_floats, stream);
-}
-
-extern "C" int uva_debug_gemm8_stamps(unsigned long long* host) {
-  return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_uva_stamps), sizeof(g_uva_stamps));
 }
 
 extern "C" long long uva_gemm_plan(int in_dtype, int ta, int tb, int M, int N, int K, int batch, int gn_prologue,
@@ -2234,8 +1695,7 @@ extern "C" long long uva_gemm_plan(int in_dtype, int ta, int tb, int M, int N, i
   if (in_dtype != UVA_DT_BF16 || K % 8 != 0 || (tb == 1 && N % 8 != 0) || (ta == 1 && M % 8 != 0)) return 0;
   const Plan8 p = plan_8ph(ta, M, N, K, batch, gn_prologue != 0, ws_floats > 0, ws_floats);
   if (p.bn) return 3 | ((long long)p.bn << 4) | ((long long)p.splits << 16);
-  static const int use_v1 = env_int("UVA_GEMM_V1", 0);
-  return (use_v1 || (ta == 2 && gn_prologue)) ? 1 : 2;
+  return (ta == 2 && gn_prologue) ? 1 : 2;
 }
 
 extern "C" int uva_conv3x3_halo_bn(int Nimg, int H, int W, int Ci, int Co);
@@ -2253,13 +1713,12 @@ extern "C" int uva_conv2d(int dtype, const void* in, const void* w, void* out, c
   const int M = Nimg * Hout * Wout, K = ks * ks * Ci;
   if (M <= 0) return 0;
   // 3x3 / s1 / p1 with 16x16-tileable maps and 64 | Ci, 128 | Co: direct halo-tile kernel (conv.hip)
-  static const int halo_mode = env_int("UVA_CONV_HALO", 1);
-  if (halo_mode && !force_generic && dtype == UVA_DT_BF16 && ks == 3 && stride == 1 && pad_t == 1 && pad_l == 1 &&
+  if (!force_generic && dtype == UVA_DT_BF16 && ks == 3 && stride == 1 && pad_t == 1 && pad_l == 1 &&
       Hout == Hin && Wout == Win && act == ACT_NONE && uva_conv3x3_halo_bn(Nimg, Hin, Win, Ci, Co) > 0)
     return uva_conv3x3_halo(in, w, out, bias, residual, Nimg, Hin, Win, Ci, Co, gn_scale, gn_shift, gn_silu, gn_part,
                             stream);
   // the 8-channel (padded RGB) input conv: store-bound special form (conv.hip)
-  if (halo_mode && !force_generic && dtype == UVA_DT_BF16 && ks == 3 && stride == 1 && pad_t == 1 && pad_l == 1 &&
+  if (!force_generic && dtype == UVA_DT_BF16 && ks == 3 && stride == 1 && pad_t == 1 && pad_l == 1 &&
       Hout == Hin && Wout == Win && act == ACT_NONE && Ci == 8 && Co == 128 && !residual && !gn_scale &&
       Hin % 16 == 0 && Win % 16 == 0)
     return uva_conv_in8(in, w, out, bias, Nimg, Hin, Win, gn_part, stream);

@@ -18,7 +18,6 @@ MI355X layout of one sampling call over R = B*16 action rows and S spaced steps:
     (which also settles the per-shape GEMM route choices before capture).
 No autograd and no backward residues (the training trunk's aux tensors) are produced.
 """
-import os
 
 import torch
 
@@ -53,7 +52,7 @@ class ActionSampler:
         self.use_fused = use_fused  # few-row fused LN+linear kernels (bf16 compute, width <= 1024)
         # LN inside fc1's A staging: every 64-column block re-normalises its 32 rows (16x redundant
         # at width 1024), measured slower than the separate LN kernel (B=32: 27.8 vs 26.0 ms / loop)
-        self.fuse_ln = os.environ.get("UVA_SAMPLER_FUSE_LN", "0") == "1"
+        self.fuse_ln = False
 
     def __deepcopy__(self, memo):
         """copies (the reference's deepcopy'd EMA policy) start without the cached buffers / graph."""

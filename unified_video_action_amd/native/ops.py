@@ -63,11 +63,7 @@ def gemm(A, B, C, M, N, K, lda, ldb, ldc, ta=0, tb=0, batch=1, inner=1, sA=(0, 0
         assert bias.dtype == torch.float32 and bias.is_contiguous()
     if aux is not None:
         assert aux.dtype == C.dtype
-    plain = (dt(A) == 1 and batch == 1 and not force_generic and residual is None and aux is None
-             and act in ("none", 0) and not drop_p > 0 and gate is None and alpha == 1.0
-             and (beta == 0.0 or (beta == 1.0 and bias is None)))
-    route = " hipBLASLt" if plain and lib().query("uva_lt_enabled") else ""
-    with _traced(f"gemm[{'NT'[ta]}{'NT'[tb]}] {'bf16' if dt(A) else 'f32'} M{M} N{N} K{K} b{batch}{route}",
+    with _traced(f"gemm[{'NT'[ta]}{'NT'[tb]}] {'bf16' if dt(A) else 'f32'} M{M} N{N} K{K} b{batch}",
                  2.0 * M * N * K * batch):
         lib().call("uva_gemm", dt(A), dt(C), ta, tb, ptr(A), ptr(B), ptr(C), M, N, K, lda, ldb, ldc, batch, inner,
                    sA[0], sA[1], sB[0], sB[1], sC[0], sC[1], ptr(bias), ptr(residual), ldr, sR[0], sR[1], ptr(aux),
@@ -78,25 +74,6 @@ def gemm(A, B, C, M, N, K, lda, ldb, ldc, ta=0, tb=0, batch=1, inner=1, sA=(0, 0
 
 
 SPLITK_WS_FLOATS = 1 << 25  # 128 MB fp32 partial slabs
-
-
-class gemm_library:
-    """Route of epilogue-free bf16 GEMMs: gemm_library("kernels") -> the hand-written kernels only
-    (the default; UVA_GEMM_LIB=1 selects "tuned" process-wide), "tuned" -> per shape, whichever of
-    them and the hipBLASLt heuristic's algorithms timed fastest (an A/B reference: within 1 % of the
-    kernels-only step since the 128x384 tile), "library" -> hipBLASLt's first algorithm (tests)."""
-
-    MODES = {"kernels": 0, "tuned": 1, "library": 2}
-
-    def __init__(self, mode):
-        self.mode = self.MODES[mode]
-
-    def __enter__(self):
-        self.prev = lib().query("uva_lt_mode", self.mode)
-        return self
-
-    def __exit__(self, *exc):
-        lib().query("uva_lt_mode", 0 if self.prev < 0 else self.prev)
 
 
 def gemm_plan(M, N, K, ta=0, tb=0, batch=1, splitk=True, gn_prologue=False, dtype=torch.bfloat16):
