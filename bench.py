@@ -38,6 +38,8 @@ PEAK_HBM_GBS = 8000.0
 # algorithmic GFLOP per sample per step (SURVEY §8d / BASELINE.md §3)
 GFLOP_PER_SAMPLE = {"pusht_video": 2611.9, "pusht_joint": 2546.2, "libero10_joint": 2641.5, "umi_multi": 2674.2}
 METRIC = "train samples/sec (video+action step) at 1/2/4/8 MI355X; loss parity"
+# tokens per sample in the MAR (4 frames x 256 latent tokens, + 64 CLIP text tokens for Libero / UMI)
+SEQ_LEN = {"pusht_video": 1024, "pusht_joint": 1024, "libero10_joint": 1088, "umi_multi": 1088}
 WORKLOAD = {
     "pusht_video": "PushT video_model (BASELINE configs[1])",
     "pusht_joint": "PushT joint video+action, all 5 task modes (BASELINE configs[2] per-GPU batch)",
@@ -67,6 +69,8 @@ def parse(argv=None):
     ap.add_argument("--no-trace", action="store_true")
     ap.add_argument("--trace-steps", type=int, default=3)
     ap.add_argument("--cpu-threads", type=int, default=0)
+    ap.add_argument("--cpu-batch-gpu", action="store_true",
+                    help="also time the CPU baseline at the config's per-GPU batch (one step; minutes)")
     ap.add_argument("--trace-out", default="", help="write every traced kernel row (tag, launches, avg ms) here")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r02e.json"))
     return ap.parse_args(argv)
@@ -253,10 +257,48 @@ def cpu_baseline(args):
     one()  # warm-up
     ts = [one() for _ in range(args.cpu_steps)]
     med = statistics.median(ts)
-    return {"value": round(B / med, 5), "unit": "samples/s", "cores": th, "kind": "port",
-            "sample": f"oracle/uva_oracle.py full training step (resize->KL-VAE->mar_base fwd/bwd->AdamW), "
-                      f"PushT video_model, fp32, dropout 0.1, B={B}: 1 warm-up + median of {args.cpu_steps} steps "
-                      f"({', '.join(f'{t:.1f}' for t in ts)} s)"}
+    out = {"value": round(B / med, 5), "unit": "samples/s", "cores": th, "kind": "port",
+           "host_cpus": host_cpus(),
+           "sample": f"oracle/uva_oracle.py full training step (resize->KL-VAE->mar_base fwd/bwd->AdamW), "
+                     f"PushT video_model, fp32, dropout 0.1, B={B}: 1 warm-up + median of {args.cpu_steps} steps "
+                     f"({', '.join(f'{t:.1f}' for t in ts)} s)"}
+    if args.cpu_batch_gpu and args.batch != B:
+        B = args.batch
+        img = torch.rand(B, 32, 3, 96, 96)
+        act = torch.rand(B, 32, 2) * 512
+        t = one()
+        out["per_gpu_batch"] = {"batch": B, "value": round(B / t, 5), "unit": "samples/s",
+                                "sample": f"one step at B={B} after the B={args.cpu_batch} runs ({t:.1f} s)"}
+    return out
+
+
+def host_cpus():
+    """the host's CPU inventory as lscpu reports it: logical CPUs, physical cores (sockets x cores
+    per socket), and the CPUs this process may run on"""
+    info = {"logical": os.cpu_count()}
+    try:
+        info["usable"] = len(os.sched_getaffinity(0))
+    except AttributeError:
+        pass
+    try:
+        phys = set()
+        cur = {}
+        with open("/proc/cpuinfo") as f:
+            for ln in f:
+                if not ln.strip():
+                    if "physical id" in cur and "core id" in cur:
+                        phys.add((cur["physical id"], cur["core id"]))
+                    cur = {}
+                    continue
+                k, _, v = ln.partition(":")
+                cur[k.strip()] = v.strip()
+                if k.strip() == "model name":
+                    info["model"] = v.strip()
+        if phys:
+            info["physical_cores"] = len(phys)
+    except OSError:
+        pass
+    return info
 
 
 def line_for(config, batch, world, steps, elapsed, per_step, loss):
@@ -264,7 +306,8 @@ def line_for(config, batch, world, steps, elapsed, per_step, loss):
     value = batch * world * steps / elapsed
     ms = elapsed / steps * 1e3
     med = statistics.median(per_step)
-    return {"config": config, "workload": WORKLOAD[config], "global_batch": batch * world, "value": round(value, 3),
+    return {"config": config, "workload": WORKLOAD[config], "global_batch": batch * world,
+            "seq_len": SEQ_LEN[config], "value": round(value, 3),
             "ms_per_step": round(ms, 2), "ms_per_step_median": round(med, 2),
             "step_tflops_per_gpu": round(gflop * batch / (ms / 1e3) / 1e3, 1),
             "step_mfma_frac": round(gflop * batch / (ms / 1e3) / 1e3 / PEAK_BF16_TFLOPS, 4),
@@ -341,7 +384,8 @@ def run(args):
         "config": {"workload": f"{args.config}: {WORKLOAD[args.config]}; step = frame select+resize -> KL-VAE "
                                f"encode (8 frames) -> mar_base MAR fwd/bwd (N=1024) -> diffusion loss -> backward "
                                f"-> fused AdamW + EMA -> LR step; dropout 0.1",
-                   "model": "UVA mar_base + KL-VAE f16", "global_batch": args.batch * world, "seq_len": 1024,
+                   "model": "UVA mar_base + KL-VAE f16", "global_batch": args.batch * world,
+                   "seq_len": SEQ_LEN[args.config],
                    "parallelism": f"dp{world}"},
         "rccl_world": world,
         "step_tflops_per_gpu": main["step_tflops_per_gpu"], "step_mfma_frac": main["step_mfma_frac"],

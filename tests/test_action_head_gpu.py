@@ -1,0 +1,76 @@
+"""conv_fc action trunk kernels (diffusion_action_loss.py:42-61) vs plain PyTorch fp32:
+Conv2d(D, D, 3, p=1) + ReLU + AdaptiveAvgPool2d((4, 4)) + flatten (c w h) forward and backward
+through ConvReluPoolFn (HIP conv, pool-(c w h), fused pool/ReLU backward, im2col in Conv2d order,
+weight layouts), fp32 (1e-5 of scale) and bf16 (2e-2); and the generic GEMM's split-K path for
+tiny-output, long-K products (the Linear(4 -> 16) frame-interpolation dW)."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def rel_err(a, b):
+    a, b = a.double(), b.double()
+    return ((a - b).abs().max() / (b.abs().max() + 1e-12)).item()
+
+
+@pytest.mark.parametrize("prec,tol", [("fp32", 1e-5), ("bf16", 2e-2)])
+@pytest.mark.parametrize("n,D", [(8, 64), (12, 768)])
+def test_conv_relu_pool_fwd_bwd_vs_torch(prec, tol, n, D):
+    from unified_video_action_amd.model.autoregressive.diffusion_action_loss import ConvReluPoolFn
+    from unified_video_action_amd.runtime import RT, cdt
+    RT.set_precision(prec)
+    try:
+        torch.manual_seed(n + D)
+        x = torch.randn(n, 16, 16, D, device=DEV)  # NHWC, first spatial axis = the reference's w
+        w = (torch.randn(D, D, 3, 3, device=DEV) / (3 * D ** 0.5)).requires_grad_(True)
+        b = (torch.randn(D, device=DEV) * 0.1).requires_grad_(True)
+        xin = x.to(cdt()).requires_grad_(True)
+        w.grad = torch.zeros_like(w)
+        b.grad = torch.zeros_like(b)
+        out = ConvReluPoolFn.apply(xin, w, b)
+        g = torch.randn(n, D * 16, device=DEV).to(out.dtype)
+        out.backward(g)
+        # reference (NCHW)
+        xr = xin.detach().float().permute(0, 3, 1, 2).clone().requires_grad_(True)
+        wr = w.detach().clone().requires_grad_(True)
+        br = b.detach().clone().requires_grad_(True)
+        if prec == "bf16":  # the same bf16-rounded operands
+            wr = wr.detach().to(torch.bfloat16).float().requires_grad_(True)
+        y = F.adaptive_avg_pool2d(F.relu(F.conv2d(xr, wr, br, padding=1)), (4, 4)).reshape(n, D * 16)
+        y.backward(g.float())
+        assert rel_err(out.float(), y) < tol
+        assert rel_err(xin.grad.float().permute(0, 3, 1, 2), xr.grad) < tol * 2
+        assert rel_err(w.grad, wr.grad) < tol * 2
+        assert rel_err(b.grad, br.grad) < tol * 2
+    finally:
+        RT.set_precision("bf16")
+
+
+def test_im2col_columns_in_conv2d_weight_order():
+    from unified_video_action_amd.native import ops
+    n, H, W, Ci = 2, 5, 7, 3
+    x = torch.arange(n * H * W * Ci, dtype=torch.float32, device=DEV).reshape(n, H, W, Ci) + 1
+    cols = torch.empty(n * H * W, Ci * 9, device=DEV)
+    ops.im2col3x3(x, cols, n, H, W, Ci)
+    ref = F.unfold(x.permute(0, 3, 1, 2), 3, padding=1)  # [n, Ci*9 (ci, kh, kw), H*W]
+    assert torch.equal(cols.reshape(n, H * W, Ci * 9).transpose(1, 2), ref)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("M,N,K", [(16, 4, 49152), (64, 2, 20000), (4, 16, 8192)])
+def test_generic_gemm_splitk_tiny_output_long_k(dtype, M, N, K):
+    """dW of the frame interpolation: [M, N] (+)= dY^T X over K rows; beta = 1 accumulates."""
+    from unified_video_action_amd.native import ops
+    torch.manual_seed(K)
+    dy = torch.randn(K, M, device=DEV).to(dtype)
+    x = torch.randn(K, N, device=DEV).to(dtype)
+    dw = torch.randn(M, N, device=DEV)
+    ref = dw.double() + dy.double().t() @ x.double()
+    ops.linear_dw(dy, x, dw, beta=1.0)
+    assert rel_err(dw, ref) < (1e-5 if dtype == torch.float32 else 2e-3)
+    dw2 = torch.empty(M, N, device=DEV)
+    ops.linear_dw(dy, x, dw2, beta=0.0)
+    assert rel_err(dw2, dy.double().t() @ x.double()) < (1e-5 if dtype == torch.float32 else 2e-3)

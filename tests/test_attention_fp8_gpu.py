@@ -2,7 +2,7 @@
 
   * uva_attn_quant_fp8 rounds qkv in place exactly as torch's float8_e4m3fn cast of x * 2^-e
     (per (batch, head, q|k|v, 64-row tile) power-of-two scales, amax * 2^-e <= 448) and writes
-    the fp8 Q/K rows and the key-permuted V^T;
+    the fp8 Q/K rows and the key-permuted V^T (the block-scaled 32x32x64 MFMA operand order);
   * the fp8 forward vs an fp32 torch softmax attention of the SAME fp8-rounded inputs, at N = 1088
     (UMI/Libero tokens, 64-key tiles) and N = 1024 (128-key tiles), with and without dropout:
     log-sum-exp within 1e-4 (exact fp8 products, fp32 sums), O within 2^-4 of max|O| at worst (P
@@ -72,8 +72,9 @@ def test_quant_matches_torch_e4m3_and_layouts(N):
     torch.testing.assert_close(qk8[:, :, 0:1] * sq, want[:, :, 0:1].float(), rtol=0, atol=0)
     torch.testing.assert_close(qk8[:, :, 1:2] * sk, want[:, :, 1:2].float(), rtol=0, atol=0)
     v8t = ws[2 * B * N * H * 64: 3 * B * N * H * 64].view(torch.float8_e4m3fn).float().reshape(B, H, 64, N)
-    pos = torch.tensor([(r & ~31) + (8 * ((r & 31) >> 2) + ((r & 31) & 3) if (r & 31) < 16
-                                     else 8 * (((r & 31) - 16) >> 2) + 4 + (((r & 31) - 16) & 3)) for r in range(N)])
+    # key r of each 64-key tile sits at 32h + 16s + i, key = 32s + (i&3) + 8(i>>2) + 4h (the P.V operand order)
+    pos = torch.tensor([(r & ~63) + 32 * ((r >> 2) & 1) + 16 * ((r & 63) >> 5) + (r & 3) + 4 * ((r & 31) >> 3)
+                        for r in range(N)])
     sv = s[:, :, 2].repeat_interleave(64, dim=1)  # [B,N,H]
     vt = v8t[:, :, :, pos].permute(0, 3, 1, 2) * sv[..., None]  # [B,N,H,64]
     torch.testing.assert_close(vt, want[:, :, 2].float(), rtol=0, atol=0)

@@ -49,6 +49,19 @@ def main(attn_only=False):
         t2 = timeit(lambda: ops.attn_bwd(qkv, out, out, lse, dvec, dqkv, B, N, H, 0.125, p, 1, mask=mask))
         print(f"attn B={B} N={N} H={H} p={p}: mask {tm:.3f} ms, fwd {t1:.3f} ms {fl/t1/1e9:.0f} TF, bwd {t2:.3f} ms "
               f"{2*fl/t2/1e9:.0f} TF(alg 8N^2d)")
+    # fp8 forward (UMI config-5 shape: B=56, N=1088) against the bf16 forward of the same shape
+    for (B8, N8) in ((32, 1024), (56, 1088)):
+        x8 = torch.randn(B8, N8, 3 * H * 64, device=dev).to(torch.bfloat16)
+        o8 = torch.empty(B8, N8, H * 64, device=dev, dtype=torch.bfloat16)
+        l8 = torch.empty(B8, H, N8, device=dev)
+        ws8 = ops.attn_fp8_workspace(B8, N8, H, dev)
+        m8 = ops.attn_dropmask(B8, N8, H, 0.1, 1, dev)
+        fl8 = 4 * B8 * H * N8 * N8 * 64
+        tq = timeit(lambda: ops.attn_quant_fp8(x8, ws8, B8, N8, H))
+        tf = timeit(lambda: ops.attn_fwd_fp8(ws8, o8, l8, B8, N8, H, 0.125, 0.1, 1, mask=m8))
+        tb = timeit(lambda: ops.attn_fwd(x8, o8, l8, B8, N8, H, 0.125, 0.1, 1, mask=m8))
+        print(f"attn B={B8} N={N8} p=0.1: fp8 quant {tq:.3f} ms, fp8 fwd {tf:.3f} ms {fl8/tf/1e9:.0f} TF, "
+              f"bf16 fwd {tb:.3f} ms {fl8/tb/1e9:.0f} TF (fp8/bf16 {tf/tb:.2f}, incl. quant {(tf+tq)/tb:.2f})")
     q = qkv.view(B, N, 3, H, 64).permute(2, 0, 3, 1, 4)
     ts = timeit(lambda: torch.nn.functional.scaled_dot_product_attention(q[0], q[1], q[2]))
     print(f"torch sdpa fwd {ts:.3f} ms {fl/ts/1e9:.0f} TF")

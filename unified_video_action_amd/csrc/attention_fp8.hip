@@ -1,31 +1,38 @@
 // FP8 (OCP e4m3) attention forward for the "fp8_attn" precision (BASELINE config 5, UMI-multi):
-// the same timm Attention / SDPA (mar_con_unified.py:201-249) with Q.K^T and P.V as
-// v_mfma_f32_16x16x32_fp8_fp8 products, fp32 accumulation and fp32 online softmax.
+// the same timm Attention / SDPA (mar_con_unified.py:201-249) with Q.K^T and P.V on the
+// block-scaled v_mfma_scale_f32_32x32x64_f8f6f4 (e4m3 operands: twice the bf16 MFMA rate; the
+// non-scaled fp8 MFMAs run at the bf16 rate, MI355X_MICROARCH.md 'Matrix cores'), fp32
+// accumulation and fp32 online softmax.
 //
 // Scaling: per (batch, head, q|k|v, 64-row tile) power-of-two scales 2^e with amax * 2^-e <= 448
 // (uva_attn_quant_fp8, one pass over the qkv GEMM output).  The same pass rounds the bf16 qkv
 // IN PLACE to the fp8 grid (x~ = fp8(x * 2^-e) * 2^e, exact in bf16), so the backward -- the bf16
 // FA2 kernels of attention.hip run on x~ with this forward's log-sum-exp -- differentiates the
 // function the forward evaluated (straight-through estimator for the rounding), and writes
-//   qk8 [B, N, 2, H, 64]  fp8 Q / K (row-major, the MFMA A / B fragments are 8 contiguous bytes)
-//   v8t [B, H, 64, N]     fp8 V^T, keys permuted inside every 32-key group so the P.V A-fragment
-//                         (8 keys of one d row, in the order the S accumulators pack them) is 8
-//                         contiguous bytes: position 8g + j holds key j < 4 ? 4g + j : 16 + 4g + j - 4
+//   qk8 [B, N, 2, H, 64]  fp8 Q / K (row-major: a lane's 32-byte operand is half a row)
+//   v8t [B, H, 64, N]     fp8 V^T, keys permuted inside every 64-key tile so the P.V A operand
+//                         (32 keys of one d row, in the order the S accumulators pack them) is 32
+//                         contiguous bytes: position 32h + 16s + i holds key 32s + (i&3) + 8(i>>2) + 4h
 //   sc   [B, 3, H, N/64]  the fp32 scales 2^e.
-// Forward (same lane layout as attention.hip: S^T = K Q^T, so each lane owns one query and P^T is
-// already the B operand of O^T = V^T P^T): the Q.K scales fold into the softmax constant per
-// 64-key sub-tile (c' = c * sq * sk); P (<= 2^8 with the lazy max rescale) is converted to e4m3
-// unscaled after multiplying by 2^(ev - E), E = the largest V scale seen so far for the row
-// block (O is rescaled by the exact power of two when E grows), and O is multiplied by E at the end.
+// The scales are the MFMAs' own e8m0 block scales (uniform per 64-row tile = per operand block),
+// so S and O come out of the matrix core already scaled: no per-element multiplies, no running
+// V-scale bookkeeping.
+// Forward lane view (32x32 C/D map): S^T = K Q^T, a lane owns one query (lane & 31) and 16 keys
+// of each 32-key subtile; its 32 probabilities of a 64-key tile, packed to e4m3 in place, are the
+// B operand of O^T = V^T P^T.  Dropout reads the bf16 kernels' MQ bit plane (attention.hip): the
+// u64 word of (query, 64-key tile) holds key k at bit ((k>>2)&3)*16 + (k>>4)*4 + (k&3), which for
+// this lane view is a compile-time position + 16 (lane >> 5).
 // The row sums use the unrounded fp32 P, so the log-sum-exp matches an fp32 softmax of x~.
 #include "common.h"
 
 #define A8_MAX 448.0f
 
-typedef long fp8x8;  // 8 e4m3 values (one 16x16x32 MFMA operand fragment)
+typedef __attribute__((ext_vector_type(8))) int i32x8;  // 32 e4m3 values: one lane's 32x32x64 operand
 
-__device__ __forceinline__ f32x4 mfma8(fp8x8 a, fp8x8 b, const f32x4& c) {
-  return __builtin_amdgcn_mfma_f32_16x16x32_fp8_fp8(a, b, c, 0, 0, 0);
+// D = A B + C over K = 64 with e8m0 block scales sa / sb (2^(s - 127)) on A / B: lane l supplies
+// row (A) or column (B) l & 31, k block l >> 5, and its scale covers exactly those 32 elements
+__device__ __forceinline__ f32x16 mfma8s(const i32x8& a, const i32x8& b, const f32x16& c, int sa, int sb) {
+  return __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(a, b, c, 0, 0, 0, sa, 0, sb);
 }
 
 // 4 floats -> 4 e4m3 bytes (round to nearest even, saturating)
@@ -34,9 +41,9 @@ __device__ __forceinline__ int pack4_fp8(float a, float b, float c, float d) {
   return __builtin_amdgcn_cvt_pk_fp8_f32(c, d, p, true);
 }
 
-// position of key r (0..31) inside its permuted 32-key group (inverse of 8g + j -> key)
+// position of key r (0..63) inside its permuted 64-key tile (inverse of 32h + 16s + i -> key)
 __host__ __device__ constexpr int v8_pos(int r) {
-  return r < 16 ? 8 * (r >> 2) + (r & 3) : 8 * ((r - 16) >> 2) + 4 + ((r - 16) & 3);
+  return 32 * ((r >> 2) & 1) + 16 * (r >> 5) + ((r & 3) + 4 * ((r & 31) >> 3));
 }
 
 // =====================================================================================
@@ -93,7 +100,7 @@ __global__ __launch_bounds__(256) void attn_quant_fp8_kernel(bf16* __restrict__ 
     *(int4*)dst = (int4){w[0], w[1], w[2], w[3]};
   } else {
     // V^T: this thread holds V[q][col .. col + 15]; scatter the bytes to [d][permuted key] in LDS
-    const int pos = (row & ~31) + v8_pos(row & 31);
+    const int pos = v8_pos(row);
 #pragma unroll
     for (int k = 0; k < 4; ++k)
 #pragma unroll
@@ -137,24 +144,27 @@ __device__ __forceinline__ void a8_dma(const uint8_t* __restrict__ Kg, const uin
   }
 }
 
-// 8-byte fragment of row r, byte columns [32 s + 8 g, +8) of an image with RB-byte rows
-template <int RB>
-__device__ __forceinline__ fp8x8 a8_frag(const uint8_t* img, int r, int s, int g) {
-  const int c = (2 * s + (g >> 1)) ^ a8_swz<RB>(r);
-  return *(const fp8x8*)(img + r * RB + c * 16 + 8 * (g & 1));
+// 32-byte operand of row r, byte columns [32 h, +32) of a 64-byte-row image (chunks 2h, 2h + 1)
+__device__ __forceinline__ i32x8 a8_frag32(const uint8_t* img, int r, int h) {
+  const int f = a8_swz<64>(r);
+  const int4 lo = *(const int4*)(img + r * 64 + (((2 * h) ^ f) << 4));
+  const int4 hi = *(const int4*)(img + r * 64 + (((2 * h + 1) ^ f) << 4));
+  return (i32x8){lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
 }
 
+__device__ __forceinline__ int e8m0_of(float pow2) { return 127 + (int)__builtin_amdgcn_frexp_expf(pow2) - 1; }
+
 // =====================================================================================
-// forward: 4 waves x 32 queries per workgroup, KT keys per LDS tile (64 or 128)
+// forward: 4 waves x 32 queries per workgroup, 64-key tiles (one 32x32x64 MFMA per 32x32 score
+// tile, one per 32 d x 32 queries of P.V)
 // =====================================================================================
-template <bool DROP, int KT>
+template <bool DROP>
 __global__ __launch_bounds__(256, 2) void attn_fwd_fp8_kernel(const uint8_t* __restrict__ qk8,
                                                            const uint8_t* __restrict__ v8t,
                                                            const float* __restrict__ sc, bf16* __restrict__ out,
                                                            float* __restrict__ lse2, const uint64_t* __restrict__ MQ,
                                                            int N, int H, float c, float dsc) {
-  constexpr int NKT = KT / 16;   // 16-key MFMA tiles per LDS tile
-  constexpr int NH = KT / 64;    // 64-key sub-tiles (scale / mask-word granules) per LDS tile
+  constexpr int KT = 64;
   // one LDS array (a second __shared__ object beside LDS-DMA targets can cost vmcnt(0) waits)
   __shared__ __attribute__((aligned(1024))) uint8_t smem[2 * 2 * KT * 64];
   auto sK = [&](int b) { return smem + b * 2 * KT * 64; };
@@ -170,186 +180,118 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_fp8_kernel(const uint8_t* __r
   const float* sq_ = sc + ((long long)(b * 3 + 0) * H + h) * nt64;
   const float* sk_ = sc + ((long long)(b * 3 + 1) * H + h) * nt64;
   const float* sv_ = sc + ((long long)(b * 3 + 2) * H + h) * nt64;
-  const int tid = threadIdx.x, w = tid >> 6, l = tid & 63, g = l >> 4, li = l & 15;
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63, lq = l & 31, hh = l >> 5;
   const int q0 = bx * 128 + w * 32;
-  const int nkv = N / KT;
-  const uint16_t* mq = DROP ? (const uint16_t*)(MQ + (long long)bh * nt64 * N) : nullptr;
+  const int qrow = q0 + lq;
+  const uint64_t* mq = DROP ? MQ + (long long)bh * nt64 * N : nullptr;  // [kv][q] words
 
-  fp8x8 qf[2][2];
-  uint32_t mw[2][NH], mwn[2][NH];
-#pragma unroll
-  for (int qt = 0; qt < 2; ++qt) {
-    const int row = q0 + qt * 16 + li;
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks)
-      qf[qt][ks] = row < N ? *(const fp8x8*)(Qg + (long long)row * ldq + ks * 32 + 8 * g) : 0;
-#pragma unroll
-    for (int hh = 0; hh < NH; ++hh) {
-      mw[qt][hh] = (DROP && row < N) ? mq[((long long)hh * N + row) * 4 + g] : 0u;
-      mwn[qt][hh] = 0u;
-    }
+  // Q^T fragment (B operand of S^T = K Q^T): query qrow, d bytes [32 hh, +32)
+  i32x8 qf = {};
+  if (qrow < N) {
+    const int4 lo = *(const int4*)(Qg + (long long)qrow * ldq + 32 * hh);
+    const int4 hi = *(const int4*)(Qg + (long long)qrow * ldq + 32 * hh + 16);
+    qf = (i32x8){lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
   }
-  const float cq = c * (q0 < N ? sq_[q0 >> 6] : 1.f);  // the wave's 32 queries share one 64-row tile
-  float m[2] = {-INFINITY, -INFINITY}, rs[2] = {0.f, 0.f};
-  float E = 0.f;  // largest V scale folded into O so far (0 = none yet)
-  f32x4 o[2][4];
+  const int sq = e8m0_of(q0 < N ? sq_[q0 >> 6] : 1.f);  // the wave's 32 queries share one 64-row tile
+  float m = -INFINITY, rs = 0.f;
+  f32x16 o[2];
 #pragma unroll
-  for (int qt = 0; qt < 2; ++qt)
+  for (int dt = 0; dt < 2; ++dt)
 #pragma unroll
-    for (int dt = 0; dt < 4; ++dt) o[qt][dt] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    for (int i = 0; i < 16; ++i) o[dt][i] = 0.f;
 
+  uint64_t mw = (DROP && qrow < N) ? mq[qrow] : 0ull;
   a8_dma<KT>(Kg, Vg, ldq, N, 0, sK(0), sV(0));
   __syncthreads();
   int cur = 0;
-  for (int kv = 0; kv < nkv; ++kv) {
-    const bool more = kv + 1 < nkv;
+  for (int kv = 0; kv < nt64; ++kv) {
+    const bool more = kv + 1 < nt64;
+    uint64_t mwn = 0ull;
     if (more) {
       a8_dma<KT>(Kg, Vg, ldq, N, kv + 1, sK(cur ^ 1), sV(cur ^ 1));
-      if (DROP) {
-#pragma unroll
-        for (int qt = 0; qt < 2; ++qt) {
-          const int row = q0 + qt * 16 + li;
-#pragma unroll
-          for (int hh = 0; hh < NH; ++hh)
-            mwn[qt][hh] = row < N ? mq[((long long)((kv + 1) * NH + hh) * N + row) * 4 + g] : 0u;
-        }
-      }
+      if (DROP && qrow < N) mwn = mq[(long long)(kv + 1) * N + qrow];
     }
     const uint8_t* cK = sK(cur);
     const uint8_t* cV = sV(cur);
-    float ck[NH], sv[NH];
+    const int sk = e8m0_of(sk_[kv]), sv = e8m0_of(sv_[kv]);
+    // S^T (32 keys x 32 queries) of the tile's two subtiles, already scaled by 2^(eq + ek)
+    f32x16 s[2];
 #pragma unroll
-    for (int hh = 0; hh < NH; ++hh) {
-      ck[hh] = cq * sk_[kv * NH + hh];
-      sv[hh] = sv_[kv * NH + hh];
+    for (int st = 0; st < 2; ++st) {
+      const f32x16 z = {};
+      s[st] = mfma8s(a8_frag32(cK, st * 32 + lq, hh), qf, z, sk, sq);
     }
-    f32x4 s[NKT][2];
+    float mx = __builtin_amdgcn_fmed3f(s[0][0], s[0][1], INFINITY);
 #pragma unroll
-    for (int kt = 0; kt < NKT; ++kt)
+    for (int st = 0; st < 2; ++st)
 #pragma unroll
-      for (int qt = 0; qt < 2; ++qt) s[kt][qt] = (f32x4){0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
-#pragma unroll
-      for (int kt = 0; kt < NKT; ++kt) {
-        const fp8x8 kf = a8_frag<64>(cK, kt * 16 + li, ks, g);
-#pragma unroll
-        for (int qt = 0; qt < 2; ++qt) s[kt][qt] = mfma8(kf, qf[qt][ks], s[kt][qt]);
-      }
+      for (int i = (st == 0 ? 2 : 0); i < 16; ++i) mx = __builtin_amdgcn_fmed3f(mx, s[st][i], INFINITY);
+    {
+      auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(mx), __float_as_uint(mx), false, false);
+      mx = fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1])) * c;
     }
-    // row max of the scaled scores: the scales are positive, so max(s * ck) = max over sub-tiles of
-    // ck * max(s) -- no per-element multiply (it folds into the exp's fma below)
-    float mx[2];
-    bool need = false;
-#pragma unroll
-    for (int qt = 0; qt < 2; ++qt) {
-      float a = -INFINITY;
-#pragma unroll
-      for (int hh = 0; hh < NH; ++hh) {
-        float t = __builtin_amdgcn_fmed3f(s[hh * 4][qt][0], s[hh * 4][qt][1], INFINITY);
-#pragma unroll
-        for (int kt = hh * 4; kt < hh * 4 + 4; ++kt)
-#pragma unroll
-          for (int r = (kt == hh * 4 ? 2 : 0); r < 4; ++r) t = __builtin_amdgcn_fmed3f(t, s[kt][qt][r], INFINITY);
-        a = fmaxf(a, t * ck[hh]);
-      }
-      a = fmaxf(a, __shfl_xor(a, 16, 64));
-      a = fmaxf(a, __shfl_xor(a, 32, 64));
-      mx[qt] = a;
-      need |= mx[qt] > m[qt] + 8.0f;
-    }
+    const bool need = mx > m + 8.0f;  // lazy rescale (m = -inf at first)
     if (__builtin_amdgcn_ballot_w64(need)) {
+      const float mn = need ? mx : m;
+      const float a = __builtin_amdgcn_exp2f(m - mn);
+      rs *= a;
 #pragma unroll
-      for (int qt = 0; qt < 2; ++qt) {
-        const float mnew = fmaxf(m[qt], mx[qt]);
-        const float alpha = __builtin_amdgcn_exp2f(m[qt] - mnew);
-        rs[qt] *= alpha;
-#pragma unroll
-        for (int dt = 0; dt < 4; ++dt) o[qt][dt] *= alpha;
-        m[qt] = mnew;
-      }
+      for (int dt = 0; dt < 2; ++dt) o[dt] *= a;
+      m = mn;
     }
-    // V scale: fold the tile's 2^ev relative to the running largest E into P (exact powers of two)
-    float vmax = sv[0];
+    // this lane's keep bits: the MQ word of its query, shifted by 16 for the upper half of lanes
+    const uint32_t wlo = hh ? __builtin_amdgcn_alignbit((uint32_t)(mw >> 32), (uint32_t)mw, 16) : (uint32_t)mw;
+    const uint32_t whi = hh ? (uint32_t)(mw >> 48) : (uint32_t)(mw >> 32);
+    const float nm = -m;
+    float ps[4] = {0.f, 0.f, 0.f, 0.f};
+    int pk[8];
 #pragma unroll
-    for (int hh = 1; hh < NH; ++hh) vmax = fmaxf(vmax, sv[hh]);
-    if (vmax > E) {
-      if (E > 0.f) {
-        const float r = E / vmax;
+    for (int st = 0; st < 2; ++st)
 #pragma unroll
-        for (int qt = 0; qt < 2; ++qt)
+      for (int i = 0; i < 16; i += 2) {
+        float p2[2];
 #pragma unroll
-          for (int dt = 0; dt < 4; ++dt) o[qt][dt] *= r;
+        for (int u = 0; u < 2; ++u) {
+          const int ii = i + u;
+          const float p = __builtin_amdgcn_exp2f(fmaf(s[st][ii], c, nm));
+          ps[ii & 3] += p;
+          // key 32 st + (ii&3) + 8 (ii>>2) + 4 hh  ->  MQ bit 16 hh + BIT
+          const int bit = 32 * ((ii >> 2) & 1) + 4 * (2 * st + (ii >> 3)) + (ii & 3);
+          p2[u] = DROP ? __int_as_float(__float_as_int(p) &
+                                        __builtin_amdgcn_sbfe(bit < 32 ? wlo : whi, bit & 31, 1))
+                       : p;
+        }
+        // byte 16 st + i (, + 1) of the operand: two e4m3 in the half-word (i & 2) of dword (16 st + i) / 4
+        const int word = (16 * st + i) >> 2;
+        if ((i & 2) == 0) pk[word] = __builtin_amdgcn_cvt_pk_fp8_f32(p2[0], p2[1], 0, false);
+        else pk[word] = __builtin_amdgcn_cvt_pk_fp8_f32(p2[0], p2[1], pk[word], true);
       }
-      E = vmax;
-    }
-    // p' = exp2(s * ck - m + log2(sv / E)) in one fma + exp; the row sum is kept per sub-tile in
-    // those units and brought back by E / sv once per sub-tile
+    rs += (ps[0] + ps[1]) + (ps[2] + ps[3]);
+    const i32x8 pf = {pk[0], pk[1], pk[2], pk[3], pk[4], pk[5], pk[6], pk[7]};
 #pragma unroll
-    for (int qt = 0; qt < 2; ++qt) {
-#pragma unroll
-      for (int hh = 0; hh < NH; ++hh) {
-        const float lp = __builtin_amdgcn_logf(sv[hh] / E);  // log2 of a power of two <= 1: exact
-        const float nm = lp - m[qt];
-        float part = 0.f;
-#pragma unroll
-        for (int kt = hh * 4; kt < hh * 4 + 4; ++kt)
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const float p = __builtin_amdgcn_exp2f(fmaf(s[kt][qt][r], ck[hh], nm));
-            part += p;
-            s[kt][qt][r] = DROP ? __int_as_float(__float_as_int(p) & __builtin_amdgcn_sbfe(mw[qt][hh], (kt & 3) * 4 + r, 1))
-                                : p;
-          }
-        rs[qt] += part * (E / sv[hh]);
-      }
-    }
-#pragma unroll
-    for (int ks = 0; ks < KT / 32; ++ks) {
-      fp8x8 pf[2];
-#pragma unroll
-      for (int qt = 0; qt < 2; ++qt) {
-        const f32x4& a = s[2 * ks][qt];
-        const f32x4& e = s[2 * ks + 1][qt];
-        const unsigned lo = (unsigned)pack4_fp8(a[0], a[1], a[2], a[3]);
-        const unsigned hi = (unsigned)pack4_fp8(e[0], e[1], e[2], e[3]);
-        pf[qt] = (fp8x8)(((unsigned long long)hi << 32) | lo);
-      }
-#pragma unroll
-      for (int dt = 0; dt < 4; ++dt) {
-        const fp8x8 vf = a8_frag<KT>(cV, dt * 16 + li, ks, g);
-#pragma unroll
-        for (int qt = 0; qt < 2; ++qt) o[qt][dt] = mfma8(vf, pf[qt], o[qt][dt]);
-      }
-    }
-    if (more) {
-      if (DROP) {
-#pragma unroll
-        for (int qt = 0; qt < 2; ++qt)
-#pragma unroll
-          for (int hh = 0; hh < NH; ++hh) mw[qt][hh] = mwn[qt][hh];
-      }
-    }
+    for (int dt = 0; dt < 2; ++dt) o[dt] = mfma8s(a8_frag32(cV, dt * 32 + lq, hh), pf, o[dt], sv, 127);
+    mw = mwn;
     __syncthreads();
     cur ^= 1;
   }
-  const long long ldo = (long long)H * 64;
+  // lane: query qrow; o[dt][i] <-> d = 32 dt + (i&3) + 8(i>>2) + 4hh
+  float lsum;
+  {
+    auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(rs), __float_as_uint(rs), false, false);
+    lsum = __uint_as_float(r[0]) + __uint_as_float(r[1]);
+  }
+  if (qrow < N) {
+    const float inv = dsc / lsum;
+    bf16* orow = out + ((long long)b * N + qrow) * ((long long)H * 64) + h * 64;
 #pragma unroll
-  for (int qt = 0; qt < 2; ++qt) {
-    float lsum = rs[qt];
-    lsum += __shfl_xor(lsum, 16, 64);
-    lsum += __shfl_xor(lsum, 32, 64);
-    const int q = q0 + qt * 16 + li;
-    if (q >= N) continue;
-    const float inv = dsc * E / lsum;
-    bf16* orow = out + ((long long)b * N + q) * ldo + h * 64;
+    for (int dt = 0; dt < 2; ++dt)
 #pragma unroll
-    for (int dt = 0; dt < 4; ++dt) {
-      bf16x4 v = {(bf16)(o[qt][dt][0] * inv), (bf16)(o[qt][dt][1] * inv), (bf16)(o[qt][dt][2] * inv),
-                  (bf16)(o[qt][dt][3] * inv)};
-      *(bf16x4*)(orow + dt * 16 + 4 * g) = v;
-    }
-    if (g == 0) lse2[(long long)bh * N + q] = m[qt] + __log2f(lsum);
+      for (int j = 0; j < 4; ++j) {
+        const bf16x4 v = {(bf16)(o[dt][4 * j] * inv), (bf16)(o[dt][4 * j + 1] * inv), (bf16)(o[dt][4 * j + 2] * inv),
+                          (bf16)(o[dt][4 * j + 3] * inv)};
+        *(bf16x4*)(orow + 32 * dt + 8 * j + 4 * hh) = v;
+      }
+    if (hh == 0) lse2[(long long)bh * N + qrow] = m + __log2f(lsum);
   }
 }
 
@@ -387,13 +329,10 @@ extern "C" int uva_attn_fwd_fp8(const void* workspace, void* out, float* lse2, c
   dim3 grid((N + 127) / 128, B * H);
   const float c = scale * 1.4426950408889634f;
   const uint64_t* MQ = drop ? (const uint64_t*)mask : nullptr;
-  const bool k128 = N % 128 == 0;
-#define A8L(D, K) attn_fwd_fp8_kernel<D, K><<<grid, 256, 0, s>>>(qk8, v8t, sc, (bf16*)out, lse2, MQ, N, H, c, D ? ds : 1.0f)
-  if (drop && k128) A8L(true, 128);
-  else if (drop) A8L(true, 64);
-  else if (k128) A8L(false, 128);
-  else A8L(false, 64);
-#undef A8L
+  if (drop)
+    attn_fwd_fp8_kernel<true><<<grid, 256, 0, s>>>(qk8, v8t, sc, (bf16*)out, lse2, MQ, N, H, c, ds);
+  else
+    attn_fwd_fp8_kernel<false><<<grid, 256, 0, s>>>(qk8, v8t, sc, (bf16*)out, lse2, nullptr, N, H, c, 1.0f);
   UVA_LAUNCH_CHECK();
   return 0;
 }

@@ -95,22 +95,29 @@ __device__ __forceinline__ float conv_gather(const TI* __restrict__ in, const Co
   return v;
 }
 
-template <typename TI, typename TC, int TA, int TB>
+// SPLIT: blockIdx.z is a K-slice of k_per_split (batch 1); raw fp32 partial sums go to part[z][M][N]
+// and splitk_reduce applies the epilogue in slice order (deterministic).  For the tiny-output,
+// long-K products (the action head's Linear(4 -> 16) frame-interpolation dW, 16 x 4 over K = B x 768
+// tokens; the diffusion heads' input_proj dW over K = rows) one 64x64 block would otherwise walk K alone.
+template <typename TI, typename TC, int TA, int TB, bool SPLIT = false>
 __global__ __launch_bounds__(256) void gemm_generic(const TI* __restrict__ A, const TI* __restrict__ B,
                                                     TC* __restrict__ C, int M, int N, int K, long long lda,
                                                     long long ldb, long long ldc, BatchStrides bs, EpiParams ep,
-                                                    ConvParams cp) {
+                                                    ConvParams cp, float* __restrict__ part = nullptr,
+                                                    int k_per_split = 0) {
   __shared__ float As[16][64 + 4];
   __shared__ float Bs[16][64 + 4];
-  const int z = blockIdx.z, zo = z / bs.binner, zi = z % bs.binner;
+  const int z = SPLIT ? 0 : blockIdx.z, zo = z / bs.binner, zi = z % bs.binner;
   A += zo * bs.sAo + zi * bs.sAi;
   B += zo * bs.sBo + zi * bs.sBi;
   const long long coff = zo * bs.sCo + zi * bs.sCi;
   const long long roff = zo * ep.sRo + zi * ep.sRi;
   const int m0 = blockIdx.y * 64, n0 = blockIdx.x * 64;
   const int t = threadIdx.x, tx = t & 15, ty = t >> 4;
+  const int kb = SPLIT ? blockIdx.z * k_per_split : 0;
+  const int ke = SPLIT ? min(K, kb + k_per_split) : K;
   float acc[4][4] = {};
-  for (int k0 = 0; k0 < K; k0 += 16) {
+  for (int k0 = kb; k0 < ke; k0 += 16) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       int e = t + i * 256;  // 0..1023 over a 64x16 tile
@@ -118,7 +125,7 @@ __global__ __launch_bounds__(256) void gemm_generic(const TI* __restrict__ A, co
       if (TA != 1) { mm = e >> 4; kk = e & 15; } else { kk = e >> 6; mm = e & 63; }
       int gm = m0 + mm, gk = k0 + kk;
       float v = 0.f;
-      if (gm < M && gk < K) {
+      if (gm < M && gk < ke) {
         if (TA == 2) v = conv_gather(A, cp, gm, gk);
         else v = to_f32(TA == 0 ? A[(long long)gm * lda + gk] : A[(long long)gk * lda + gm]);
       }
@@ -128,7 +135,7 @@ __global__ __launch_bounds__(256) void gemm_generic(const TI* __restrict__ A, co
       int gn = n0 + nn;
       gk = k0 + kk;
       v = 0.f;
-      if (gn < N && gk < K) v = to_f32(TB == 0 ? B[(long long)gn * ldb + gk] : B[(long long)gk * ldb + gn]);
+      if (gn < N && gk < ke) v = to_f32(TB == 0 ? B[(long long)gn * ldb + gk] : B[(long long)gk * ldb + gn]);
       Bs[kk][nn] = v;
     }
     __syncthreads();
@@ -149,8 +156,10 @@ __global__ __launch_bounds__(256) void gemm_generic(const TI* __restrict__ A, co
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       int r = m0 + ty * 4 + i, c = n0 + tx * 4 + j;
-      if (r < M && c < N)
-        epi_store<TC>(C, ldc, coff, ep, roff, r, c, N, (long long)z * M * N + (long long)r * N + c, acc[i][j]);
+      if (r < M && c < N) {
+        if (SPLIT) part[((long long)blockIdx.z * M + r) * N + c] = acc[i][j];
+        else epi_store<TC>(C, ldc, coff, ep, roff, r, c, N, (long long)z * M * N + (long long)r * N + c, acc[i][j]);
+      }
     }
 }
 
@@ -1426,7 +1435,31 @@ static void launch_splitk_reduce(const float* part, int splits, void* C, int M, 
 template <typename TI, typename TC>
 static int launch_generic(int ta, int tb, const void* A, const void* B, void* C, int M, int N, int K, long long lda,
                           long long ldb, long long ldc, int batch, const BatchStrides& bs, const EpiParams& ep,
-                          const ConvParams& cp, hipStream_t s) {
+                          const ConvParams& cp, hipStream_t s, float* ws = nullptr, long long ws_floats = 0) {
+  const long long nblk = (long long)((N + 63) / 64) * ((M + 63) / 64);
+  if (batch == 1 && ws && ta != 2 && nblk < 64 && K >= 4096) {
+    // split K into slices of >= 256 so that ~512 blocks walk it; partial slabs in the workspace
+    int splits = (int)((512 + nblk - 1) / nblk);
+    if (splits > K / 256) splits = K / 256;
+    while (splits > 1 && (long long)splits * M * N > ws_floats) --splits;
+    if (splits > 1) {
+      const int kps = ((K + splits - 1) / splits + 15) / 16 * 16;
+      splits = (K + kps - 1) / kps;
+      dim3 sgrid((N + 63) / 64, (M + 63) / 64, splits);
+#define GS(a, b) gemm_generic<TI, TC, a, b, true><<<sgrid, 256, 0, s>>>((const TI*)A, (const TI*)B, (TC*)C, M, N, K, \
+                                                                        lda, ldb, ldc, bs, ep, cp, ws, kps)
+      if (ta == 0 && tb == 0) GS(0, 0);
+      else if (ta == 0 && tb == 1) GS(0, 1);
+      else if (ta == 1 && tb == 0) GS(1, 0);
+      else if (ta == 1 && tb == 1) GS(1, 1);
+      else return (int)hipErrorInvalidValue;
+#undef GS
+      UVA_LAUNCH_CHECK();
+      launch_splitk_reduce<TC>(ws, splits, C, M, N, ldc, ep, s);
+      UVA_LAUNCH_CHECK();
+      return 0;
+    }
+  }
   dim3 grid((N + 63) / 64, (M + 63) / 64, batch);
 #define GG(a, b) gemm_generic<TI, TC, a, b><<<grid, 256, 0, s>>>((const TI*)A, (const TI*)B, (TC*)C, M, N, K, lda, ldb, ldc, bs, ep, cp)
   if (ta == 2 && tb == 0) GG(2, 0);
@@ -1660,12 +1693,16 @@ static int gemm_dispatch(int in_dtype, int out_dtype, int ta, int tb, const void
       return launch_mfma<float>(ta, tb, A, B, C, M, N, K, lda, ldb, ldc, batch, bs, ep, cp, ws, ws_floats, stream);
     }
     if (out_dtype == UVA_DT_BF16)
-      return launch_generic<bf16, bf16>(ta, tb, A, B, C, M, N, K, lda, ldb, ldc, batch, bs, ep, cp, stream);
-    return launch_generic<bf16, float>(ta, tb, A, B, C, M, N, K, lda, ldb, ldc, batch, bs, ep, cp, stream);
+      return launch_generic<bf16, bf16>(ta, tb, A, B, C, M, N, K, lda, ldb, ldc, batch, bs, ep, cp, stream, ws,
+                                        ws_floats);
+    return launch_generic<bf16, float>(ta, tb, A, B, C, M, N, K, lda, ldb, ldc, batch, bs, ep, cp, stream, ws,
+                                       ws_floats);
   }
   if (out_dtype == UVA_DT_F32)
-    return launch_generic<float, float>(ta, tb, A, B, C, M, N, K, lda, ldb, ldc, batch, bs, ep, cp, stream);
-  return launch_generic<float, bf16>(ta, tb, A, B, C, M, N, K, lda, ldb, ldc, batch, bs, ep, cp, stream);
+    return launch_generic<float, float>(ta, tb, A, B, C, M, N, K, lda, ldb, ldc, batch, bs, ep, cp, stream, ws,
+                                        ws_floats);
+  return launch_generic<float, bf16>(ta, tb, A, B, C, M, N, K, lda, ldb, ldc, batch, bs, ep, cp, stream, ws,
+                                     ws_floats);
 }
 
 extern "C" int uva_gemm(int in_dtype, int out_dtype, int ta, int tb, const void* A, const void* B, void* C, int M,

@@ -2,13 +2,12 @@
 (reference: model/autoregressive/diffusion_action_loss.py, act_model_type="conv_fc").
 
 Trunk: z [B, 4*256, D] -> per-frame NHWC 16x16 -> conv3x3+ReLU (implicit-GEMM HIP conv,
-fused ReLU epilogue) -> AdaptiveAvgPool(4,4) -> fc(ReLU) -> fc -> Linear(4->16 frames)
+fused ReLU epilogue) -> AdaptiveAvgPool(4,4) + flatten (HIP) -> fc(ReLU) -> fc -> Linear(4->16 frames)
 -> refine MLP -> SimpleMLPAdaLN diffusion loss over B*16 rows (plain mean).
 sample(): the same trunk, then the spaced reverse-diffusion loop (sampler.ActionSampler).
 """
 import torch
 import torch.nn as nn
-import torch.nn.functional as F
 
 from ...native import ops
 from ...runtime import cdt
@@ -17,39 +16,48 @@ from .functional import F32, as_dtype, grad_buf, linear
 from .sampler import ActionSampler
 
 
-class Conv3x3ReluFn(torch.autograd.Function):
-    """NHWC conv3x3 (stride 1, pad 1) + bias + ReLU; weight in nn.Conv2d layout [Co, Ci, 3, 3]."""
+class ConvReluPoolFn(torch.autograd.Function):
+    """Conv2d(D, D, 3, p=1) + bias + ReLU + AdaptiveAvgPool2d((4, 4)) + flatten (c w h) of NHWC
+    [n, 16, 16, D] (diffusion_action_loss.py:42-47, 113-124); weight in nn.Conv2d layout [Co, Ci, 3, 3].
+    No ATen kernels: the weight changes layout in one HIP pass, the pool writes (c w h) directly,
+    the backward fuses the pool's broadcast with the ReLU mask, and dW = dpre^T im2col(x) with the
+    im2col columns in (ci, kh, kw) order accumulates straight into the Conv2d-layout gradient."""
 
     @staticmethod
     def forward(ctx, x, weight, bias):
         n, H, W, Ci = x.shape
         Co = weight.shape[0]
-        xc = as_dtype(x, cdt())
-        wk = as_dtype(weight.detach().permute(0, 2, 3, 1), cdt())
-        out = torch.empty(n, H, W, Co, dtype=cdt(), device=x.device)
-        ops.conv2d(xc, wk, out, n, H, W, Ci, Co, 3, 1, 1, 1, H, W, bias=bias.detach(), act="relu")
-        ctx.save_for_backward(xc, weight, bias, out)
+        cd = cdt()
+        xc = as_dtype(x, cd)
+        wk = torch.empty(Co, 3, 3, Ci, dtype=cd, device=x.device)
+        ops.conv3x3_weight_layout(weight.detach(), wk, 0)
+        post = torch.empty(n, H, W, Co, dtype=cd, device=x.device)
+        ops.conv2d(xc, wk, post, n, H, W, Ci, Co, 3, 1, 1, 1, H, W, bias=bias.detach(), act="relu")
+        pooled = torch.empty(n, Co * 16, dtype=cd, device=x.device)
+        ops.pool4x4_cwh(post, pooled, n, Co)
+        ctx.save_for_backward(xc, weight, bias, post)
         ctx.xdt = x.dtype
-        return out
+        return pooled
 
     @staticmethod
     def backward(ctx, g):
-        xc, weight, bias, out = ctx.saved_tensors
+        xc, weight, bias, post = ctx.saved_tensors
         n, H, W, Ci = xc.shape
         Co = weight.shape[0]
-        dpre = torch.empty(n * H * W, Co, dtype=cdt(), device=g.device)
-        ops.act_bwd(out.reshape(-1, Co), g.contiguous().reshape(-1, Co), dpre, "relu")
+        cd = cdt()
+        dpre = torch.empty(n, H, W, Co, dtype=cd, device=g.device)
+        ops.pool4x4_relu_bwd(post, g.contiguous(), dpre, n, Co)
         # dX = conv(dpre, W flipped & transposed)
-        wt = as_dtype(weight.detach().flip(2, 3).permute(1, 2, 3, 0), cdt())
-        dx = torch.empty(n, H, W, Ci, dtype=cdt(), device=g.device)
+        wt = torch.empty(Ci, 3, 3, Co, dtype=cd, device=g.device)
+        ops.conv3x3_weight_layout(weight.detach(), wt, 1)
+        dx = torch.empty(n, H, W, Ci, dtype=cd, device=g.device)
         ops.conv2d(dpre, wt, dx, n, H, W, Co, Ci, 3, 1, 1, 1, H, W)
-        # dW[co][(kh,kw,ci)] = dpre^T im2col(x)
-        cols = F.pad(xc, (0, 0, 1, 1, 1, 1)).unfold(1, 3, 1).unfold(2, 3, 1)  # n,H,W,Ci,3,3
-        cols = cols.permute(0, 1, 2, 4, 5, 3).reshape(n * H * W, 9 * Ci).contiguous()
-        dwk = torch.zeros(Co, 9 * Ci, dtype=F32, device=g.device)
-        ops.linear_dw(dpre, cols, dwk, beta=0.0)
-        grad_buf(weight).add_(dwk.reshape(Co, 3, 3, Ci).permute(0, 3, 1, 2))
-        ops.colsum(dpre, grad_buf(bias))
+        # dW[co][(ci, kh, kw)] += dpre^T im2col(x)
+        cols = torch.empty(n * H * W, Ci * 9, dtype=cd, device=g.device)
+        ops.im2col3x3(xc, cols, n, H, W, Ci)
+        ops.linear_dw(dpre.reshape(-1, Co), cols, grad_buf(weight).view(Co, Ci * 9), beta=1.0)
+        del cols
+        ops.colsum(dpre.reshape(-1, Co), grad_buf(bias))
         return as_dtype(dx, ctx.xdt), None, None
 
 
@@ -77,9 +85,7 @@ class DiffActLoss(nn.Module):
     def trunk(self, z):
         B, N, D = z.shape
         f = z.reshape(B * 4, 16, 16, D)  # (b t), w, h, c   with s = w*16 + h
-        f = Conv3x3ReluFn.apply(f, self.conv[0].weight, self.conv[0].bias)
-        f = f.reshape(B * 4, 4, 4, 4, 4, D).mean(dim=(2, 4))  # AdaptiveAvgPool2d((4,4)) 16 -> 4
-        f = f.permute(0, 3, 1, 2).reshape(B * 4, D * 16)  # (c w h)
+        f = ConvReluPoolFn.apply(f, self.conv[0].weight, self.conv[0].bias)  # [B*4, D*16] in (c w h) order
         f = linear(f, self.fc[0], act="relu", out_dtype=cdt())
         f = linear(f, self.fc[2], out_dtype=F32).reshape(B, 4, D)
         f = linear(f.transpose(1, 2), self.interpolate, out_dtype=F32).transpose(1, 2)  # B,16,D

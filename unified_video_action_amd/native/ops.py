@@ -388,6 +388,32 @@ def conv_fuses_gn(Nimg, H, W, Ci, Co, ks, stride, dtype=torch.bfloat16):
             lib().query("uva_conv3x3_halo_bn", Nimg, H, W, Ci, Co) > 0)
 
 
+def pool4x4_cwh(x, out, n, C):
+    """AdaptiveAvgPool2d((4,4)) of NHWC [n,16,16,C] flattened (c w h) -> out [n, 16 C]"""
+    assert x.is_contiguous() and out.is_contiguous() and x.dtype == out.dtype
+    assert x.numel() == n * 256 * C and out.numel() == n * 16 * C
+    lib().call("uva_pool4x4_cwh", dt(x), ptr(x), ptr(out), n, C, stream())
+
+
+def pool4x4_relu_bwd(post, gpool, dpre, n, C):
+    assert post.is_contiguous() and gpool.is_contiguous() and dpre.is_contiguous() and post.dtype == dpre.dtype
+    assert post.numel() == dpre.numel() == n * 256 * C and gpool.numel() == n * 16 * C
+    lib().call("uva_pool4x4_relu_bwd", dt(post), ptr(post), dt(gpool), ptr(gpool), ptr(dpre), n, C, stream())
+
+
+def im2col3x3(x, cols, n, H, W, Ci):
+    assert x.is_contiguous() and cols.is_contiguous() and x.dtype == cols.dtype
+    assert x.numel() == n * H * W * Ci and cols.numel() == n * H * W * Ci * 9
+    lib().call("uva_im2col3x3", dt(x), ptr(x), ptr(cols), n, H, W, Ci, stream())
+
+
+def conv3x3_weight_layout(w, out, mode):
+    """fp32 nn.Conv2d weight [Co,Ci,3,3] -> mode 0 [Co,3,3,Ci] / mode 1 flipped [Ci,3,3,Co]"""
+    Co, Ci = w.shape[0], w.shape[1]
+    assert w.dtype == torch.float32 and w.is_contiguous() and out.is_contiguous() and out.numel() == w.numel()
+    lib().call("uva_conv3x3_weight_layout", ptr(w), dt(out), ptr(out), Co, Ci, int(mode), stream())
+
+
 def groupnorm_finalize_tiles(part, Nimg, HW, C, gamma, beta, scale, shift, eps=1e-6, tile_rows=128):
     lib().call("uva_groupnorm_finalize_tiles", ptr(part), Nimg, HW, C, tile_rows, ptr(gamma), ptr(beta), float(eps),
                ptr(scale), ptr(shift), stream())
