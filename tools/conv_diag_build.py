@@ -1,0 +1,81 @@
+"""Diagnostic builds of the GN halo conv (timing only; results are WRONG by construction): each
+variant patches a copy of csrc/conv.hip, compiles it, and links ab/diag_<name>.so from the in-tree
+objects with conv.o replaced.  Run the timings with tools/conv_diag.sh on the GPU box."""
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CSRC = os.path.join(ROOT, "unified_video_action_amd", "csrc")
+OBJ = os.path.join(ROOT, "unified_video_action_amd", "build_obj")
+AB = os.path.join(ROOT, "ab")
+FLAGS = ["--offload-arch=gfx950", "-O3", "-fPIC", "-std=c++17", "-munsafe-fp-atomics", "-Wno-unused-result",
+         "-I" + CSRC]
+
+ANCHOR = "  const int pid = ch_xcd_remap(blockIdx.x, nblk);"
+VARIANTS = {
+    "base": [],
+    # GN apply without SiLU (no exp / rcp)
+    "nosilu": [("if (gn_silu) {", "if (false) {")],
+    # register-B weight loads always from step 0's offset (L1/L2-hot lines: the weight stream's latency)
+    "bhot": [("const int soff = __builtin_amdgcn_readfirstlane((tap * Ci + cc * 64) * 2);",
+              "const int soff = 0;")],
+    # no halo restaging at the chunk boundary (the chunk-1 MFMAs read stale LDS)
+    # no epilogue (MFMA results folded into one improbable-condition store)
+    "noepi": [("    ch_lds_barrier();  // the epilogue's LDS image overlays the halo buffers",
+               "    ch_lds_barrier();\n    { float sm = 0.f;\n      for (int f = 0; f < G::FM; ++f) for (int g = 0; g < G::FN; ++g) sm += acc[f][g][0] + acc[f][g][3];\n"
+               "      if (sm == 1.2345e-30f) out[tid] = (bf16)sm;\n      return; }")],
+    # register-epilogue form without its epilogue
+    "rnoepi": [("    // ---- register epilogue: + residual",
+                "    { float sm = 0.f;\n      for (int f = 0; f < G::FM; ++f) for (int g = 0; g < G::FN; ++g) sm += acc[f][g][0] + acc[f][g][3];\n"
+                "      if (sm == 1.2345e-30f) out[tid] = (bf16)sm;\n      return; }\n    // ---- register epilogue: + residual")],
+    # register epilogue without the GroupNorm partial sums
+    "rnogn": [("    if (gn_part) {\n      const int gsz = Co / 32;", "    if (false) {\n      const int gsz = Co / 32;"),
+              ("        if (gn_part) {\n          const uint2 u", "        if (false) {\n          const uint2 u")],
+    # register epilogue without the output stores (GN sums kept)
+    "rnost": [("        *(bf16x4*)(out + (pix0 + (long long)f * W) * Co + c0 + g * 16) = o;", "")],
+    # MFMA loop with the weight fragment outer
+    "gouter": [("""          for (int f = 0; f < G::FM; ++f)
+#pragma unroll
+            for (int g = 0; g < G::FN; ++g)
+              acc[f][g] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bq[cur][ks][g], fa[ks][f], acc[f][g], 0, 0, 0);""",
+                """          for (int g = 0; g < G::FN; ++g)
+#pragma unroll
+            for (int f = 0; f < G::FM; ++f)
+              acc[f][g] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bq[cur][ks][g], fa[ks][f], acc[f][g], 0, 0, 0);""")],
+    # accumulators not seeded with the bias
+    "zinit": [("    if (RB && bias) {", "    if (false) {")],
+    # operands in the pixel-major order (wrong layout for the epilogue; timing only)
+    "aorder": [("mfma_f32_16x16x32_bf16(bq[cur][ks][g], fa[ks][f], acc[f][g], 0, 0, 0)",
+                "mfma_f32_16x16x32_bf16(fa[ks][f], bq[cur][ks][g], acc[f][g], 0, 0, 0)")],
+    # the second co-resident workgroup of each CU (dispatch slots 256..511) starts ~half a tile late
+    "stag2": [(ANCHOR, "  if (blockIdx.x >= 256 && blockIdx.x < 512) for (int i = 0; i < 2; ++i) __builtin_amdgcn_s_sleep(127);\n" + ANCHOR)],
+    "stag4": [(ANCHOR, "  if (blockIdx.x >= 256 && blockIdx.x < 512) for (int i = 0; i < 4; ++i) __builtin_amdgcn_s_sleep(127);\n" + ANCHOR)],
+    "stag8": [(ANCHOR, "  if (blockIdx.x >= 256 && blockIdx.x < 512) for (int i = 0; i < 8; ++i) __builtin_amdgcn_s_sleep(127);\n" + ANCHOR)],
+    "nostage": [("        halo_store((cc + 1) & 1);\n        ch_lds_barrier();", "        ch_lds_barrier();")],
+}
+
+
+def build(name, subs):
+    src = open(os.path.join(CSRC, "conv.hip")).read()
+    for a, b in subs:
+        assert a in src, (name, a)
+        src = src.replace(a, b)
+    tmp = os.path.join(CSRC, f"_diag_{name}.hip")
+    open(tmp, "w").write(src)
+    try:
+        obj = os.path.join(AB, f"conv_{name}.o")
+        subprocess.run(["/opt/rocm/bin/hipcc"] + FLAGS + ["-c", tmp, "-o", obj], check=True)
+    finally:
+        os.remove(tmp)
+    objs = [os.path.join(OBJ, f) for f in sorted(os.listdir(OBJ)) if f.endswith(".o") and f != "conv.o"] + [obj]
+    subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-shared", "-fPIC", "-o",
+                    os.path.join(AB, f"diag_{name}.so")] + objs, check=True)
+    os.remove(obj)
+
+
+if __name__ == "__main__":
+    os.makedirs(AB, exist_ok=True)
+    for n in (sys.argv[1:] or VARIANTS):
+        build(n, VARIANTS[n])
+        print("built", n)

@@ -223,3 +223,26 @@ def aug_bench():
 
 if __name__ == "__main__" and len(sys.argv) > 1 and sys.argv[1] == "aug":
     aug_bench()
+
+
+def conv0_bench():
+    """The GN-fused VAE convs as the encoder runs them (GN+SiLU prologue, bias + residual + GN-stats
+    epilogue): level 0 (256x256, C128) and level 1 (128x128, C128), n = 256."""
+    dev = "cuda"
+    for (n, H, Ci, Co) in ((256, 256, 128, 128), (256, 128, 128, 128)):
+        x = torch.randn(n, H, H, Ci, device=dev).to(torch.bfloat16)
+        w = (torch.randn(Co, 3, 3, Ci, device=dev) * 0.05).to(torch.bfloat16)
+        out = torch.empty(n, H, H, Co, device=dev, dtype=torch.bfloat16)
+        sc = torch.rand(n, Ci, device=dev) + 0.5
+        sh = torch.randn(n, Ci, device=dev) * 0.3
+        res = torch.randn(n, H, H, Co, device=dev).to(torch.bfloat16)
+        bias = torch.randn(Co, device=dev)
+        part = torch.empty(n * H * H // 128, 32, 2, device=dev)
+        fl = 2 * n * H * H * Co * 9 * Ci
+        t = timeit(lambda: ops.conv2d(x, w, out, n, H, H, Ci, Co, 3, 1, 1, 1, H, H, bias=bias, residual=res,
+                                      gn_scale=sc, gn_shift=sh, gn_part=part), iters=10)
+        print(f"gnconv n{n} {H}x{H} C{Ci}: {t:.3f} ms {fl/t/1e9:.0f} TF")
+
+
+if __name__ == "__main__" and len(sys.argv) > 1 and sys.argv[1] == "conv0":
+    conv0_bench()

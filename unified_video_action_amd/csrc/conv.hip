@@ -67,7 +67,8 @@ struct ConvHCfg {
   static constexpr int MAIN_BYTES = (NHB * HALO_ELEMS + (RB ? 0 : NWB * BT)) * 2;  // RB: weights in VGPRs
   static constexpr int TP = BN + 4;             // epilogue fp32 pitch
   static constexpr int EPI_BYTES = 128 * TP * 4 + NW * (BN / 8) * 8 * 2 * 4;
-  static constexpr int LDS_BYTES = MAIN_BYTES > EPI_BYTES ? MAIN_BYTES : EPI_BYTES;
+  // RB finishes from registers: no epilogue image
+  static constexpr int LDS_BYTES = (RB || MAIN_BYTES > EPI_BYTES) ? MAIN_BYTES : EPI_BYTES;
 };
 
 // workgroup barrier ordering LDS only: the epilogue's global stores stay in flight across it
@@ -141,6 +142,7 @@ __global__ __launch_bounds__(TR * 32, 16 / TR) void conv3x3_halo(const bf16* __r
   // base + immediate offset (no per-step address VALU)
   constexpr bool RB = (VAR & 64) != 0 && GN && !R3 && !SPREAD;
   static_assert(!SPREAD || ConvHCfg<BN, TR>::ROUNDS <= 8, "one staging round per tap 1..8");
+  static_assert(!RB || TR == 8, "the register epilogue writes one 128-pixel GroupNorm unit per tile");
   using G = ConvHCfg<BN, TR, R3, HD, RB>;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   bf16* halo = (bf16*)smem;
@@ -257,13 +259,22 @@ __global__ __launch_bounds__(TR * 32, 16 / TR) void conv3x3_halo(const bf16* __r
                                                16, (int)hoff[i], cc * 128, 0, 0);
   };
 
+  const int frow = lane & 15, fk = lane >> 4;
+  // RB: the product is formed transposed (weights as the MFMA A operand, pixels as B), so lane
+  // (frow, fk) accumulates channels c0 + g*16 .. +3 (c0 = n0 + wn*32 + fk*4) of pixel (row f, column
+  // frow): one GroupNorm group (Co = 128) or a quarter / half of one in a lane, 8-B output runs, and
+  // the epilogue finishes from registers (no LDS image, no barrier); the bias seeds the accumulators
   f32x4 acc[G::FM][G::FN];
 #pragma unroll
-  for (int i = 0; i < G::FM; ++i)
+  for (int j = 0; j < G::FN; ++j) {
+    f32x4 b0 = (f32x4){0.f, 0.f, 0.f, 0.f};
+    if (RB && bias) {
+      const float4 b = *(const float4*)(bias + n0 + wn * (G::FN * 16) + j * 16 + fk * 4);
+      b0 = (f32x4){b.x, b.y, b.z, b.w};
+    }
 #pragma unroll
-    for (int j = 0; j < G::FN; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
-
-  const int frow = lane & 15, fk = lane >> 4;
+    for (int i = 0; i < G::FM; ++i) acc[i][j] = b0;
+  }
   // RB: B fragment (ks, g) of step s for this lane: 16 B at wt[(n0 + wn*32 + g*16 + frow) * K +
   // tap*Ci + cc*64 + ks*32 + fk*8]; per-lane part in vb[g] (+ ks*64 B immediate), step part in
   // soffset.  Step 0's fragments are issued ahead of the halo so their latency overlaps it.
@@ -323,6 +334,12 @@ __global__ __launch_bounds__(TR * 32, 16 / TR) void conv3x3_halo(const bf16* __r
     // A fragment (ks, f) of tap (kh, kw): halo pixel (wm*FM + f + kh, frow + kw), channels
     // (ks*4 + fk)*8.. -> lane base + ((f + kh) * 18 + kw) * PP + ks * 32
     const int abase = (wm * G::FM * CH_W + frow) * G::PP + fk * 8;
+    // residual of the lane's outputs (8 B each), loaded at tap 0 of the last chunk (no next halo there)
+    // (rows >= RQ_PRE at the epilogue's start: all 8 rows up front spilled)
+    constexpr int RQ_PRE = G::ROUNDS < G::FM ? G::ROUNDS : G::FM;
+    static_assert(G::FN == 2, "the permlane16 pairing joins the wave's two 16-channel fragments");
+    const long long pix0 = ((long long)n * H + oh0) * W + ow0 + frow;  // pixel (row 0, column frow)
+    const int c0 = n0 + wn * (G::FN * 16) + fk * 4;
     for (int cc = 0; cc < nch; ++cc) {
       const bf16* hcur = halo + (cc & 1) * G::HALO_ELEMS + abase;
       const bool more = cc + 1 < nch;
@@ -332,7 +349,12 @@ __global__ __launch_bounds__(TR * 32, 16 / TR) void conv3x3_halo(const bf16* __r
         const int cur = tap & 1, nxt = cur ^ 1;  // tap 8's next set is copied to set 0 below
         if (s + 1 < S) bload(s + 1, bq[nxt]);
         if (tap == 0 && more) halo_load(cc + 1);
-        if (tap == 0 && !more && residual) res_load();
+        if (tap == 0 && !more && residual) {
+          // rows 0..RQ_PRE-1 into the (now free) halo staging registers (the epilogue's 16-B runs)
+          const int csr = n0 + wn * (G::FN * 16) + (fk & 1) * 16 + (fk >> 1) * 8;
+#pragma unroll
+          for (int f = 0; f < RQ_PRE; ++f) hreg[f] = *(const bf16x8*)(residual + (pix0 + (long long)f * W) * Co + csr);
+        }
         const int kh = tap / 3, kw = tap % 3;
         bf16x8 fa[2][G::FM];
 #pragma unroll
@@ -347,7 +369,7 @@ __global__ __launch_bounds__(TR * 32, 16 / TR) void conv3x3_halo(const bf16* __r
           for (int f = 0; f < G::FM; ++f)
 #pragma unroll
             for (int g = 0; g < G::FN; ++g)
-              acc[f][g] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[ks][f], bq[cur][ks][g], acc[f][g], 0, 0, 0);
+              acc[f][g] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bq[cur][ks][g], fa[ks][f], acc[f][g], 0, 0, 0);
         __builtin_amdgcn_s_setprio(0);
       }
       // tap 8 loaded step s+1 into set 1; the next chunk's tap 0 reads set 0
@@ -362,7 +384,73 @@ __global__ __launch_bounds__(TR * 32, 16 / TR) void conv3x3_halo(const bf16* __r
         ch_lds_barrier();
       }
     }
-    ch_lds_barrier();  // the epilogue's LDS image overlays the halo buffers
+    // ---- register epilogue.  One v_permlane16_swap per accumulator word pairs lane rows fk, fk^1 so that
+    //      each lane holds 8 consecutive channels cs.. of its pixel (16-B runs; the 4 rows of a wave
+    //      cover the 64-B channel range of each pixel): 8-channel runs at rows 0/1/2/3 = +0/+16/+8/+24.
+    //      Then + residual (16 B), bf16 16-B stores, and the GroupNorm partial sums of the stored
+    //      values (lane: its 8 rows; then the 16 columns (lanes frow); then rows fk, fk^2 for gsz 16)
+    const int cs = n0 + wn * (G::FN * 16) + (fk & 1) * 16 + (fk >> 1) * 8;
+    bf16x8 rq[G::FM];
+    if (residual) {
+#pragma unroll
+      for (int f = 0; f < G::FM; ++f)
+        rq[f] = f < RQ_PRE ? hreg[f] : *(const bf16x8*)(residual + (pix0 + (long long)f * W) * Co + cs);
+    }
+    float sa = 0.f, sb = 0.f, qa = 0.f, qb = 0.f;
+#pragma unroll
+    for (int f = 0; f < G::FM; ++f) {
+      float v[8];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(acc[f][0][i]), __float_as_uint(acc[f][1][i]),
+                                                        false, false);
+        v[i] = __uint_as_float(r[0]);
+        v[4 + i] = __uint_as_float(r[1]);
+      }
+      if (residual) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] += (float)rq[f][e];
+      }
+      bf16x8 o;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) o[e] = (bf16)v[e];
+      *(bf16x8*)(out + (pix0 + (long long)f * W) * Co + cs) = o;
+      if (gn_part) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float q = (float)o[e], w2 = (float)o[4 + e];
+          sa += q;
+          qa += q * q;
+          sb += w2;
+          qb += w2 * w2;
+        }
+      }
+    }
+    if (gn_part) {
+      const int gsz = Co / 32;  // 4 (two groups per lane), 8 (one) or 16 (one, with row fk^2)
+      if (gsz >= 8) {
+        sa += sb;
+        qa += qb;
+      }
+#pragma unroll
+      for (int o = 1; o < 16; o <<= 1) {
+        sa += __shfl_xor(sa, o, 64);
+        qa += __shfl_xor(qa, o, 64);
+        sb += __shfl_xor(sb, o, 64);
+        qb += __shfl_xor(qb, o, 64);
+      }
+      if (gsz >= 16) {
+        sa = xor_lane_sum(sa, 32);
+        qa = xor_lane_sum(qa, 32);
+      }
+      if (frow == 0 && (gsz < 16 || fk < 2)) {
+        const long long t128 = (long long)n * (tiles_x * tiles_y) + (sp % (tiles_x * tiles_y));
+        float* gp = gn_part + (t128 * 32 + cs / gsz) * 2;
+        *(float2*)gp = make_float2(sa, qa);
+        if (gsz == 4) *(float2*)(gp + 2) = make_float2(sb, qb);
+      }
+    }
+    return;
   } else
   for (int cc = 0; cc < nch; ++cc) {
     const bf16* hcur = halo + (R3 ? 0 : (cc & 1)) * G::HALO_ELEMS;
