@@ -22,11 +22,15 @@
 //     is bank-conflict-free for every tap offset (ds_read_b128, 16-lane groups);
 //   * v_mfma_f32_16x16x32_bf16, fp32 accumulation; waves 2(M) x 4(N) of 128 px x 64 co (BN 256)
 //     or 4(M) x 2(N) of 64 x 64 (BN 128);
-//   * epilogue through LDS (128-pixel halves of the tile, fp32), bias + bf16 residual, 16-B
-//     stores, and the deterministic per-(128-pixel half, group) GroupNorm(32) partial sums of
-//     the stored output for the NEXT GroupNorm (uva_groupnorm_finalize_tiles, tile_rows 128).
+//   * epilogue: bias + bf16 residual, 16-B stores, and the deterministic per-(128-pixel half, group)
+//     GroupNorm(32) partial sums of the stored output for the NEXT GroupNorm
+//     (uva_groupnorm_finalize_tiles, tile_rows 128).  The GN (register-B) form finishes from
+//     registers: its product is formed transposed (lane = 4 channels of one pixel), one
+//     v_permlane16_swap per accumulator word turns that into 16-B channel runs, the bias seeds the
+//     accumulators; no LDS image, no barrier (level-0 6.48 -> 6.22 ms; 8-B runs straight from the
+//     transposed accumulators measured 6.80: the stores split into 16 x 32-B pieces per
+//     instruction).  The plain form stages the fp32 tile through LDS (128-pixel halves).
 #include "common.h"
-#include <stdlib.h>
 
 #define CH_T 16   // tile width (pixels)
 #define CH_W 18   // halo width
