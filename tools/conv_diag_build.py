@@ -48,6 +48,8 @@ VARIANTS = {
     # operands in the pixel-major order (wrong layout for the epilogue; timing only)
     "aorder": [("mfma_f32_16x16x32_bf16(bq[cur][ks][g], fa[ks][f], acc[f][g], 0, 0, 0)",
                 "mfma_f32_16x16x32_bf16(fa[ks][f], bq[cur][ks][g], acc[f][g], 0, 0, 0)")],
+    # attention dropout planes without the hash (timing of the step without the mask cost)
+    "maskfree": [("    const uint32_t hv = drop_hash(key, pair0 + j);", "    const uint32_t hv = (uint32_t)(pair0 + j) * 0x9E3779B1u;")],
     # the second co-resident workgroup of each CU (dispatch slots 256..511) starts ~half a tile late
     "stag2": [(ANCHOR, "  if (blockIdx.x >= 256 && blockIdx.x < 512) for (int i = 0; i < 2; ++i) __builtin_amdgcn_s_sleep(127);\n" + ANCHOR)],
     "stag4": [(ANCHOR, "  if (blockIdx.x >= 256 && blockIdx.x < 512) for (int i = 0; i < 4; ++i) __builtin_amdgcn_s_sleep(127);\n" + ANCHOR)],
@@ -56,19 +58,23 @@ VARIANTS = {
 }
 
 
+FILES = {"maskfree": "attention.hip"}
+
+
 def build(name, subs):
-    src = open(os.path.join(CSRC, "conv.hip")).read()
+    fn = FILES.get(name, "conv.hip")
+    src = open(os.path.join(CSRC, fn)).read()
     for a, b in subs:
         assert a in src, (name, a)
         src = src.replace(a, b)
     tmp = os.path.join(CSRC, f"_diag_{name}.hip")
     open(tmp, "w").write(src)
     try:
-        obj = os.path.join(AB, f"conv_{name}.o")
+        obj = os.path.join(AB, f"{fn[:-4]}_{name}.o")
         subprocess.run(["/opt/rocm/bin/hipcc"] + FLAGS + ["-c", tmp, "-o", obj], check=True)
     finally:
         os.remove(tmp)
-    objs = [os.path.join(OBJ, f) for f in sorted(os.listdir(OBJ)) if f.endswith(".o") and f != "conv.o"] + [obj]
+    objs = [os.path.join(OBJ, f) for f in sorted(os.listdir(OBJ)) if f.endswith(".o") and f != fn[:-4] + ".o"] + [obj]
     subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-shared", "-fPIC", "-o",
                     os.path.join(AB, f"diag_{name}.so")] + objs, check=True)
     os.remove(obj)

@@ -4,9 +4,13 @@ sampler) and of the action sampler alone, graph vs eager.  Run on the GPU box:
 Prints one JSON line per batch size."""
 import argparse
 import json
+import os
+import sys
 import time
 
 import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
 def main():

@@ -21,8 +21,13 @@ __device__ __forceinline__ float wave_sum(float v) {
   return v;
 }
 
-template <int LN, int ACT, int GATE, typename TC, int KS>
-__global__ __launch_bounds__(256) void sampler_linear_kernel(
+// NARROW = false: 4 waves x 16 columns, every wave over the full K (a 32 x 64 tile per workgroup).
+// NARROW = true (few rows: the 32 x 64 grid would leave most CUs idle, e.g. 16 workgroups for
+// R = 16, N = 1024): a 32 x 16 tile per workgroup, its 8 waves split K (each streams K/8 x 16 of
+// W), partial tiles summed through LDS in wave order (deterministic) -- 4x the workgroups, 1/8 of
+// each wave's weight stream.
+template <int LN, int ACT, int GATE, typename TC, int KS, bool NARROW>
+__global__ __launch_bounds__(NARROW ? 512 : 256) void sampler_linear_kernel(
     const void* __restrict__ A, long long lda, const float* __restrict__ lnw, const float* __restrict__ lnb,
     const bf16* __restrict__ shift, const bf16* __restrict__ scale, long long ldm, float eps,
     const bf16* __restrict__ W, const float* __restrict__ bias, const bf16* __restrict__ gate, long long ldg,
@@ -30,25 +35,30 @@ __global__ __launch_bounds__(256) void sampler_linear_kernel(
   // K = 32 * KS is a compile-time constant: every load / MFMA below sits in one straight-line
   // block, so the 32 weight loads issue back to back instead of one memory latency each
   constexpr int K = 32 * KS;
+  constexpr int NW = NARROW ? 8 : 4, NT = NW * 64;
+  constexpr int KSW = NARROW ? KS / NW : KS;  // k-steps of 32 per wave
+  static_assert(!NARROW || KS % NW == 0, "K slices of whole k-steps");
   __shared__ bf16 sA[SL_BM * SL_LDA];
+  __shared__ f32x4 sRed[NARROW ? NW * 2 * 64 : 1];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int m0 = blockIdx.x * SL_BM;
-  const int n0 = blockIdx.y * SL_BN + wave * 16;
-  // 1. this wave's weight fragments: column n0 + (lane & 15), k = 32 s + 8 (lane >> 4) .. +8
+  const int n0 = NARROW ? blockIdx.y * 16 : blockIdx.y * SL_BN + wave * 16;
+  const int kw0 = NARROW ? wave * KSW * 32 : 0;  // this wave's K slice
+  // 1. this wave's weight fragments: column n0 + (lane & 15), k = kw0 + 32 s + 8 (lane >> 4) .. +8
   //    (columns >= N read row 0: their accumulators are never stored)
-  bf16x8 bw[KS];
+  bf16x8 bw[KSW];
   {
     const int n = n0 + (lane & 15);
-    const bf16* wp = W + (long long)(n < N ? n : 0) * K + 8 * (lane >> 4);
+    const bf16* wp = W + (long long)(n < N ? n : 0) * K + kw0 + 8 * (lane >> 4);
 #pragma unroll
-    for (int s = 0; s < KS; ++s) bw[s] = *(const bf16x8*)(wp + 32 * s);
+    for (int s = 0; s < KSW; ++s) bw[s] = *(const bf16x8*)(wp + 32 * s);
   }
   // 2. A tile -> LDS (bf16), rows >= R zero
   if (LN) {
     // two rows per wave iteration (independent load/reduce chains overlap); a lane owns 4
     // consecutive columns per 256-column slice, so every operand load is a vector load
     const float* X = (const float*)A;
-    for (int r0 = 2 * wave; r0 < SL_BM; r0 += 8) {
+    for (int r0 = 2 * wave; r0 < SL_BM; r0 += 2 * NW) {
       float4 v[2][K / 256];
       float mean[2], rstd[2];
 #pragma unroll
@@ -109,7 +119,7 @@ __global__ __launch_bounds__(256) void sampler_linear_kernel(
   } else {
     const bf16* Ab = (const bf16*)A;
     const int kv = K / 8;
-    for (int i = tid; i < SL_BM * kv; i += 256) {
+    for (int i = tid; i < SL_BM * kv; i += NT) {
       const int r = i / kv, k = (i % kv) * 8;
       const int m = m0 + r;
       bf16x8 v = m < R ? *(const bf16x8*)(Ab + (long long)m * lda + k) : bf16x8{};
@@ -119,14 +129,28 @@ __global__ __launch_bounds__(256) void sampler_linear_kernel(
   __syncthreads();
   // 3. 2 (rows) x 1 (cols) 16x16 tiles per wave over the full K
   f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
-  const bf16* a0 = sA + (lane & 15) * SL_LDA + 8 * (lane >> 4);
+  const bf16* a0 = sA + (lane & 15) * SL_LDA + kw0 + 8 * (lane >> 4);
   const bf16* a1 = a0 + 16 * SL_LDA;
 #pragma unroll
-  for (int s = 0; s < KS; ++s) {
+  for (int s = 0; s < KSW; ++s) {
     const bf16x8 fa0 = *(const bf16x8*)(a0 + 32 * s);
     const bf16x8 fa1 = *(const bf16x8*)(a1 + 32 * s);
     acc0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa0, bw[s], acc0, 0, 0, 0);
     acc1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa1, bw[s], acc1, 0, 0, 0);
+  }
+  if constexpr (NARROW) {
+    // K-slice partials -> LDS; wave 0 sums them in wave order and runs the epilogue
+    sRed[(wave * 2 + 0) * 64 + lane] = acc0;
+    sRed[(wave * 2 + 1) * 64 + lane] = acc1;
+    __syncthreads();
+    if (wave != 0) return;
+    acc0 = sRed[lane];
+    acc1 = sRed[64 + lane];
+#pragma unroll
+    for (int w = 1; w < NW; ++w) {
+      acc0 += sRed[(w * 2 + 0) * 64 + lane];
+      acc1 += sRed[(w * 2 + 1) * 64 + lane];
+    }
   }
   // 4. epilogue: lane holds rows 4 (lane >> 4) + j (+16), column lane & 15
   const int n = n0 + (lane & 15);
@@ -159,11 +183,21 @@ extern "C" int uva_sampler_linear(int ln, const void* A, long long lda, const fl
   if ((gate == nullptr) != (res == nullptr) || (ln && (!shift || !scale)) || (act != 0 && act != ACT_SILU)) {
     return (int)hipErrorInvalidValue;
   }
-  dim3 grid((unsigned)((R + SL_BM - 1) / SL_BM), (unsigned)((N + SL_BN - 1) / SL_BN));
-#define SLKK(L, AC, G, T, KSV)                                                                             \
-  sampler_linear_kernel<L, AC, G, T, KSV><<<grid, 256, 0, s>>>(A, lda, lnw, lnb, (const bf16*)shift,         \
-                                                               (const bf16*)scale, ldm, eps, (const bf16*)W, bias, \
-                                                               (const bf16*)gate, ldg, res, ldr, (T*)out, ldo, R, N)
+  // the 32 x 64 tile grid, or (under 64 workgroups) the narrow 32 x 16 tiles with K split over 8 waves
+  const unsigned mb = (unsigned)((R + SL_BM - 1) / SL_BM);
+  const bool narrow = (long long)mb * ((N + SL_BN - 1) / SL_BN) < 64;
+  const dim3 grid(mb, (unsigned)(narrow ? (N + 15) / 16 : (N + SL_BN - 1) / SL_BN));
+#define SLKK(L, AC, G, T, KSV)                                                                                    \
+  do {                                                                                                            \
+    if (narrow)                                                                                                   \
+      sampler_linear_kernel<L, AC, G, T, KSV, true><<<grid, 512, 0, s>>>(                                         \
+          A, lda, lnw, lnb, (const bf16*)shift, (const bf16*)scale, ldm, eps, (const bf16*)W, bias,                \
+          (const bf16*)gate, ldg, res, ldr, (T*)out, ldo, R, N);                                                  \
+    else                                                                                                          \
+      sampler_linear_kernel<L, AC, G, T, KSV, false><<<grid, 256, 0, s>>>(                                        \
+          A, lda, lnw, lnb, (const bf16*)shift, (const bf16*)scale, ldm, eps, (const bf16*)W, bias,                \
+          (const bf16*)gate, ldg, res, ldr, (T*)out, ldo, R, N);                                                  \
+  } while (0)
 #define SLK(L, AC, G, T)                                                                                  \
   do {                                                                                                    \
     if (K == 1024) SLKK(L, AC, G, T, 32);                                                                 \

@@ -12,8 +12,9 @@ MI355X layout of one sampling call over R = B*16 action rows and S spaced steps:
     GEMM (the sampler's dominant FLOPs; per step it would be S launches at M=R);
   * the step loop is what is left: input_proj, d x (adaLN-LN, fc1 + SiLU, fc2 + gate +
     residual) and LN-modulate + final linear, the linears as few-row fused kernels
-    (uva_sampler_linear: 32x64 tiles over the full K, weights preloaded into registers,
-    optional LayerNorm in the A staging -- used for the final layer),
+    (uva_sampler_linear: 32x64 tiles over the full K, weights preloaded into registers, or for
+    few rows 32x16 tiles with K split over 8 waves; optional LayerNorm in the A staging -- used
+    for the final layer, and for fc1 at few rows),
     and the fused p_sample update kernel (uva_p_sample_step) -- replayed from a captured HIP graph after one eager step
     (which also settles the per-shape GEMM route choices before capture).
 No autograd and no backward residues (the training trunk's aux tensors) are produced.
@@ -50,9 +51,10 @@ class ActionSampler:
         self.sched = sampling_schedule(respacing)
         self.use_graph = use_graph
         self.use_fused = use_fused  # few-row fused LN+linear kernels (bf16 compute, width <= 1024)
-        # LN inside fc1's A staging: every 64-column block re-normalises its 32 rows (16x redundant
-        # at width 1024), measured slower than the separate LN kernel (B=32: 27.8 vs 26.0 ms / loop)
-        self.fuse_ln = False
+        # LN inside fc1's A staging re-normalises the rows once per column block: at B=32 (512 rows)
+        # measured slower than the separate LN kernel (27.8 vs 26.0 ms / loop); at few rows (B=1:
+        # 16 rows) the separate LN launch costs more than the redundant re-normalisation
+        self.fuse_ln_rows = 64
 
     def __deepcopy__(self, memo):
         """copies (the reference's deepcopy'd EMA policy) start without the cached buffers / graph."""
@@ -118,7 +120,7 @@ class ActionSampler:
         if st["fused"]:
             for i, (modw, modb, w1, b1, w2, b2, lnw, lnb) in enumerate(blocks):
                 m = mod[:, 3 * W * i:3 * W * (i + 1)]
-                if self.fuse_ln:
+                if R <= self.fuse_ln_rows:
                     ops.sampler_linear(x, compute_weight(w1), st["a"], bias=b1.detach(), act="silu", ln=True,
                                        lnw=lnw.detach(), lnb=lnb.detach(), shift=m[:, :W], scale=m[:, W:2 * W])
                 else:
