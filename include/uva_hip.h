@@ -187,6 +187,24 @@ int uva_sampler_linear(int ln, const void* A, long long lda, const float* lnw, c
                        const void* gate, long long ldg, const float* res, long long ldr, int odt, void* out,
                        long long ldo, int R, int N, int K, hipStream_t stream);
 
+/* ---- persistent action sampler (inference, bf16, R <= 16 rows: B = 1): the whole S-step
+ *      p_sample_loop of SimpleMLPAdaLN in one launch (replaces, per step: input_proj, depth x
+ *      (uva_sampler_linear LN+SiLU, uva_sampler_linear gate+residual), the final LN linear and
+ *      uva_p_sample_step -- diffusion_loss.py:142-189,261-283; gaussian_diffusion.py:395-440).
+ * Weights stacked per kind: w1/w2 bf16 [depth, W, W], b1/b2/lnw/lnb fp32 [depth, W]; win bf16 [W, C],
+ * bin [W]; wf bf16 [2C, W], bfin [2C].  mod: bf16 [S, R, ldmod] adaLN table (block i shift | scale |
+ * gate at 3Wi, final shift | scale at 3W depth); coef fp32 [S, 8] (uva_p_sample_step's order);
+ * noise fp32 [S, R, C]; x0 fp32 [R, C] (x_T) -> x_out [R, C].  work: uva_sampler_persistent_workspace
+ * bytes, 256-B aligned (the call zeroes its counters with a memset node).  W == 1024, depth == 6,
+ * C <= 16.  uva_sampler_persistent_status: the spin give-up flag of the last run (0 = clean; syncs). */
+long long uva_sampler_persistent_workspace(int W);
+int uva_sampler_persistent(int R, int C, int W, int depth, int S, int clip, float eps, const void* w1, const float* b1,
+                           const void* w2, const float* b2, const float* lnw, const float* lnb, const void* win,
+                           const float* bin, const void* wf, const float* bfin, const void* mod, long long ldmod,
+                           const float* coef, const float* noise, const float* x0, float* x_out, void* work,
+                           long long work_bytes, hipStream_t stream);
+int uva_sampler_persistent_status(const void* work, unsigned* flag, hipStream_t stream);
+
 /* ---- optimizer + EMA (policy:343-360 torch AdamW; ema_model.py:57-89) ----------------- */
 /* One launch per parameter group region (16-B aligned p/g/m/v/ema): n_decay = n applies the
  * group's weight decay wd, n_decay = 0 none.  ema (nullable) gets the fused EMA update with

@@ -54,11 +54,70 @@ VARIANTS = {
     "stag2": [(ANCHOR, "  if (blockIdx.x >= 256 && blockIdx.x < 512) for (int i = 0; i < 2; ++i) __builtin_amdgcn_s_sleep(127);\n" + ANCHOR)],
     "stag4": [(ANCHOR, "  if (blockIdx.x >= 256 && blockIdx.x < 512) for (int i = 0; i < 4; ++i) __builtin_amdgcn_s_sleep(127);\n" + ANCHOR)],
     "stag8": [(ANCHOR, "  if (blockIdx.x >= 256 && blockIdx.x < 512) for (int i = 0; i < 8; ++i) __builtin_amdgcn_s_sleep(127);\n" + ANCHOR)],
+    # A fragments read from LDS at tap 0 of each chunk only (later taps reuse them): the A-read cost
+    "noA": [("""        bf16x8 fa[2][G::FM];
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+          for (int f = 0; f < G::FM; ++f)
+            fa[ks][f] =""", """        if (tap == 0)
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+          for (int f = 0; f < G::FM; ++f)
+            fa[ks][f] ="""),
+            ("""    for (int cc = 0; cc < nch; ++cc) {
+      const bf16* hcur = halo + (cc & 1) * G::HALO_ELEMS + abase;""", """    bf16x8 fa[2][G::FM];
+    for (int cc = 0; cc < nch; ++cc) {
+      const bf16* hcur = halo + (cc & 1) * G::HALO_ELEMS + abase;""")],
+    # the same, A fragments re-read at taps 0 and 4 (half the LDS A traffic)
+    "halfA": [("""        bf16x8 fa[2][G::FM];
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+          for (int f = 0; f < G::FM; ++f)
+            fa[ks][f] =""", """        if ((tap & 1) == 0)
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+          for (int f = 0; f < G::FM; ++f)
+            fa[ks][f] ="""),
+            ("""    for (int cc = 0; cc < nch; ++cc) {
+      const bf16* hcur = halo + (cc & 1) * G::HALO_ELEMS + abase;""", """    bf16x8 fa[2][G::FM];
+    for (int cc = 0; cc < nch; ++cc) {
+      const bf16* hcur = halo + (cc & 1) * G::HALO_ELEMS + abase;""")],
+    # persistent sampler: hand-off waits skipped (results wrong; the latency of the waits)
+    "ps_nowait": [("      if (__hip_atomic_load((gu32*)cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= target) break;",
+                   "      break;")],
+    # persistent sampler: exchanged rows not re-loaded (stale registers / LDS; latency of the sc1 loads)
+    "ps_noload": [("        if (r < R)\n          v = __builtin_bit_cast", "        if (r < 0)\n          v = __builtin_bit_cast"),
+                  ("        const u32x4v v = __builtin_amdgcn_raw_buffer_load_b128(rs_ha, (row * W + c8) * 2, 0, PS_SC1);\n        *(u32x4v*)(sA + row * PS_LDA + c8) = v;",
+                   "        (void)row; (void)c8;")],
+    # persistent sampler: no publish (counter adds skipped) AND no waits
+    "ps_nosync": [("      if (__hip_atomic_load((gu32*)cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= target) break;",
+                   "      break;"),
+                  ("  asm volatile(\"s_waitcnt vmcnt(0)\" ::: \"memory\");  // the storing wave's sc1 stores have left\n  if ((threadIdx.x & 63) == 0)",
+                   "  if (false)")],
+    # persistent sampler: s_memtime stamps of workgroup 0 / thread 0 at every phase point of step 50,
+    # written at work + 1024 (tools/ps_stamps.py reads them); the workspace header grows to 8 KB
+    "ps_stamps": [("  return 256 + 2LL * PS_R * W * 4 + (long long)PS_R * W * 2;", "  return 8192 + 2LL * PS_R * W * 4 + (long long)PS_R * W * 2;"),
+                  ("  p.hx = (float*)((char*)work + 256);", "  p.hx = (float*)((char*)work + 8192);"),
+                  ("  p.ha = (bf16*)((char*)work + 256 + 2LL * PS_R * W * 4);", "  p.ha = (bf16*)((char*)work + 8192 + 2LL * PS_R * W * 4);"),
+                  ("  for (int k = 0; k < p.S; ++k) {\n    const unsigned target", "  unsigned long long* stp = (unsigned long long*)((char*)p.cnt + 1024);\n  int sti = 0;\n#define STAMP() do { if (blockIdx.x == 0 && tid == 0 && k == 50) stp[sti++] = __builtin_amdgcn_s_memtime(); } while (0)\n  for (int k = 0; k < p.S; ++k) {\n    STAMP();\n    const unsigned target"),
+                  ("#pragma unroll 1\n    for (int blk = 0; blk < D; ++blk) {", "    STAMP();\n#pragma unroll 1\n    for (int blk = 0; blk < D; ++blk) {"),
+                  ("        ps_wait(p.cnt + 2 * blk - 1, target, p.err);\n        load_h((blk - 1) & 1);\n        res_from_hx((blk - 1) & 1);",
+                   "        ps_wait(p.cnt + 2 * blk - 1, target, p.err);\n        STAMP();\n        load_h((blk - 1) & 1);\n        res_from_hx((blk - 1) & 1);"),
+                  ("      ln_mod(true);\n      __syncthreads();\n      mma(bw, 0);", "      ln_mod(true);\n      __syncthreads();\n      STAMP();\n      mma(bw, 0);"),
+                  ("        ps_publish(p.cnt + 2 * blk);\n      }", "        ps_publish(p.cnt + 2 * blk);\n      }\n      STAMP();"),
+                  ("      ps_wait(p.cnt + 2 * blk, target, p.err);\n", "      ps_wait(p.cnt + 2 * blk, target, p.err);\n      STAMP();\n"),
+                  ("        ps_publish(p.cnt + 2 * blk + 1);\n      }", "        ps_publish(p.cnt + 2 * blk + 1);\n      }\n      STAMP();"),
+                  ("      ps_wait(p.cnt + 2 * D - 1, target, p.err);\n      load_h((D - 1) & 1);", "      ps_wait(p.cnt + 2 * D - 1, target, p.err);\n      STAMP();\n      load_h((D - 1) & 1);")],
     "nostage": [("        halo_store((cc + 1) & 1);\n        ch_lds_barrier();", "        ch_lds_barrier();")],
 }
 
 
-FILES = {"maskfree": "attention.hip"}
+FILES = {"maskfree": "attention.hip", "ps_nowait": "sampler.hip", "ps_noload": "sampler.hip",
+         "ps_nosync": "sampler.hip", "ps_stamps": "sampler.hip"}
 
 
 def build(name, subs):

@@ -45,8 +45,12 @@ class ActionSampler:
     # B*1024 tokens) the general 256x256-tile GEMMs are the right tool
     FUSED_MAX_ROWS = 1024
 
-    def __init__(self, net, respacing="100", use_graph=True, use_fused=True, clip_denoised=True):
+    def __init__(self, net, respacing="100", use_graph=True, use_fused=True, clip_denoised=True,
+                 use_persistent=True):
         self.net = net
+        # few rows (R <= 16: action sampling at B = 1): the whole loop as ONE persistent launch
+        # (uva_sampler_persistent) instead of the captured ~15 launches per step
+        self.use_persistent = use_persistent
         self.clip = clip_denoised  # action head: True (diffusion_action_loss.py:218); video head: False
         self.sched = sampling_schedule(respacing)
         self.use_graph = use_graph
@@ -162,7 +166,7 @@ class ActionSampler:
         cd = cdt()
         # RT.param_gen: the optimizer / EMA kernels rewrite weights without bumping _version, and the
         # captured graph and the concatenated modulation weights (wcat / bcat) must follow them
-        sig = (R, C, str(cd), float(temperature), str(dev), self.use_fused, RT.param_gen,
+        sig = (R, C, str(cd), float(temperature), str(dev), self.use_fused, self.use_persistent, RT.param_gen,
                tuple((p.data_ptr(), p._version) for p in net.parameters()))
         cache = getattr(self, "_cache", None)
         if cache is not None and cache["sig"] == sig:
@@ -183,6 +187,24 @@ class ActionSampler:
                   mean=torch.empty(R, dtype=F32, device=dev), rstd=torch.empty(R, dtype=F32, device=dev),
                   out=torch.empty(R, 2 * C, dtype=F32, device=dev), graph=None,
                   fused=self.use_fused and cd == torch.bfloat16 and W in (256, 512, 1024) and R <= self.FUSED_MAX_ROWS)
+        st["persist"] = (self.use_persistent and st["fused"] and st["mod"] is not None and R <= 16 and W == 1024
+                         and len(blocks) == 6 and C <= 16 and dev.type == "cuda")
+        if st["persist"]:
+            # weights stacked per kind (one base pointer each), coefficient table [S, 8] on the device
+            st["pack"] = dict(
+                w1=torch.stack([compute_weight(b[2]) for b in blocks]).contiguous(),
+                b1=torch.stack([b[3].detach().float() for b in blocks]).contiguous(),
+                w2=torch.stack([compute_weight(b[4]) for b in blocks]).contiguous(),
+                b2=torch.stack([b[5].detach().float() for b in blocks]).contiguous(),
+                lnw=torch.stack([b[6].detach().float() for b in blocks]).contiguous(),
+                lnb=torch.stack([b[7].detach().float() for b in blocks]).contiguous(),
+                win=compute_weight(net.input_proj.weight).contiguous(),
+                bin=net.input_proj.bias.detach().float().contiguous(),
+                wf=compute_weight(fl[2]).contiguous(), bfin=fl[3].detach().float().contiguous())
+            st["coef"] = torch.tensor([list(self.sched.steps[k][2]) + [float(temperature)] for k in range(S)],
+                                      dtype=F32, device=dev)
+            st["work"] = ops.sampler_persistent_workspace(W, dev)
+            st["xo"] = torch.empty(R, C, dtype=F32, device=dev)
         self._cache = st
         return st
 
@@ -198,6 +220,10 @@ class ActionSampler:
             raise ValueError(f"cond rows {c.shape[0]} != noise rows {R}")
         st = self._state(R, C, dev, temperature)
         self._modulation(c, st)
+        if st["persist"]:
+            ops.sampler_persistent(st["pack"], st["mod"], st["coef"], step_noise.contiguous(), noise.contiguous(),
+                                   st["xo"], st["work"], clip=self.clip)
+            return st["xo"].clone()
         st["x"].copy_(noise)
         st["x_net"].copy_(noise)
         st["noise"].copy_(step_noise)

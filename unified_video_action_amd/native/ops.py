@@ -237,6 +237,36 @@ def diffusion_loss(x0, noise, t, out, tables, loss_row, dl):
                ctypes.cast(arr, ctypes.c_void_p), ptr(loss_row), ptr(dl), rows, C, stream())
 
 
+def sampler_persistent(pack, mod, coef, noise, x0, x_out, work, clip=True, eps=1e-6):
+    """The whole p_sample_loop of the action head in one launch (uva_sampler_persistent).
+    pack: dict of the stacked weights (w1, b1, w2, b2, lnw, lnb, win, bin, wf, bfin); mod [S, R, ncol]
+    bf16; coef [S, 8] fp32; noise [S, R, C]; x0 / x_out [R, C] fp32; work: uva_sampler_persistent_workspace
+    bytes (uint8, 256-B aligned)."""
+    S, R, C = noise.shape
+    depth, W = pack["b1"].shape
+    for t in (coef, noise, x0, x_out, mod):
+        if not t.is_contiguous():
+            raise ValueError("sampler_persistent: contiguous operands required")
+    if mod.shape[:2] != (S, R) or coef.shape != (S, 8) or x0.shape != (R, C) or x_out.shape != (R, C):
+        raise ValueError("sampler_persistent: shape mismatch")
+    lib().call("uva_sampler_persistent", R, C, W, depth, S, int(clip), float(eps), ptr(pack["w1"]), ptr(pack["b1"]),
+               ptr(pack["w2"]), ptr(pack["b2"]), ptr(pack["lnw"]), ptr(pack["lnb"]), ptr(pack["win"]),
+               ptr(pack["bin"]), ptr(pack["wf"]), ptr(pack["bfin"]), ptr(mod), mod.shape[2], ptr(coef), ptr(noise),
+               ptr(x0), ptr(x_out), ptr(work), work.numel(), stream())
+
+
+def sampler_persistent_workspace(W, device):
+    return torch.empty(lib().query("uva_sampler_persistent_workspace", W), dtype=torch.uint8, device=device)
+
+
+def sampler_persistent_status(work):
+    """1 if a spin of the last persistent sampler run on `work` gave up (results invalid); syncs."""
+    flag = ctypes.c_uint(0)
+    lib().call("uva_sampler_persistent_status", ptr(work), ctypes.cast(ctypes.pointer(flag), ctypes.c_void_p),
+               stream())
+    return flag.value
+
+
 def p_sample_step(out, x, noise, coef, x_new, x_net=None, clip=True):
     """One reverse diffusion step (uva_p_sample_step); coef = 8 python floats of the step."""
     rows, C = x.shape
