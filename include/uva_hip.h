@@ -88,6 +88,13 @@ int uva_conv3x3_halo_bn(int Nimg, int H, int W, int Ci, int Co);
 int uva_conv3x3_halo(const void* in, const void* w, void* out, const float* bias, const void* residual, int Nimg,
                      int H, int W, int Ci, int Co, const float* gn_scale, const float* gn_shift, int gn_silu,
                      float* gn_part, hipStream_t stream);
+/* Downsample (vaekl.py Downsample with_conv: F.pad(x, (0, 1, 0, 1)) then 3x3 / stride 2 / pad 0) as a
+ * halo-tile kernel: NHWC bf16 [Nimg][Hin][Win][Ci] -> [Nimg][Hin/2][Win/2][Co], bias, optional fused
+ * GN partials of the output.  uva_conv3x3s2_ok: Hin % 16, Win % 32, Ci % 64, Co % 128 == 0.
+ * uva_conv2d routes 3x3/s2/p0 with Hout == Hin/2 (the implicit bottom/right zero pad) here. */
+int uva_conv3x3s2_ok(int Nimg, int Hin, int Win, int Ci, int Co);
+int uva_conv3x3s2_halo(const void* in, const void* w, void* out, const float* bias, int Nimg, int Hin, int Win,
+                       int Ci, int Co, float* gn_part, hipStream_t stream);
 /* Encoder.conv_in (vaekl.py:246-249) on the 8-channel padded frame -> 128 channels, bf16, bias, optional
  * fused GN partials; H, W % 16 == 0.  uva_conv2d routes Ci == 8, Co == 128 3x3/s1/p1 here. */
 int uva_conv_in8(const void* in, const void* w, void* out, const float* bias, int Nimg, int H, int W,

@@ -95,3 +95,52 @@ def test_conv_in8_matches_torch(n, H, W):
     rstd = (o.var(dim=(1, 3), unbiased=False) + 1e-6).rsqrt()
     assert rel_err(gsc, rstd.repeat_interleave(4, dim=1)) < 1e-4
     assert rel_err(gsh, -mean.repeat_interleave(4, dim=1) * rstd.repeat_interleave(4, dim=1)) < 1e-4
+
+
+@pytest.mark.parametrize("n,H,W,Ci,Co", [(2, 32, 32, 128, 128), (1, 64, 32, 256, 256), (3, 16, 64, 64, 128),
+                                         (1, 48, 96, 128, 256)])
+@pytest.mark.parametrize("gn", [False, True])
+def test_conv_s2_halo_matches_torch(n, H, W, Ci, Co, gn):
+    """Downsample (vaekl.py Downsample with_conv): F.pad(x, (0, 1, 0, 1)) + 3x3 / stride 2 / pad 0,
+    routed by uva_conv2d to the stride-2 halo kernel; also checked against the implicit-GEMM route."""
+    from unified_video_action_amd.native import ops
+    from unified_video_action_amd.native.lib import lib
+    torch.manual_seed(3 * n + H + W + Ci + Co)
+    assert lib().query("uva_conv3x3s2_ok", n, H, W, Ci, Co) > 0
+    x = torch.randn(n, H, W, Ci, device=DEV).to(torch.bfloat16)
+    w = (torch.randn(Co, 3, 3, Ci, device=DEV) * 0.05).to(torch.bfloat16)
+    bias = torch.randn(Co, device=DEV) * 0.1
+    Ho, Wo = H // 2, W // 2
+    out = torch.empty(n, Ho, Wo, Co, device=DEV, dtype=torch.bfloat16)
+    part = torch.empty(n * Ho * Wo // 128, 32, 2, device=DEV) if gn else None
+    ops.conv2d(x, w, out, n, H, W, Ci, Co, 3, 2, 0, 0, Ho, Wo, bias=bias, gn_part=part)
+    xp = F.pad(x.float().permute(0, 3, 1, 2), (0, 1, 0, 1))
+    ref = F.conv2d(xp, w.float().permute(0, 3, 1, 2), bias, stride=2).permute(0, 2, 3, 1)
+    assert rel_err(out.float(), ref) < 1e-2
+    gen = torch.empty_like(out)
+    ops.conv2d(x, w, gen, n, H, W, Ci, Co, 3, 2, 0, 0, Ho, Wo, bias=bias, force_generic=True)
+    assert rel_err(out.float(), gen.float()) < 1e-2
+    if gn:
+        gamma = torch.randn(Co, device=DEV)
+        beta = torch.randn(Co, device=DEV)
+        gsc = torch.empty(n, Co, device=DEV)
+        gsh = torch.empty(n, Co, device=DEV)
+        ops.groupnorm_finalize_tiles(part, n, Ho * Wo, Co, gamma, beta, gsc, gsh, eps=1e-6)
+        o = out.double().reshape(n, Ho * Wo, 32, Co // 32)
+        mean = o.mean(dim=(1, 3))
+        rstd = (o.var(dim=(1, 3), unbiased=False) + 1e-6).rsqrt()
+        sc_ref = gamma.double()[None] * rstd.repeat_interleave(Co // 32, dim=1)
+        sh_ref = beta.double()[None] - mean.repeat_interleave(Co // 32, dim=1) * sc_ref
+        assert rel_err(gsc, sc_ref) < 1e-4
+        assert rel_err(gsh, sh_ref) < 1e-4
+
+
+def test_conv_s2_halo_eligibility():
+    from unified_video_action_amd.native.lib import lib
+    q = lambda *a: lib().query("uva_conv3x3s2_ok", *a) > 0  # noqa: E731
+    assert q(256, 256, 256, 128, 128) and q(256, 128, 128, 128, 128)
+    assert q(256, 64, 64, 256, 256) and q(256, 32, 32, 256, 256)
+    assert not q(4, 24, 32, 128, 128)   # Hin % 16
+    assert not q(4, 32, 16, 128, 128)   # Win % 32
+    assert not q(4, 32, 32, 32, 128)    # Ci % 64
+    assert not q(4, 32, 32, 128, 64)    # Co % 128

@@ -120,9 +120,10 @@ FILES = {"maskfree": "attention.hip", "ps_nowait": "sampler.hip", "ps_noload": "
          "ps_nosync": "sampler.hip", "ps_stamps": "sampler.hip"}
 
 
-def build(name, subs):
+def build(name, subs, whole=None):
+    """whole: path of a complete replacement for the source file (an A/B of a rewritten kernel)."""
     fn = FILES.get(name, "conv.hip")
-    src = open(os.path.join(CSRC, fn)).read()
+    src = open(whole or os.path.join(CSRC, fn)).read()
     for a, b in subs:
         assert a in src, (name, a)
         src = src.replace(a, b)
@@ -141,6 +142,10 @@ def build(name, subs):
 
 if __name__ == "__main__":
     os.makedirs(AB, exist_ok=True)
+    if len(sys.argv) == 4 and sys.argv[1] == "--file":  # --file NAME PATH: conv.hip replaced by PATH
+        build(sys.argv[2], [], whole=sys.argv[3])
+        print("built", sys.argv[2])
+        sys.exit(0)
     for n in (sys.argv[1:] or VARIANTS):
         build(n, VARIANTS[n])
         print("built", n)

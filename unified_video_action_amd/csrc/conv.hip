@@ -701,6 +701,228 @@ __global__ __launch_bounds__(TR * 32, 16 / TR) void conv3x3_halo(const bf16* __r
   }
 }
 
+// =====================================================================================
+// Downsample conv (vaekl.py:59-72: F.pad(x, (0, 1, 0, 1)) then 3x3 / stride 2 / no padding) as a
+// halo-tile kernel.  Output tile 8 x 16 pixels x 128 channels, 256 threads, two workgroups per CU;
+// per 64-channel chunk the 17 x 33-pixel input halo (zero past the bottom / right edge = the pad)
+// is staged ONCE in LDS -- the implicit-GEMM route re-gathered every input element 2.25x from L2
+// (455 TFLOP/s at the level-0 shape) -- with the columns de-interleaved into an even plane (17
+// pixels per row) and an odd plane (16): tap column kw = 0 / 1 / 2 of output column ow reads
+// pixel ow / ow / ow + 1 of the even / odd / even plane, so every A fragment is 16 CONSECUTIVE
+// pixels of one plane row, as in the stride-1 kernel.  Channel-chunk-major image: 16-B chunk c of
+// plane pixel p at (c * 576 + p) * 16 B, so a fragment read is 16 consecutive 16-B slots (no bank
+// conflict) at the lane's base + a compile-time offset (an XOR swizzle made every address a VALU
+// computation and spilled), 73.7 KB per workgroup.  The halo is written by LDS-DMA (buffer loads
+// into LDS, 16 B per lane, 18 wave-instructions per wave all in flight at once, per-lane source
+// offsets computed once).  Level-0 shape (n256 256x256 C128), same box: implicit-GEMM route 2.72 ms
+// (455 TFLOP/s); VGPR-staged fill (~3 loads per thread in flight) 2.56; this 2.07-2.15 ms (~590).
+// Rejected: 32-channel chunks double-buffered so chunk cc + 1's DMA runs under chunk cc's taps
+// (2.26 ms; a weight ring one chunk deep so no waited load follows the DMA: 2.50) -- two workgroups
+// per CU already overlap one's fill with the other's taps.
+// Weights as in the register-B stride-1 kernel: the transposed product (weights = A operand,
+// pixels = B), each wave 32 output channels x the tile's 128 pixels, weight fragments streamed
+// from L2 into VGPRs one tap ahead (buffer loads, K offset in soffset); bias-seeded accumulators;
+// register epilogue (permlane16 pairing into 16-B channel runs) with the GroupNorm(32) partial
+// sums of the stored output per 128-pixel tile for the next level's first GroupNorm.
+// =====================================================================================
+#define S2_HW 33                      // halo columns: 2 x 16 + 1
+#define S2_HH 17                      // halo rows: 2 x 8 + 1
+#define S2_PE (S2_HH * 17)            // even-plane pixels (17 per row); the odd plane follows (16 per row)
+#define S2_HPIX (S2_HH * S2_HW)       // 561
+#define S2_CS 576                     // slots per channel chunk (561 rounded up to whole wave-instructions)
+#define S2_DI 18                      // LDS-DMA wave-instructions per wave: 8 * 576 / 64 / 4
+#define S2_LDS (S2_CS * 8 * 16)       // 73728 B
+__global__ __launch_bounds__(256, 2) void conv3x3s2_kernel(const bf16* __restrict__ in, const bf16* __restrict__ wt,
+                                                          bf16* __restrict__ out, const float* __restrict__ bias,
+                                                          float* __restrict__ gn_part, int Nimg, int Hin, int Win,
+                                                          int Ci, int Co) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  bf16* halo = (bf16*)smem;
+  constexpr int FM = 8, FN = 2;
+  const int Hout = Hin / 2, Wout = Win / 2;
+  const int tiles_x = Wout / 16, tiles_y = Hout / 8, ncb = Co / 128;
+  const int nblk = Nimg * tiles_y * tiles_x * ncb;
+  const int pid = ch_xcd_remap(blockIdx.x, nblk);
+  const int cb = pid % ncb, sp = pid / ncb;
+  const int tx = sp % tiles_x, ty = (sp / tiles_x) % tiles_y, n = sp / (tiles_x * tiles_y);
+  const int oh0 = ty * 8, ow0 = tx * 16, n0 = cb * 128;
+  const int ih0 = 2 * oh0, iw0 = 2 * ow0;
+  const int K = 9 * Ci, nch = Ci / 64, S = nch * 9;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wn = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int frow = lane & 15, fk = lane >> 4;
+
+  // chunk cc of the input halo -> LDS by LDS-DMA through a per-image descriptor: slot j = 64 b + lane
+  // of wave-instruction b = wid * 18 + i holds chunk c = j / 576 of plane pixel p = j % 576; the
+  // channel chunk cc goes in soffset.  Pixels past the bottom / right edge (the F.pad border) and
+  // the slots past 561 get an offset beyond the descriptor's range: the DMA writes zeros.
+  const __amdgpu_buffer_rsrc_t rs_in = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(in + (long long)n * Hin * Win * Ci), 0, __builtin_amdgcn_readfirstlane(Hin * Win * Ci * 2), 0x00020000);
+  unsigned hoff[S2_DI];
+#pragma unroll
+  for (int i = 0; i < S2_DI; ++i) {
+    const int j = (wn * S2_DI + i) * 64 + lane;
+    const int c = j / S2_CS, p = j - c * S2_CS;
+    const bool odd = p >= S2_PE;
+    const int q = odd ? p - S2_PE : p, wdt = odd ? 16 : 17;
+    const int hy = q / wdt, hx = 2 * (q - hy * wdt) + (odd ? 1 : 0);
+    const int ih = ih0 + hy, iw = iw0 + hx;
+    hoff[i] = (p < S2_HPIX && ih < Hin && iw < Win) ? (unsigned)(((ih * Win + iw) * Ci + c * 8) * 2) : 0x80000000u;
+  }
+  auto halo_fill = [&](int cc) __attribute__((always_inline)) {
+    const int soff = __builtin_amdgcn_readfirstlane(cc * 128);
+#pragma unroll
+    for (int i = 0; i < S2_DI; ++i)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs_in, (__attribute__((address_space(3))) void*)(halo + (wn * S2_DI + i) * 512),
+                                               16, (int)hoff[i], soff, 0, 0);
+  };
+
+  // bias-seeded accumulators: acc[f][g] = out[pixel (row f, column frow)][channel n0 + wn*32 + g*16 + fk*4 + r]
+  f32x4 acc[FM][FN];
+#pragma unroll
+  for (int g = 0; g < FN; ++g) {
+    f32x4 b0 = (f32x4){0.f, 0.f, 0.f, 0.f};
+    if (bias) {
+      const float4 b = *(const float4*)(bias + n0 + wn * 32 + g * 16 + fk * 4);
+      b0 = (f32x4){b.x, b.y, b.z, b.w};
+    }
+#pragma unroll
+    for (int f = 0; f < FM; ++f) acc[f][g] = b0;
+  }
+  // weight fragment (ks, g) of step s: 16 B at wt[(n0 + wn*32 + g*16 + frow) * K + tap*Ci + cc*64 + ks*32 + fk*8]
+  const __amdgpu_buffer_rsrc_t rs_w =
+      __builtin_amdgcn_make_buffer_rsrc((void*)wt, 0, __builtin_amdgcn_readfirstlane(Co * K * 2), 0x00020000);
+  int vb[FN];
+#pragma unroll
+  for (int g = 0; g < FN; ++g) vb[g] = ((n0 + wn * 32 + g * 16 + frow) * K + fk * 8) * 2;
+  bf16x8 bq[2][2][FN];  // [register set][ks][g]
+  auto bload = [&](int s, bf16x8 (&dst)[2][FN]) __attribute__((always_inline)) {
+    const int cc = s / 9, tap = s - cc * 9;
+    const int soff = __builtin_amdgcn_readfirstlane((tap * Ci + cc * 64) * 2);
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int g = 0; g < FN; ++g)
+        dst[ks][g] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rs_w, vb[g] + ks * 64, soff, 0));
+  };
+  bload(0, bq[0]);
+  const bf16* abase = halo + (fk * S2_CS + frow) * 8;  // lane part of every A fragment address
+
+  for (int cc = 0; cc < nch; ++cc) {
+    if (cc > 0) ch_lds_barrier();  // every wave is done with chunk cc-1's halo
+    halo_fill(cc);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+#pragma unroll
+    for (int tap = 0; tap < 9; ++tap) {
+      const int s = cc * 9 + tap;
+      const int cur = tap & 1, nxt = cur ^ 1;  // tap 8's next set is copied to set 0 below
+      if (s + 1 < S) bload(s + 1, bq[nxt]);
+      const int kh = tap / 3, kw = tap % 3;
+      bf16x8 fa[2][FM];
+#pragma unroll
+      for (int f = 0; f < FM; ++f) {
+        const int hy = 2 * f + kh;
+        const int p0 = kw == 1 ? S2_PE + hy * 16 : hy * 17 + (kw == 2 ? 1 : 0);  // compile-time
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) fa[ks][f] = *(const bf16x8*)(abase + (ks * 4 * S2_CS + p0) * 8);
+      }
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+        for (int f = 0; f < FM; ++f)
+#pragma unroll
+          for (int g = 0; g < FN; ++g)
+            acc[f][g] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bq[cur][ks][g], fa[ks][f], acc[f][g], 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
+    }
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int g = 0; g < FN; ++g) bq[0][ks][g] = bq[1][ks][g];
+  }
+
+  // ---- register epilogue (as the stride-1 register-B kernel): channel runs cs .. cs + 7 of pixel
+  //      (row f, column frow), bf16 16-B stores, GroupNorm partial sums of the stored values
+  const long long pix0 = ((long long)n * Hout + oh0) * Wout + ow0 + frow;
+  const int cs = n0 + wn * 32 + (fk & 1) * 16 + (fk >> 1) * 8;
+  float sa = 0.f, sb = 0.f, qa = 0.f, qb = 0.f;
+#pragma unroll
+  for (int f = 0; f < FM; ++f) {
+    float v[8];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(acc[f][0][i]), __float_as_uint(acc[f][1][i]),
+                                                      false, false);
+      v[i] = __uint_as_float(r[0]);
+      v[4 + i] = __uint_as_float(r[1]);
+    }
+    bf16x8 o;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) o[e] = (bf16)v[e];
+    *(bf16x8*)(out + (pix0 + (long long)f * Wout) * Co + cs) = o;
+    if (gn_part) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float q = (float)o[e], w2 = (float)o[4 + e];
+        sa += q;
+        qa += q * q;
+        sb += w2;
+        qb += w2 * w2;
+      }
+    }
+  }
+  if (gn_part) {
+    const int gsz = Co / 32;  // 4 (two groups per lane), 8 (one) or 16 (one, with row fk^2)
+    if (gsz >= 8) {
+      sa += sb;
+      qa += qb;
+    }
+#pragma unroll
+    for (int o = 1; o < 16; o <<= 1) {
+      sa += __shfl_xor(sa, o, 64);
+      qa += __shfl_xor(qa, o, 64);
+      sb += __shfl_xor(sb, o, 64);
+      qb += __shfl_xor(qb, o, 64);
+    }
+    if (gsz >= 16) {
+      sa = xor_lane_sum(sa, 32);
+      qa = xor_lane_sum(qa, 32);
+    }
+    if (frow == 0 && (gsz < 16 || fk < 2)) {
+      const long long t128 = (long long)n * (tiles_x * tiles_y) + (sp % (tiles_x * tiles_y));
+      float* gp = gn_part + (t128 * 32 + cs / gsz) * 2;
+      *(float2*)gp = make_float2(sa, qa);
+      if (gsz == 4) *(float2*)(gp + 2) = make_float2(sb, qb);
+    }
+  }
+}
+
+extern "C" int uva_conv3x3s2_ok(int Nimg, int Hin, int Win, int Ci, int Co) {
+  return Nimg > 0 && Hin % 16 == 0 && Win % 32 == 0 && Ci % 64 == 0 && Ci >= 64 && Co % 128 == 0 &&
+         (long long)Co * 9 * Ci * 2 < (1LL << 31);
+}
+
+extern "C" int uva_conv3x3s2_halo(const void* in, const void* w, void* out, const float* bias, int Nimg, int Hin,
+                                  int Win, int Ci, int Co, float* gn_part, hipStream_t stream) {
+  if (Nimg <= 0) return 0;
+  if (!uva_conv3x3s2_ok(Nimg, Hin, Win, Ci, Co) || (((uintptr_t)in | (uintptr_t)w | (uintptr_t)out) % 16))
+    return (int)hipErrorInvalidValue;
+  const long long nblk = (long long)Nimg * (Hin / 16) * (Win / 32) * (Co / 128);
+  if (nblk >= (1ll << 31)) return (int)hipErrorInvalidValue;
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)conv3x3s2_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, S2_LDS);
+    attr = true;
+  }
+  conv3x3s2_kernel<<<dim3((unsigned)nblk), 256, S2_LDS, stream>>>((const bf16*)in, (const bf16*)w, (bf16*)out, bias,
+                                                                   gn_part, Nimg, Hin, Win, Ci, Co);
+  UVA_LAUNCH_CHECK();
+  return 0;
+}
+
 // eligibility of the halo kernel (host side mirror: native/ops.py conv_halo_ok)
 static int halo_bn(int Nimg, int H, int W, int Ci, int Co) {
   if (H % CH_T || W % CH_T || Ci % 64 || Ci < 64) return 0;

@@ -1740,6 +1740,9 @@ extern "C" int uva_conv3x3_halo(const void* in, const void* w, void* out, const 
                                 int Nimg, int H, int W, int Ci, int Co, const float* gn_scale, const float* gn_shift,
                                 int gn_silu, float* gn_part, hipStream_t stream);
 
+extern "C" int uva_conv3x3s2_ok(int Nimg, int Hin, int Win, int Ci, int Co);
+extern "C" int uva_conv3x3s2_halo(const void* in, const void* w, void* out, const float* bias, int Nimg, int Hin,
+                                  int Win, int Ci, int Co, float* gn_part, hipStream_t stream);
 extern "C" int uva_conv_in8(const void* in, const void* w, void* out, const float* bias, int Nimg, int H, int W,
                             float* gn_part, hipStream_t stream);
 
@@ -1754,6 +1757,11 @@ extern "C" int uva_conv2d(int dtype, const void* in, const void* w, void* out, c
       Hout == Hin && Wout == Win && act == ACT_NONE && uva_conv3x3_halo_bn(Nimg, Hin, Win, Ci, Co) > 0)
     return uva_conv3x3_halo(in, w, out, bias, residual, Nimg, Hin, Win, Ci, Co, gn_scale, gn_shift, gn_silu, gn_part,
                             stream);
+  // Downsample: F.pad(0, 1, 0, 1) + 3x3 / s2 / p0 with 8x16-tileable outputs: halo-tile kernel (conv.hip)
+  if (!force_generic && dtype == UVA_DT_BF16 && ks == 3 && stride == 2 && pad_t == 0 && pad_l == 0 &&
+      Hout * 2 == Hin && Wout * 2 == Win && act == ACT_NONE && !residual && !gn_scale &&
+      uva_conv3x3s2_ok(Nimg, Hin, Win, Ci, Co))
+    return uva_conv3x3s2_halo(in, w, out, bias, Nimg, Hin, Win, Ci, Co, gn_part, stream);
   // the 8-channel (padded RGB) input conv: store-bound special form (conv.hip)
   if (!force_generic && dtype == UVA_DT_BF16 && ks == 3 && stride == 1 && pad_t == 1 && pad_l == 1 &&
       Hout == Hin && Wout == Win && act == ACT_NONE && Ci == 8 && Co == 128 && !residual && !gn_scale &&

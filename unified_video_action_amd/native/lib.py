@@ -45,7 +45,10 @@ class UvaLib:
                 "There is no CPU fallback on the product path.")
         self._lib = ctypes.CDLL(path)
         self.sigs = parse_header()
+        ab = bool(os.environ.get("UVA_LIB_PATH"))
         for name, (res, args) in self.sigs.items():
+            if ab and not hasattr(self._lib, name):
+                continue  # an older A/B build: entry points it predates stay unbound (calling one raises)
             fn = getattr(self._lib, name)  # AttributeError = missing export -> loud
             fn.restype = res
             fn.argtypes = args
