@@ -10,7 +10,7 @@ CSRC = os.path.join(ROOT, "unified_video_action_amd", "csrc")
 OBJ = os.path.join(ROOT, "unified_video_action_amd", "build_obj")
 AB = os.path.join(ROOT, "ab")
 FLAGS = ["--offload-arch=gfx950", "-O3", "-fPIC", "-std=c++17", "-munsafe-fp-atomics", "-Wno-unused-result",
-         "-I" + CSRC]
+         "-I" + CSRC] + os.environ.get("DIAG_FLAGS", "").split()
 
 ANCHOR = "  const int pid = ch_xcd_remap(blockIdx.x, nblk);"
 VARIANTS = {
@@ -112,6 +112,27 @@ VARIANTS = {
                   ("      ps_wait(p.cnt + 2 * blk, target, p.err);\n", "      ps_wait(p.cnt + 2 * blk, target, p.err);\n      STAMP();\n"),
                   ("        ps_publish(p.cnt + 2 * blk + 1);\n      }", "        ps_publish(p.cnt + 2 * blk + 1);\n      }\n      STAMP();"),
                   ("      ps_wait(p.cnt + 2 * D - 1, target, p.err);\n      load_h((D - 1) & 1);", "      ps_wait(p.cnt + 2 * D - 1, target, p.err);\n      STAMP();\n      load_h((D - 1) & 1);")],
+    # GN + SiLU with scalar f32 VALU (the packed v_pk_* forms cost extra issue beside MFMAs)
+    "gnscalar": [("""#pragma unroll
+          for (int j = 0; j < 8; j += 2) {
+            const f32x2 x = {(float)v[j], (float)v[j + 1]};
+            f32x2 u = x * (f32x2){gsc[j], gsc[j + 1]} + (f32x2){gsh[j], gsh[j + 1]};
+            if (gn_silu) {
+              const f32x2 t = u * (f32x2){-1.4426950408889634f, -1.4426950408889634f};
+              const f32x2 d = (f32x2){__builtin_amdgcn_exp2f(t.x), __builtin_amdgcn_exp2f(t.y)} + (f32x2){1.f, 1.f};
+              u = u * (f32x2){__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y)};
+            }
+            v[j] = (bf16)u.x;
+            v[j + 1] = (bf16)u.y;
+          }""", """#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            float u = __builtin_fmaf((float)v[j], gsc[j], gsh[j]);
+            if (gn_silu) {
+              const float d = __builtin_amdgcn_exp2f(u * -1.4426950408889634f) + 1.f;
+              u = u * __builtin_amdgcn_rcpf(d);
+            }
+            v[j] = (bf16)u;
+          }""")],
     "nostage": [("        halo_store((cc + 1) & 1);\n        ch_lds_barrier();", "        ch_lds_barrier();")],
 }
 
