@@ -143,32 +143,41 @@ __global__ __launch_bounds__(256) void attn_mask_kernel(uint64_t* __restrict__ M
   const int q = qb * 64 + mask_pos(L);  // lane L holds the query whose MK bit is L
   const uint32_t key = drop_key(seed);
   const uint64_t pair0 = (((uint64_t)bh * N + q) * (uint64_t)N + (uint64_t)kv * 64) >> 1;
-  uint32_t lo = 0, hi = 0;  // MQ word of this lane's query (bit mask_pos(k) <-> key kv*64 + k)
+  // pair0 is a multiple of 32 (N % 64 == 0), so pair0 + j (j < 32) changes only its low 5 bits:
+  // drop_hash's first word for pair j is x0 ^ j (no 64-bit arithmetic in the loop)
+  const uint32_t x0 = drop_first(key, pair0);
+  uint32_t lo = 0, hi = 0;  // DROP bits of this lane's query (bit mask_pos(k) <-> key kv*64 + k)
 #pragma unroll
   for (int j = 0; j < 32; ++j) {
-    const uint32_t hv = drop_hash(key, pair0 + j);
-    const uint32_t k0 = (hv & 0xFFFFu) >= th, k1 = (hv >> 16) >= th;
+    const uint32_t hv = drop_mix(x0 ^ (uint32_t)j);
+    // element dropped iff its 16-bit draw < th: the sign of draw - th
+    const uint32_t d0 = ((hv & 0xFFFFu) - th) >> 31, d1 = ((hv >> 16) - th) >> 31;
     const int p0 = mask_pos(2 * j), p1 = mask_pos(2 * j + 1);
-    if (p0 < 32) lo |= k0 << p0; else hi |= k0 << (p0 - 32);
-    if (p1 < 32) lo |= k1 << p1; else hi |= k1 << (p1 - 32);
+    if (p0 < 32) lo |= d0 << p0; else hi |= d0 << (p0 - 32);
+    if (p1 < 32) lo |= d1 << p1; else hi |= d1 << (p1 - 32);
   }
+  lo = ~lo;
+  hi = ~hi;
   MQ[((long long)bh * nt + kv) * N + q] = ((uint64_t)hi << 32) | lo;
   // 64x64 bit transpose across the wave (rows = lanes): afterwards lane L' holds, at bit L, the
   // bit mask_pos(L') of lane L, i.e. keep(query with MK position L, key kv*64 + mask_pos(L')).
+  // Branch-free: per stage the lane's shift amounts and keep mask are selects, the exchange a
+  // ds_swizzle (xor within 32 lanes) or v_permlane32_swap (the 32-lane stage).
   {
     const bool up = L & 32;
-    const uint32_t r = (uint32_t)__shfl_xor((int)(up ? lo : hi), 32, 64);
-    if (up) lo = r; else hi = r;
+    const auto r = __builtin_amdgcn_permlane32_swap(up ? lo : hi, up ? lo : hi, false, false);
+    const uint32_t o = up ? r[0] : r[1];  // the other half's word
+    if (up) lo = o; else hi = o;
   }
 #define UVA_TSTAGE(J, M)                                                                    \
   {                                                                                         \
     const bool up = L & (J);                                                                \
-    const uint32_t sl = up ? (lo & (M)) : ((lo >> (J)) & (M));                              \
-    const uint32_t sh = up ? (hi & (M)) : ((hi >> (J)) & (M));                              \
-    const uint32_t rl = (uint32_t)__shfl_xor((int)sl, (J), 64);                             \
-    const uint32_t rh = (uint32_t)__shfl_xor((int)sh, (J), 64);                             \
-    lo = up ? ((lo & ~(M)) | rl) : ((lo & (M)) | (rl << (J)));                               \
-    hi = up ? ((hi & ~(M)) | rh) : ((hi & (M)) | (rh << (J)));                               \
+    const uint32_t sr = up ? 0u : (uint32_t)(J); /* down lanes send and receive the high halves */ \
+    const uint32_t km = up ? ~(M) : (M);                                                    \
+    const uint32_t rl = (uint32_t)__builtin_amdgcn_ds_swizzle((int)((lo >> sr) & (M)), 0x1F | ((J) << 10)); \
+    const uint32_t rh = (uint32_t)__builtin_amdgcn_ds_swizzle((int)((hi >> sr) & (M)), 0x1F | ((J) << 10)); \
+    lo = (lo & km) | (rl << sr);                                                            \
+    hi = (hi & km) | (rh << sr);                                                            \
   }
   UVA_TSTAGE(16, 0x0000FFFFu)
   UVA_TSTAGE(8, 0x00FF00FFu)

@@ -62,8 +62,21 @@ __device__ __forceinline__ uint32_t drop_key(uint64_t seed) {
   k ^= k >> 15;
   return k;
 }
+// drop_hash = drop_mix(first word); split so a caller hashing pairs base..base+31 of a 32-aligned
+// base can form the first word as (base's first word) ^ j
+__device__ __forceinline__ uint32_t drop_first(uint32_t key, uint64_t pair) {
+  return (uint32_t)pair ^ (key + __builtin_rotateleft32((uint32_t)(pair >> 32), 11));
+}
+__device__ __forceinline__ uint32_t drop_mix(uint32_t x) {
+  x ^= x >> 16;
+  x *= 0x7feb352du;
+  x ^= x >> 15;
+  x *= 0x846ca68bu;
+  x ^= x >> 16;
+  return x;
+}
 __device__ __forceinline__ uint32_t drop_hash(uint32_t key, uint64_t pair) {
-  uint32_t x = (uint32_t)pair ^ (key + __builtin_rotateleft32((uint32_t)(pair >> 32), 11));
+  uint32_t x = drop_first(key, pair);
   x ^= x >> 16;
   x *= 0x7feb352du;
   x ^= x >> 15;
