@@ -33,7 +33,10 @@ extern "C" {
  * C[z] = epi(alpha * opA[z] (MxK) . opB[z]^T (NxK)) ; ta/tb select stored layouts
  * (ta=0: A[M][K], ta=1: A[K][M]; tb=0: B[N][K], tb=1: B[K][N]).  Batch z = zo*inner+zi
  * with outer/inner strides.  Epilogue order: +bias[n] -> aux=pre-act -> act -> dropout
- * (counter hash, p, seed) -> +residual -> +beta*C_old.
+ * (counter hash, p, seed) -> +residual -> +beta*C_old.  act = 16 + ACT kind selects the
+ * activation BACKWARD: no forward activation and the residual operand is the saved
+ * pre-activation, multiplied in as act'(pre) instead of added (GELU/dropout backward of
+ * timm Mlp fused into the fc2 dX product, mar_con_unified.py:201-249).
  * Replaces: every nn.Linear fwd/bwd (timm Block qkv/proj/fc1/fc2
  * mar_con_unified.py:201-249; z_proj/z_proj_cond/proj_cond_x_layer/decoder_embed
  * :92-95,185-187,218; SimpleMLPAdaLN diffusion_loss.py:219-283; DiffActLoss fc/refine

@@ -142,3 +142,39 @@ def test_conv8_with_groupnorm_stats(residual):
     sh_ref = beta.double()[None] - mean.repeat_interleave(Co // 32, dim=1) * sc_ref
     assert rel_err(sc, sc_ref) < 1e-4
     assert rel_err(sh, sh_ref) < 1e-4
+
+
+@pytest.mark.parametrize("act", ["gelu", "silu"])
+@pytest.mark.parametrize("M,N,K,p", [(4096, 768, 3072, 0.1), (1000, 1024, 1024, 0.0), (256, 64, 96, 0.1)])
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+def test_linear_dx_act_matches_act_bwd(act, M, N, K, p, dtype):
+    """Activation(+dropout) backward fused into the dX GEMM epilogue (act = 16 + kind) against the
+    separate route: dX GEMM -> act_bwd (the same counter-hash keep bits, row * K + col) and against
+    a plain fp32 torch reference of act'(pre) * keep / (1 - p) * (dy @ w).  Tolerance: bf16 -> 2e-2
+    of the output scale (the separate route rounds dy @ w to bf16 first), fp32 -> 1e-5."""
+    from unified_video_action_amd.native import ops
+    torch.manual_seed(M + N + K)
+    dy = (torch.randn(M, N, device=DEV) * 0.5).to(dtype)
+    w = (torch.randn(N, K, device=DEV) * 0.05).to(dtype)
+    pre = (torch.randn(M, K, device=DEV) * 2).to(dtype)
+    fused = torch.empty(M, K, device=DEV, dtype=dtype)
+    ops.linear_dx_act(dy, w, fused, pre, act, drop_p=p, seed=77)
+    da = torch.empty(M, K, device=DEV, dtype=dtype)
+    ops.linear_dx(dy, w, da)
+    split = torch.empty(M, K, device=DEV, dtype=dtype)
+    ops.act_bwd(pre, da, split, act, drop_p=p, seed=77)
+    tol = 2e-2 if dtype == torch.bfloat16 else 1e-5
+    assert rel_err(fused.float(), split.float()) < tol
+    # fp32 reference with the kernels' own keep bits (recovered from the separate route on ones)
+    keep = torch.ones(M, K, device=DEV)
+    if p > 0:
+        ones = torch.ones(M, K, device=DEV, dtype=dtype)
+        kb = torch.empty(M, K, device=DEV, dtype=dtype)
+        ops.act_bwd(None, ones, kb, "none", drop_p=p, seed=77)
+        keep = kb.float()  # 0 or 1 / (1 - p)
+        assert abs((keep > 0).float().mean().item() - (1 - p)) < 0.01
+    x = pre.float().requires_grad_(True)
+    y = F.gelu(x) if act == "gelu" else F.silu(x)
+    g = (dy.float() @ w.float()) * keep
+    (dx_ref,) = torch.autograd.grad(y, x, g)
+    assert rel_err(fused.float(), dx_ref) < tol * 5

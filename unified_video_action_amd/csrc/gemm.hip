@@ -33,6 +33,8 @@ struct EpiParams {
   const void* gate;       // adaLN gate (row-major, ld = ldg, dtype gate_dt) or null
   long long ldg;
   int gate_dt, res_dt;    // runtime dtypes of gate / residual (UVA_DT_*)
+  int res_grad;           // ACT_* kind: "residual" is a pre-activation and the output is multiplied by
+                          // act'(pre) instead of added (activation backward fused into the dX GEMM)
 };
 
 struct BatchStrides {
@@ -69,7 +71,8 @@ __device__ __forceinline__ float epi_store(TC* C, long long ldc, long long coff,
   }
   if (ep.residual) {
     long long ri = roff + (long long)row * ep.ldr + col;
-    v += ep.res_dt == UVA_DT_BF16 ? (float)((const bf16*)ep.residual)[ri] : ((const float*)ep.residual)[ri];
+    const float r = ep.res_dt == UVA_DT_BF16 ? (float)((const bf16*)ep.residual)[ri] : ((const float*)ep.residual)[ri];
+    v = ep.res_grad ? v * act_grad(ep.res_grad, r) : v + r;
   }
   if (ep.beta != 0.f) v += ep.beta * to_f32(C[ci]);
   const TC o = from_f32<TC>(v);
@@ -412,7 +415,7 @@ __device__ __forceinline__ void epi_apply_row8(TC* __restrict__ C, long long cba
     float t = x[e];
     if (ep.drop_thresh) t = keep[e] ? t * ep.drop_scale : 0.f;
     if (ep.gate) t *= in.gate[e];
-    if (ep.residual) t += in.res[e];
+    if (ep.residual) t = ep.res_grad ? t * act_grad(ep.res_grad, in.res[e]) : t + in.res[e];
     if (ep.beta != 0.f) t += ep.beta * in.prev[e];
     o[e] = t;
   }
@@ -1666,6 +1669,10 @@ static EpiParams make_epi(const float* bias, const void* residual, long long ldr
   ep.residual = residual;
   ep.aux = aux;
   ep.act = act;
+  if (act >= 16) {  // activation backward: no forward activation, residual = pre-activation
+    ep.res_grad = act - 16;
+    ep.act = 0;
+  }
   ep.alpha = alpha;
   ep.beta = beta;
   uva_drop_params(drop_p, &ep.drop_thresh, &ep.drop_scale);

@@ -294,13 +294,17 @@ class BlockFn(torch.autograd.Function):
         ops.act_bwd_bias(None, g2, dpre2, grad_buf(fc2b), "none", drop_p=p_proj, seed=seeds[3])
         ops.linear_dw(dpre2, a, grad_buf(fc2w))
         Hd = fc1w.shape[0]
-        da = torch.empty(M, Hd, dtype=c, device=dev)
-        ops.linear_dx(dpre2, compute_weight(fc2w), da)
-        del dpre2
         # fc1 (gelu + drop1)
         dpre1 = torch.empty(M, Hd, dtype=c, device=dev)
-        ops.act_bwd_bias(pre1, da, dpre1, grad_buf(fc1b), "gelu", drop_p=p_proj, seed=seeds[2])
-        del da
+        if RT.act_bwd_in_gemm:
+            ops.linear_dx_act(dpre2, compute_weight(fc2w), dpre1, pre1, "gelu", drop_p=p_proj, seed=seeds[2])
+            ops.colsum(dpre1, grad_buf(fc1b))
+        else:
+            da = torch.empty(M, Hd, dtype=c, device=dev)
+            ops.linear_dx(dpre2, compute_weight(fc2w), da)
+            ops.act_bwd_bias(pre1, da, dpre1, grad_buf(fc1b), "gelu", drop_p=p_proj, seed=seeds[2])
+            del da
+        del dpre2
         ops.linear_dw(dpre1, h2, grad_buf(fc1w))
         # dX of the LN-fed GEMMs in the compute dtype (autocast: the matmul's input grad is half
         # precision before the cast back to the fp32 LayerNorm output); LN backward reads it as is
@@ -434,10 +438,14 @@ class AdaLNTrunkFn(torch.autograd.Function):
             ops.gate_bwd(dx, hm2, mod[:, 2 * W:], dhm2, dmod[:, 2 * W:])
             ops.linear_dw(dhm2, a, grad_buf(w2))
             ops.colsum(dhm2, grad_buf(b2))
-            da = torch.empty(R, W, dtype=c, device=dev)
-            ops.linear_dx(dhm2, compute_weight(w2), da)
             dpre1 = torch.empty(R, W, dtype=c, device=dev)
-            ops.act_bwd_bias(pre1, da, dpre1, grad_buf(b1), "silu")
+            if RT.act_bwd_in_gemm and pre1.dtype == c:
+                ops.linear_dx_act(dhm2, compute_weight(w2), dpre1, pre1, "silu")
+                ops.colsum(dpre1, grad_buf(b1))
+            else:
+                da = torch.empty(R, W, dtype=c, device=dev)
+                ops.linear_dx(dhm2, compute_weight(w2), da)
+                ops.act_bwd_bias(pre1, da, dpre1, grad_buf(b1), "silu")
             ops.linear_dw(dpre1, h, grad_buf(w1))
             dh = torch.empty(R, W, dtype=F32, device=dev)
             ops.linear_dx(dpre1, compute_weight(w1), dh)

@@ -102,6 +102,17 @@ def linear_dx(dy, w, dx, beta=0.0):
     gemm(dy, w, dx, M, K, N, _ld(dy), _ld(w), _ld(dx), 0, 1, beta=beta)
 
 
+def linear_dx_act(dy, w, dx, pre, act, drop_p=0.0, seed=0):
+    """dx[M,K] = act'(pre) * dropout(dy[M,N] @ w[N,K]) -- the dX product of the Linear after an
+    activation (+dropout) fused with that activation's backward (epilogue mode act = 16 + kind,
+    pre = the saved pre-activation [M,K]); the dropout index is row * K + col, as act_bwd's."""
+    M, N = dy.shape
+    K = w.shape[1]
+    assert dx.shape == (M, K) and pre.shape == (M, K) and pre.is_contiguous() and dx.is_contiguous()
+    gemm(dy, w, dx, M, K, N, _ld(dy), _ld(w), _ld(dx), 0, 1, residual=pre, ldr=_ld(pre), act=16 + ACT[act],
+         drop_p=drop_p, seed=seed)
+
+
 def linear_dw(dy, x, dw, beta=1.0):
     """dw[N,K] (+)= dy[M,N]^T @ x[M,K]  (fp32 grad buffer, accumulate by default)."""
     M, N = dy.shape

@@ -22,6 +22,10 @@ class _Runtime:
         # (/residual) pass each; the fused-epilogue GEMMs (False) measured equal-to-slower: the fused
         # fc1 epilogue's stores are not hidden at one workgroup per CU
         self.mlp_split_epilogue = True
+        # activation (+dropout) backward of the MLPs fused into the following Linear's dX GEMM
+        # epilogue (act'(pre) * dropout(dY W)); bias grad by a column sum of the stored result.
+        # False: dX GEMM -> separate act_bwd + column-sum pass (tests compare the two)
+        self.act_bwd_in_gemm = False  # off until measured on hardware (tools/job_actbwd.sh)
         self._seed_base = 0x5EED
         self._ctr = itertools.count()
         # attention dropout masks: per Block the (B, N, H, p) of its last training forward, and the
