@@ -72,7 +72,7 @@ def parse(argv=None):
     ap.add_argument("--cpu-batch-gpu", action="store_true",
                     help="also time the CPU baseline at the config's per-GPU batch (one step; minutes)")
     ap.add_argument("--trace-out", default="", help="write every traced kernel row (tag, launches, avg ms) here")
-    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r03.json"))
+    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r03_end.json"))
     return ap.parse_args(argv)
 
 
