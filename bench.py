@@ -56,8 +56,9 @@ def parse(argv=None):
     ap.add_argument("--batch", type=int, default=32)
     ap.add_argument("--config", default="pusht_video", choices=sorted(GFLOP_PER_SAMPLE))
     ap.add_argument("--precision", default="bf16", help="bf16 | fp8_attn (fp8 e4m3 attention) | fp32")
-    ap.add_argument("--other-configs", default="pusht_joint:64",
-                    help="N=1 only: extra config:batch entries measured after the main line ('' = none)")
+    ap.add_argument("--other-configs", default="pusht_joint:64,umi_multi:56:bf16,umi_multi:56:fp8_attn",
+                    help="N=1 only: extra config:batch[:precision] entries measured after the main line "
+                         "('' = none; precision defaults to --precision)")
     ap.add_argument("--other-steps", type=int, default=20)
     ap.add_argument("--launch-check", action="store_true",
                     help="check the --gpus N process wiring (gloo, no GPU work) and exit")
@@ -65,12 +66,16 @@ def parse(argv=None):
                     help="N=1: steps fed from host batches through the pinned prefetcher (0 = skip)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-batch", type=int, default=2, help="CPU baseline batch (BASELINE configs[0]: 2)")
-    ap.add_argument("--cpu-steps", type=int, default=3, help="timed CPU steps (median) after one warm-up step")
+    ap.add_argument("--cpu-warmup", type=int, default=5, help="CPU warm-up steps (BASELINE.md §4: 5)")
+    ap.add_argument("--cpu-steps", type=int, default=10, help="timed CPU steps, median reported (BASELINE.md §4: 10)")
+    ap.add_argument("--cpu-budget-s", type=float, default=150.0,
+                    help="wall budget of the B=2 leg: fewer timed steps (stated in `sample`) when a step is slow")
     ap.add_argument("--no-trace", action="store_true")
     ap.add_argument("--trace-steps", type=int, default=3)
-    ap.add_argument("--cpu-threads", type=int, default=0)
-    ap.add_argument("--cpu-batch-gpu", action="store_true",
-                    help="also time the CPU baseline at the config's per-GPU batch (one step; minutes)")
+    ap.add_argument("--cpu-threads", type=int, default=0,
+                    help="0 = the host's physical cores, capped by this process's cgroup CPU quota")
+    ap.add_argument("--no-cpu-batch-gpu", action="store_true",
+                    help="skip the CPU baseline step at the config's per-GPU batch")
     ap.add_argument("--trace-out", default="", help="write every traced kernel row (tag, launches, avg ms) here")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r03_end.json"))
     return ap.parse_args(argv)
@@ -225,13 +230,47 @@ def h2d_probe(state, device, steps):
             "ms_per_step_fed_from_host": round(fed_ms, 2)}
 
 
+def cpu_quota():
+    """CPUs this process may use by its cgroup (v2 cpu.max / v1 cfs quota), or None if unlimited."""
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            return max(1, int(int(q) / int(per)))
+    except (OSError, ValueError):
+        pass
+    try:
+        q = int(open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us").read())
+        per = int(open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read())
+        if q > 0:
+            return max(1, q // per)
+    except (OSError, ValueError):
+        pass
+    return None
+
+
+def cpu_threads(args, info):
+    """all host cores (physical), but never more than the cgroup quota allows (a
+    thread pool over the quota only time-slices)."""
+    if args.cpu_threads:
+        return args.cpu_threads
+    n = info.get("physical_cores") or info.get("usable") or os.cpu_count() or 1
+    q = cpu_quota()
+    if q is not None:
+        n = min(n, q)
+    return max(1, min(n, info.get("usable") or n))
+
+
 def cpu_baseline(args):
-    """oracle (PyTorch-CPU fp32 restatement, pinned to the reference) on a bounded sample: the
-    same training step at BASELINE configs[0]'s batch (2), one warm-up step, median of a few."""
+    """oracle (PyTorch-CPU fp32 restatement, pinned to the reference) timed per BASELINE.md §4: all
+    physical host cores (cgroup quota permitting), 5 warm-up steps + the median of 10 at BASELINE
+    configs[0]'s batch (2), then one step at the config's per-GPU batch.  The B=2 leg keeps to
+    --cpu-budget-s: if the warm-up shows a step too slow for 15 of them, fewer are timed (stated)."""
     import torch
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import uva_oracle as O
-    th = args.cpu_threads or torch.get_num_threads()
+    info = host_cpus()
+    info["cgroup_quota_cpus"] = cpu_quota()
+    th = cpu_threads(args, info)
     torch.set_num_threads(th)
     torch.manual_seed(0)
     mar = O.mar_base(task_name="pusht", act_dim=2, predict_action=args.config != "pusht_video")
@@ -239,11 +278,10 @@ def cpu_baseline(args):
     vae = O.AutoencoderKLEncoder()
     pol = O.PolicyOracle(mar, vae, [2 / 512, 2 / 512], [-1.0, -1.0]).train()
     opt = torch.optim.AdamW(mar.parameters(), lr=1e-4, betas=(0.9, 0.95), weight_decay=0.02)
-    B = args.cpu_batch
-    img = torch.rand(B, 32, 3, 96, 96)
-    act = torch.rand(B, 32, 2) * 512
 
-    def one():
+    def one(B):
+        img = torch.rand(B, 32, 3, 96, 96)
+        act = torch.rand(B, 32, 2) * 512
         rng = {"orders": torch.stack([torch.randperm(256) for _ in range(B)]).numpy(), "mask_rate": 0.85,
                "randint": [torch.randint(0, 1000, (B * 1024,))], "randn_like": [torch.randn(B * 1024, 16)],
                "vae_eps_x": torch.randn(B * 4, 16, 16, 16), "vae_eps_c": torch.randn(B * 4, 16, 16, 16)}
@@ -254,21 +292,29 @@ def cpu_baseline(args):
         opt.zero_grad()
         return time.perf_counter() - t0
 
-    one()  # warm-up
-    ts = [one() for _ in range(args.cpu_steps)]
+    B = args.cpu_batch
+    t_start = time.perf_counter()
+    warm = [one(B)]
+    nwarm, nsteps = args.cpu_warmup, args.cpu_steps
+    if warm[0] * (nwarm + nsteps) > args.cpu_budget_s:  # keep the default bench within minutes
+        nsteps = max(3, min(nsteps, int(args.cpu_budget_s / warm[0]) - 2))
+        nwarm = max(1, min(nwarm, int(args.cpu_budget_s / warm[0]) - nsteps))
+    warm += [one(B) for _ in range(nwarm - 1)]
+    ts = [one(B) for _ in range(nsteps)]
     med = statistics.median(ts)
+    proto = f"{nwarm} warm-up + median of {nsteps} steps"
+    if (nwarm, nsteps) != (args.cpu_warmup, args.cpu_steps):
+        proto += (f" (BASELINE.md §4 asks {args.cpu_warmup} + {args.cpu_steps}; cut to the "
+                  f"{args.cpu_budget_s:.0f} s budget at {warm[0]:.1f} s per step)")
     out = {"value": round(B / med, 5), "unit": "samples/s", "cores": th, "kind": "port",
-           "host_cpus": host_cpus(),
+           "host_cpus": info,
            "sample": f"oracle/uva_oracle.py full training step (resize->KL-VAE->mar_base fwd/bwd->AdamW), "
-                     f"PushT video_model, fp32, dropout 0.1, B={B}: 1 warm-up + median of {args.cpu_steps} steps "
-                     f"({', '.join(f'{t:.1f}' for t in ts)} s)"}
-    if args.cpu_batch_gpu and args.batch != B:
-        B = args.batch
-        img = torch.rand(B, 32, 3, 96, 96)
-        act = torch.rand(B, 32, 2) * 512
-        t = one()
-        out["per_gpu_batch"] = {"batch": B, "value": round(B / t, 5), "unit": "samples/s",
-                                "sample": f"one step at B={B} after the B={args.cpu_batch} runs ({t:.1f} s)"}
+                     f"PushT video_model, fp32, dropout 0.1, B={B}, torch.set_num_threads({th}): {proto} "
+                     f"({', '.join(f'{t:.2f}' for t in ts)} s; B={B} leg {time.perf_counter() - t_start:.0f} s)"}
+    if not args.no_cpu_batch_gpu and args.batch != B:
+        t = one(args.batch)  # the warm-ups above already paged in the weights and kernels
+        out["per_gpu_batch"] = {"batch": args.batch, "value": round(args.batch / t, 5), "unit": "samples/s",
+                                "sample": f"one step at B={args.batch} after the B={B} runs ({t:.1f} s)"}
     return out
 
 
@@ -364,12 +410,16 @@ def run(args):
     others = []
     if world == 1 and args.other_configs:
         for item in args.other_configs.split(","):
-            cfg, _, b = item.partition(":")
+            cfg, b, prec = (item.split(":") + ["", ""])[:3]
             b = int(b or args.batch)
+            prec = prec or args.precision
             torch.cuda.empty_cache()
-            e, ps, lo, st = timed_run(cfg, b, args.other_steps, args.warmup, args.precision, device, world, rank)
+            e, ps, lo, st = timed_run(cfg, b, args.other_steps, args.warmup, prec, device, world, rank)
             del st
-            others.append(dict(line_for(cfg, b, world, args.other_steps, e, ps, lo), steps=args.other_steps))
+            others.append(dict(line_for(cfg, b, world, args.other_steps, e, ps, lo), steps=args.other_steps,
+                               precision=prec))
+        from unified_video_action_amd.runtime import RT
+        RT.set_precision(args.precision)
     if rank != 0:
         if world > 1:
             dist.barrier()

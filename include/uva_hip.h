@@ -206,7 +206,10 @@ int uva_sampler_linear(int ln, const void* A, long long lda, const float* lnw, c
  * gate at 3Wi, final shift | scale at 3W depth); coef fp32 [S, 8] (uva_p_sample_step's order);
  * noise fp32 [S, R, C]; x0 fp32 [R, C] (x_T) -> x_out [R, C].  work: uva_sampler_persistent_workspace
  * bytes, 256-B aligned (the call zeroes its counters with a memset node).  W == 1024, depth == 6,
- * C <= 16.  uva_sampler_persistent_status: the spin give-up flag of the last run (0 = clean; syncs). */
+ * C <= 16.  A run in which any hand-off wait hit its spin bound writes NaN to every x_out element and
+ * sets the give-up flag; uva_sampler_persistent_status reads that flag (0 = clean; syncs the stream).
+ * The 64 workgroups must be co-resident (one per CU): callers check the CU count first.
+ * uva_sampler_persistent_test_hook(1): the NEXT launch publishes no phase (tests of the give-up path). */
 long long uva_sampler_persistent_workspace(int W);
 int uva_sampler_persistent(int R, int C, int W, int depth, int S, int clip, float eps, const void* w1, const float* b1,
                            const void* w2, const float* b2, const float* lnw, const float* lnb, const void* win,
@@ -214,6 +217,7 @@ int uva_sampler_persistent(int R, int C, int W, int depth, int S, int clip, floa
                            const float* coef, const float* noise, const float* x0, float* x_out, void* work,
                            long long work_bytes, hipStream_t stream);
 int uva_sampler_persistent_status(const void* work, unsigned* flag, hipStream_t stream);
+int uva_sampler_persistent_test_hook(int no_publish);
 
 /* ---- optimizer + EMA (policy:343-360 torch AdamW; ema_model.py:57-89) ----------------- */
 /* One launch per parameter group region (16-B aligned p/g/m/v/ema): n_decay = n applies the

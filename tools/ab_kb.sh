@@ -1,5 +1,5 @@
 # same-box A/B: focused tests ($FOCUS) on the in-tree build, then kbench mode $KB on
-# ab/libuva_base.so and the in-tree build (twice each, interleaved)
+# abx/libuva_base.so and the in-tree build (twice each, interleaved)
 set -o pipefail
 export TMPDIR=/tmp
 mkdir -p gpurun_out
@@ -9,7 +9,7 @@ if [ -n "$FOCUS" ]; then
 fi
 for i in 1 2; do
 for L in base new; do
-  if [ $L = base ]; then export UVA_LIB_PATH=$PWD/ab/libuva_base.so; else unset UVA_LIB_PATH; fi
-  echo "== $L"; timeout -k 10 200 python tools/tools_kbench.py $KB 2>&1 | grep -v amdgpu.ids || exit 1
+  if [ $L = base ]; then PY="python tools/ab_run.py abx/libuva_base.so"; else PY=python; fi
+  echo "== $L"; timeout -k 10 200 $PY tools/tools_kbench.py $KB 2>&1 | grep -v amdgpu.ids || exit 1
 done
 done

@@ -1,0 +1,22 @@
+"""Same-box A/B of two library builds (tools only; the product path never reads an override):
+
+    python tools/ab_run.py <path/to/libuva_other.so> <script.py> [args...]
+
+binds <lib> through native.lib.use_library() and then runs <script.py> as __main__.  Entry points
+that the other build predates stay unbound and are listed on stderr."""
+import os
+import runpy
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+if __name__ == "__main__":
+    if len(sys.argv) < 3:
+        raise SystemExit(__doc__)
+    from unified_video_action_amd.native.lib import use_library
+    use_library(sys.argv[1])
+    script = sys.argv[2]
+    sys.argv = sys.argv[2:]
+    sys.path.insert(0, os.path.dirname(os.path.abspath(script)))
+    runpy.run_path(script, run_name="__main__")

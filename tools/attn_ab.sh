@@ -1,5 +1,5 @@
 # attention dev loop: correctness tests of the in-tree build, then the attention micro-bench on the
-# in-tree build and on ab/libuva_base.so (same box)
+# in-tree build and on abx/libuva_base.so (same box)
 set -o pipefail
 mkdir -p gpurun_out
 export TMPDIR=/tmp
@@ -8,7 +8,7 @@ rc=$?
 tail -15 gpurun_out/attn_t.log
 [ $rc -eq 0 ] || exit 1
 for L in new base; do
-  if [ $L = base ]; then export UVA_LIB_PATH=$PWD/ab/libuva_base.so; else unset UVA_LIB_PATH; fi
+  if [ $L = base ]; then PY="python tools/ab_run.py abx/libuva_base.so"; else PY=python; fi
   echo "== $L"
-  timeout -k 10 120 python tools/tools_kbench.py attn 2>&1 | grep -v amdgpu.ids || exit 1
+  timeout -k 10 120 $PY tools/tools_kbench.py attn 2>&1 | grep -v amdgpu.ids || exit 1
 done

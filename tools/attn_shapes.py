@@ -1,4 +1,4 @@
-"""Attention forward / backward times over (B, N) shapes at p = 0.1 (same-box A/B with UVA_LIB_PATH)."""
+"""Attention forward / backward times over (B, N) shapes at p = 0.1 (same-box A/B: tools/ab_run.py)."""
 import sys
 import torch
 sys.path.insert(0, ".")

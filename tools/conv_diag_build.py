@@ -1,5 +1,5 @@
 """Diagnostic builds of the GN halo conv (timing only; results are WRONG by construction): each
-variant patches a copy of csrc/conv.hip, compiles it, and links ab/diag_<name>.so from the in-tree
+variant patches a copy of csrc/conv.hip, compiles it, and links abx/diag_<name>.so from the in-tree
 objects with conv.o replaced.  Run the timings with tools/conv_diag.sh on the GPU box."""
 import os
 import subprocess
@@ -8,7 +8,7 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 CSRC = os.path.join(ROOT, "unified_video_action_amd", "csrc")
 OBJ = os.path.join(ROOT, "unified_video_action_amd", "build_obj")
-AB = os.path.join(ROOT, "ab")
+AB = os.path.join(ROOT, "abx")
 FLAGS = ["--offload-arch=gfx950", "-O3", "-fPIC", "-std=c++17", "-munsafe-fp-atomics", "-Wno-unused-result",
          "-I" + CSRC] + os.environ.get("DIAG_FLAGS", "").split()
 

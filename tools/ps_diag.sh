@@ -1,7 +1,7 @@
-# time the B=1 sampler (tools_infer_bench.py) on every ab/diag_*.so build (tools/conv_diag_build.py ps_* variants)
+# time the B=1 sampler (tools_infer_bench.py) on every abx/diag_*.so build (tools/conv_diag_build.py ps_* variants)
 set -o pipefail
 export TMPDIR=/tmp
-for L in ab/diag_*.so; do
+for L in abx/diag_*.so; do
   echo "== $L"
-  UVA_LIB_PATH=$PWD/$L timeout -k 10 120 python tools/tools_infer_bench.py --batches 1 --iters 10 2>&1 | grep -v amdgpu.ids || exit 1
+  timeout -k 10 120 python tools/ab_run.py $L tools/tools_infer_bench.py --batches 1 --iters 10 2>&1 | grep -v amdgpu.ids || exit 1
 done

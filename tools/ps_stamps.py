@@ -1,5 +1,5 @@
 """Phase timeline of the persistent sampler from the ps_stamps diagnostic build (tools/conv_diag_build.py
-ps_stamps; UVA_LIB_PATH=ab/diag_ps_stamps.so python tools/ps_stamps.py): s_memtime deltas (shader cycles)
+ps_stamps; python tools/ab_run.py abx/diag_ps_stamps.so tools/ps_stamps.py): s_memtime deltas (shader cycles)
 of workgroup 0 at step 50."""
 import sys
 import torch

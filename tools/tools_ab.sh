@@ -1,7 +1,7 @@
 #!/bin/bash
 # Same-box A/B of an env switch on the full bench: bash tools/tools_ab.sh VAR "A B" [rounds]
 # prints value per run, alternating A, B, A, B ... (box-to-box variance is ~2-5 %, larger than
-# most single changes).  VAR=UVA_LIB_PATH compares two builds of the library.
+# most single changes).  Two builds of the library: tools/ab_bench.sh.
 VAR=$1; VALS=$2; R=${3:-2}
 for r in $(seq $R); do for v in $VALS; do
   tag=$(echo "$v" | tr '/.' '__')

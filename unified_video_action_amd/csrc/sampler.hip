@@ -275,6 +275,7 @@ struct PSParams {
   unsigned* err;       // give-up flag
   int R, C, depth, S, clip;
   float eps;
+  int no_publish;  // test hook only (uva_sampler_persistent_test_hook): no phase is ever published
 };
 
 // wave sum by DPP (quad perms, row rotates) and two lane swaps: six VALU steps of a few cycles each,
@@ -291,9 +292,10 @@ __device__ __forceinline__ float wave_sum_dpp(float v) {
   return __uint_as_float(r[0]) + __uint_as_float(r[1]);
 }
 
-__device__ __forceinline__ void ps_publish(unsigned* cnt) {
+__device__ __forceinline__ void ps_publish(unsigned* cnt, int no_publish) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the storing wave's sc1 stores have left
-  if ((threadIdx.x & 63) == 0) __hip_atomic_fetch_add((gu32*)cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if ((threadIdx.x & 63) == 0 && !no_publish)
+    __hip_atomic_fetch_add((gu32*)cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 __device__ __forceinline__ void ps_wait(unsigned* cnt, unsigned target, unsigned* err) {
@@ -518,7 +520,7 @@ __global__ __launch_bounds__(256, 1) void sampler_persistent_kernel(PSParams p) 
           __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4v, o), rs_ha, (row * W + col0 + c8) * 2, 0,
                                                  PS_SC1);
         }
-        ps_publish(p.cnt + 2 * blk);
+        ps_publish(p.cnt + 2 * blk, p.no_publish);
       }
       // ---- fc2: h' = h + gate * (a W2^T + b2), my 16 columns
       if (blk + 1 < D) {
@@ -564,7 +566,7 @@ __global__ __launch_bounds__(256, 1) void sampler_persistent_kernel(PSParams p) 
         const int row = l >> 2, c4 = (l & 3) * 4;
         const u32x4v o = *(const u32x4v*)(sT + row * 16 + c4);
         __builtin_amdgcn_raw_buffer_store_b128(o, rs_hx, (((blk & 1) * PS_R + row) * W + col0 + c4) * 4, 0, PS_SC1);
-        ps_publish(p.cnt + 2 * blk + 1);
+        ps_publish(p.cnt + 2 * blk + 1, p.no_publish);
       }
     }
     // ---- final layer (every workgroup): out = modulate(LN(h)) Wf^T + bf, N = 2C <= 32
@@ -614,11 +616,22 @@ __global__ __launch_bounds__(256, 1) void sampler_persistent_kernel(PSParams p) 
     }
   }
   if (blockIdx.x == 0) {
+    // a run in which any wait gave up (some workgroup computed on a stale exchange buffer) returns
+    // NaN, never plausible-looking actions; the host also reads the flag (sampler.py)
+    const bool bad = __hip_atomic_load((gu32*)p.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u;
     const int r = tid >> 4, c = tid & 15;
-    if (r < R && c < C) p.x_out[r * C + c] = sX[tid];
+    if (r < R && c < C) p.x_out[r * C + c] = bad ? __builtin_nanf("") : sX[tid];
   }
 }
 }  // namespace
+
+// test hook: the NEXT uva_sampler_persistent launch publishes no phase, so every hand-off wait runs
+// into its spin bound -> the give-up path (flag set, NaN output) is exercised deterministically
+static int ps_test_no_publish = 0;
+extern "C" int uva_sampler_persistent_test_hook(int no_publish) {
+  ps_test_no_publish = no_publish ? 1 : 0;
+  return 0;
+}
 
 extern "C" long long uva_sampler_persistent_workspace(int W) {
   return 256 + 2LL * PS_R * W * 4 + (long long)PS_R * W * 2;
@@ -664,6 +677,8 @@ extern "C" int uva_sampler_persistent(int R, int C, int W, int depth, int S, int
   p.S = S;
   p.clip = clip;
   p.eps = eps;
+  p.no_publish = ps_test_no_publish;
+  ps_test_no_publish = 0;  // one launch only
   // > 80 KB of LDS: one workgroup per CU (the hand-off's measured form), 64 of 256 CUs
   constexpr int kLds = 96 * 1024;
   static bool attr = false;

@@ -20,6 +20,8 @@ MI355X layout of one sampling call over R = B*16 action rows and S spaced steps:
 No autograd and no backward residues (the training trunk's aux tensors) are produced.
 """
 
+import warnings
+
 import torch
 
 from ...native import ops
@@ -188,7 +190,8 @@ class ActionSampler:
                   out=torch.empty(R, 2 * C, dtype=F32, device=dev), graph=None,
                   fused=self.use_fused and cd == torch.bfloat16 and W in (256, 512, 1024) and R <= self.FUSED_MAX_ROWS)
         st["persist"] = (self.use_persistent and st["fused"] and st["mod"] is not None and R <= 16 and W == 1024
-                         and len(blocks) == 6 and C <= 16 and dev.type == "cuda")
+                         and len(blocks) == 6 and C <= 16 and dev.type == "cuda"
+                         and ops.sampler_persistent_fits(dev))
         if st["persist"]:
             # weights stacked per kind (one base pointer each), coefficient table [S, 8] on the device
             st["pack"] = dict(
@@ -223,7 +226,16 @@ class ActionSampler:
         if st["persist"]:
             ops.sampler_persistent(st["pack"], st["mod"], st["coef"], step_noise.contiguous(), noise.contiguous(),
                                    st["xo"], st["work"], clip=self.clip)
-            return st["xo"].clone()
+            # the launch relies on its 64 workgroups being co-resident; if any hand-off wait ran into
+            # its spin bound (CUs held by other streams, a partitioned device) the kernel wrote NaN and
+            # set the flag: recompute this call on the captured-graph route and stop using the
+            # persistent kernel for this state (one 4-byte read, ~tens of us at B = 1)
+            if ops.sampler_persistent_status(st["work"]) == 0:
+                return st["xo"].clone()
+            warnings.warn("persistent action sampler gave up on a hand-off (workgroups not co-resident); "
+                          "recomputing on the captured-graph route", RuntimeWarning)
+            st["persist"] = False
+            self.persistent_giveups = getattr(self, "persistent_giveups", 0) + 1
         st["x"].copy_(noise)
         st["x_net"].copy_(noise)
         st["noise"].copy_(step_noise)

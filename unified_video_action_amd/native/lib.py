@@ -4,11 +4,13 @@ missing or a symbol is absent, import of the product path fails loudly."""
 import ctypes
 import os
 import re
+import sys
 
 _PKG = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 _ROOT = os.path.dirname(_PKG)
-# UVA_LIB_PATH: an alternative build of this library (same-box A/B of two builds, tools_ab.sh)
-LIB_PATH = os.environ.get("UVA_LIB_PATH") or os.path.join(_PKG, "libuva_hip.so")
+# the product library; nothing in the environment can replace it (A/B runs of another build go
+# through tools/ab_run.py, which calls use_library() before the first load)
+LIB_PATH = os.path.join(_PKG, "libuva_hip.so")
 HEADER = os.path.join(_ROOT, "include", "uva_hip.h")
 
 _CTYPE = {
@@ -38,21 +40,26 @@ def parse_header(path=HEADER):
 
 
 class UvaLib:
-    def __init__(self, path=LIB_PATH):
+    def __init__(self, path=LIB_PATH, allow_missing=False):
         if not os.path.exists(path):
             raise RuntimeError(
                 f"libuva_hip.so not found at {path}: run __graft_entry__.build() (hipcc gfx950). "
                 "There is no CPU fallback on the product path.")
+        self.path = path
         self._lib = ctypes.CDLL(path)
         self.sigs = parse_header()
-        ab = bool(os.environ.get("UVA_LIB_PATH"))
+        self.unbound = []
         for name, (res, args) in self.sigs.items():
-            if ab and not hasattr(self._lib, name):
-                continue  # an older A/B build: entry points it predates stay unbound (calling one raises)
+            if allow_missing and not hasattr(self._lib, name):
+                self.unbound.append(name)  # an older A/B build: calling one of these raises
+                continue
             fn = getattr(self._lib, name)  # AttributeError = missing export -> loud
             fn.restype = res
             fn.argtypes = args
             setattr(self, "_" + name, fn)
+        if self.unbound:
+            print(f"[uva] {path}: {len(self.unbound)} entry points of include/uva_hip.h not exported "
+                  f"(older build): {', '.join(self.unbound)}", file=sys.stderr, flush=True)
 
     def call(self, name, *args):
         rc = getattr(self, "_" + name)(*args)
@@ -71,4 +78,15 @@ def lib():
     global _LIB
     if _LIB is None:
         _LIB = UvaLib()
+    return _LIB
+
+
+def use_library(path):
+    """tools only (tools/ab_run.py): bind another build of the library for a same-box A/B run.
+    Must run before the first lib() call; entry points the older build lacks stay unbound and are
+    listed once on stderr."""
+    global _LIB
+    if _LIB is not None:
+        raise RuntimeError(f"use_library({path}): {_LIB.path} is already loaded")
+    _LIB = UvaLib(os.path.abspath(path), allow_missing=True)
     return _LIB

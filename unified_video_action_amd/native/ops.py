@@ -266,6 +266,21 @@ def sampler_persistent(pack, mod, coef, noise, x0, x_out, work, clip=True, eps=1
                ptr(x0), ptr(x_out), ptr(work), work.numel(), stream())
 
 
+def sampler_persistent_test_hook(no_publish=True):
+    """tests only: the next uva_sampler_persistent launch publishes no phase (forces the give-up path)."""
+    lib().call("uva_sampler_persistent_test_hook", int(bool(no_publish)))
+
+
+PERSISTENT_SAMPLER_CUS = 64  # workgroups of uva_sampler_persistent, one per CU, all co-resident
+
+
+def sampler_persistent_fits(device):
+    """the persistent sampler's 64 workgroups (96 KB of LDS each: one per CU) can all be resident at
+    once on `device` -- False on a partitioned device with fewer CUs, where every hand-off would spin
+    into its bound."""
+    return torch.cuda.get_device_properties(device).multi_processor_count >= PERSISTENT_SAMPLER_CUS
+
+
 def sampler_persistent_workspace(W, device):
     return torch.empty(lib().query("uva_sampler_persistent_workspace", W), dtype=torch.uint8, device=device)
 
