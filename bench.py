@@ -144,6 +144,7 @@ def build(config, precision, device):
     presets.fit_normalizer(config, pol)
     ema_model = copy.deepcopy(pol)  # workspace:70-72 (before get_optimizer, as the reference)
     opt = pol.get_optimizer(weight_decay=0.02, learning_rate=1e-4, betas=(0.9, 0.95))
+    opt.overlap_tail = True  # step() follows backward directly: the DP tail reduces under AdamW
     pol.to(device).train()
     ema_model.to(device)
     sched = get_scheduler("cosine", opt, num_warmup_steps=1000, num_training_steps=100000)

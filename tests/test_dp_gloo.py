@@ -2,11 +2,14 @@
   * the real policy (mar_base, PushT joint, fp32): get_optimizer's flat layout + default_buckets
     cover every trainable parameter exactly once (buckets + tail), every Block / diffusion trunk
     carries its bucket hook, and the reducer is created lazily once the process group exists; the
-    26 real hooks fired in reverse order from inside a backward pass issue ONE collective each (the
-    no-decay ranges reduce in the tail) and the reduced flat gradient equals the sum over ranks;
+    26 real hooks fired in reverse order from inside a backward pass issue one collective per large
+    range (the heads' remaining parameters with the last decoder Block, the decoder prelude with the
+    last encoder Block; the small no-decay ranges merged into a few), the tail is only the encoder
+    input side, and the reduced flat gradient equals the sum over ranks;
   * the reducer protocol on a small torch model: async per-bucket launches from backward, the
-    end-of-backward completion callback, the tail bucket, 1/world averaging -- equal to a
-    single-process run on the concatenated batch."""
+    end-of-backward completion callback, the tail bucket (also deferred to the optimizer's
+    wait_tail), 1/world averaging -- equal to a single-process run on the concatenated batch;
+  * the optimizer's AdamW split around a deferred tail tiles every group region once."""
 import os
 import socket
 
@@ -60,7 +63,7 @@ def _named_groups(m):
     return [[x for x in named if is_no_decay(*x)], [x for x in named if not is_no_decay(*x)]]
 
 
-def _tiny_worker(rank, world, port, q):
+def _tiny_worker(rank, world, port, q, defer=False):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     from unified_video_action_amd.runtime import RT
@@ -75,6 +78,7 @@ def _tiny_worker(rank, world, port, q):
     assert int(red.coverage().min()) == 1 and int(red.coverage().max()) == 1
     g = torch.Generator().manual_seed(123)
     x = torch.randn(8, 4, generator=g)[rank * 4:(rank + 1) * 4]
+    red.defer_tail = defer
     red.arm()
 
     # launch each block's bucket from inside backward, after its parameter grads are accumulated
@@ -87,6 +91,10 @@ def _tiny_worker(rank, world, port, q):
     handles = [b[0].weight.register_post_accumulate_grad_hook(post_hook(b)) for b in m.blocks]
     m(x).backward()  # the queued end-of-backward callback completes the reduction
     assert not red.pending and not red.handles
+    if defer:  # the tail's collectives are left in flight for the optimizer (wait_tail)
+        assert len(red.tail_handles) == len(red.tail) > 0
+        red.wait_tail()
+    assert not red.tail_handles
     for h in handles:
         h.remove()
     q.put((rank, (store.grad / world).clone()))
@@ -94,11 +102,12 @@ def _tiny_worker(rank, world, port, q):
 
 
 @pytest.mark.timeout(120)
-def test_grad_reducer_world2_matches_single_process():
+@pytest.mark.parametrize("defer", [False, True])
+def test_grad_reducer_world2_matches_single_process(defer):
     world, port = 2, _free_port()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    procs = [ctx.Process(target=_tiny_worker, args=(r, world, port, q)) for r in range(world)]
+    procs = [ctx.Process(target=_tiny_worker, args=(r, world, port, q, defer)) for r in range(world)]
     for p in procs:
         p.start()
     res = dict(q.get(timeout=100) for _ in range(world))
@@ -175,7 +184,7 @@ def _policy_worker(rank, world, port, q):
     q.put((rank, int(cov[inside].min()), int(cov[inside].max()), int(cov.max()), st.n_params, n_trainable,
            len(hooked), sum(callable(getattr(m, "_uva_bucket_hook", None)) for m in hooked), opt.grad_scale,
            len(red.buckets), ok, len(calls), len(red.tail), sum(len(b) for b in red.buckets), n_bucket_calls,
-           red.pending))
+           red.pending, sum(k for _, k in red.tail)))
     dist.destroy_process_group()
 
 
@@ -191,14 +200,19 @@ def test_mar_base_buckets_cover_every_param_once():
     for p in procs:
         p.join(timeout=30)
     for (rank, cmin, cmax, call, n_store, n_train, n_hooked, n_with_hook, scale, n_buckets, ok, n_calls, n_tail,
-         n_ranges, n_bucket_calls, pending) in res:
+         n_ranges, n_bucket_calls, pending, tail_elems) in res:
         assert cmin == 1 and cmax == 1 and call == 1, (cmin, cmax, call)
         assert n_store == n_train == 261_079_156, n_store  # PushT joint MAR
-        assert n_hooked == 26 and n_with_hook == 26 and n_buckets == 26  # 24 Blocks + 2 diffusion trunks
+        # 24 Blocks + 2 diffusion trunks, + the heads' remaining params (time / cond embeddings,
+        # input_proj, the conv_fc trunk) fired by the last decoder Block, + the decoder prelude fired
+        # by the last encoder Block
+        assert n_hooked == 26 and n_with_hook == 26 and n_buckets == 28
         assert scale == 0.5
         assert ok, "reduced flat gradient != sum over ranks"
-        assert n_ranges == 26 and n_bucket_calls >= 26, (n_ranges, n_bucket_calls)  # one collective per bucket
-        assert n_calls == 26 + n_tail and n_tail <= 4, (n_calls, n_tail)  # + the few contiguous tail ranges
+        assert n_ranges >= 28 and n_bucket_calls >= n_ranges, (n_ranges, n_bucket_calls)
+        assert tail_elems < 2_100_000, tail_elems  # only the encoder input side (~8 MB) after backward
+        # + the small no-decay ranges, merged with their neighbours into a handful of collectives
+        assert n_tail <= 4 and 1 <= n_calls - n_ranges - n_tail <= 8, (n_calls, n_ranges, n_tail)
         assert not pending
 
 
@@ -238,3 +252,23 @@ def test_bench_under_torchrun_sees_the_launcher_world():
     assert r.returncode == 0, r.stderr[-2000:]
     lines = [json.loads(ln) for ln in r.stdout.splitlines() if ln.startswith("{")]
     assert lines == [{"launch_check": True, "world": 2, "gpus": 2, "rank_sum": 1.0}]
+
+
+def test_adamw_tail_segments_split():
+    """the optimizer's two AdamW phases under a deferred tail: the widened (16-B aligned) tail
+    segments and their complement tile every group region exactly once, every piece 16-B aligned."""
+    from unified_video_action_amd.workspace.optim import GradReducer, _segments
+    red = GradReducer.__new__(GradReducer)
+    red.tail = [(5, 3), (9, 20), (101, 2), (300, 77)]
+    segs = red.tail_segments()
+    assert segs == [(4, 28), (100, 4), (300, 80)]
+    for off, n in [(0, 64), (96, 256), (380, 1000)]:
+        cnt = torch.zeros(off + n, dtype=torch.int32)
+        for ph in (0, 1):
+            for o, k in _segments(off, n, segs, ph):
+                assert o % 4 == 0 and k > 0
+                cnt[o:o + k] += 1
+        assert bool((cnt[off:] == 1).all()) and int(cnt[:off].sum()) == 0
+        assert _segments(off, n, segs, None) == [(off, n)]
+    for o, k in red.tail:  # every tail element is in a phase-1 piece
+        assert any(a <= o and o + k <= a + b for a, b in segs)

@@ -119,8 +119,9 @@ class ParamStore:
             ops.cast(self.flat, self.shadow)
 
     def ranges_of(self, module):
-        """[(off, len)] covering the module's params, merged per group."""
-        rs = sorted(self.offsets[id(p)] for p in module.parameters() if id(p) in self.offsets)
+        """[(off, len)] covering the params of a module (or of an iterable of parameters), merged."""
+        params = module.parameters() if hasattr(module, "parameters") else module
+        rs = sorted(self.offsets[id(p)] for p in params if id(p) in self.offsets)
         merged = []
         for o, k in rs:
             if merged and merged[-1][0] + merged[-1][1] == o:
@@ -183,6 +184,8 @@ class FusedAdamWEMA(torch.optim.Optimizer):
         """zeroes the flat gradient buffer; gradients stay views of it (set_to_none is ignored:
         a None grad would break the flat layout the fused kernels write into)."""
         self._sync()
+        if self.reducer is not None:
+            self.reducer.wait_tail()  # never zero under an in-flight all-reduce
         self.store.zero_grad()
 
     @torch.no_grad()
@@ -198,19 +201,42 @@ class FusedAdamWEMA(torch.optim.Optimizer):
         ema = self.attached_ema()
         d = ema.get_decay(ema.optimization_step) if ema is not None else 0.0
         st = self.store
-        for g, (off, n) in zip(self.param_groups, st.group_ranges):
-            if n == 0:
-                continue
-            b1, b2 = g["betas"]
-            sl = slice(off, off + n)
-            ops.adamw_ema(st.flat[sl], st.grad[sl], self.m[sl], self.v[sl],
-                          ema.flat[sl] if ema is not None else None,
-                          st.shadow[sl] if st.shadow is not None else None, n if g["weight_decay"] else 0,
-                          g["lr"], b1, b2, g["eps"], g["weight_decay"], self.step_count, self.grad_scale, d)
+        red = self.reducer
+        late = red.tail_segments() if (red is not None and red.tail_handles) else []
+        # a deferred DP tail (GradReducer.defer_tail): AdamW runs over everything else first, under
+        # the tail's all-reduce, then over the tail once it has landed
+        for phase in ((0, 1) if late else (None,)):
+            if phase == 1:
+                red.wait_tail()
+            for g, (off, n) in zip(self.param_groups, st.group_ranges):
+                if n == 0:
+                    continue
+                for o, k in _segments(off, n, late, phase):
+                    self._adamw(g, o, k, ema, d)
         if ema is not None:
             ema.mark_fused(self.step_count)
         RT.bump_params()
         return loss
+
+    def _adamw(self, g, o, k, ema, d):
+        st = self.store
+        b1, b2 = g["betas"]
+        sl = slice(o, o + k)
+        ops.adamw_ema(st.flat[sl], st.grad[sl], self.m[sl], self.v[sl], ema.flat[sl] if ema is not None else None,
+                      st.shadow[sl] if st.shadow is not None else None, k if g["weight_decay"] else 0,
+                      g["lr"], b1, b2, g["eps"], g["weight_decay"], self.step_count, self.grad_scale, d)
+
+    @property
+    def overlap_tail(self):
+        return getattr(self, "_overlap_tail", False)
+
+    @overlap_tail.setter
+    def overlap_tail(self, on):
+        """True: the loop calls step() right after backward with no gradient reader in between (the
+        workspace, bench.py), so the DP tail's all-reduce may run under the AdamW of the rest."""
+        self._overlap_tail = bool(on)
+        if self.reducer is not None:
+            self.reducer.defer_tail = self._overlap_tail
 
     # ---- EMA fusion ------------------------------------------------------------------------
     def attach_ema(self, ema):
@@ -231,6 +257,7 @@ class FusedAdamWEMA(torch.optim.Optimizer):
         world = dist.get_world_size()
         if world > 1:
             self.reducer = GradReducer(self.store, default_buckets(model))
+            self.reducer.defer_tail = self.overlap_tail
             self.grad_scale = 1.0 / world
         return self.reducer
 
@@ -283,10 +310,58 @@ class FusedAdamWEMA(torch.optim.Optimizer):
                     mine[k] = tuple(theirs[k]) if k == "betas" else theirs[k]
 
 
+def _segments(off, n, late, phase):
+    """[off, off + n) split for the two AdamW phases: phase 0 = everything outside the `late`
+    segments, phase 1 = inside them, None = all.  `late` is sorted, 16-B aligned (GradReducer.
+    tail_segments), so every piece starts 16-B aligned as the AdamW kernel requires."""
+    if phase is None:
+        return [(off, n)]
+    end, out, pos = off + n, [], off
+    for o, k in late:
+        a, b = max(o, off), min(o + k, end)
+        if a >= b:
+            continue
+        if phase == 0 and a > pos:
+            out.append((pos, a - pos))
+        if phase == 1:
+            out.append((a, b - a))
+        pos = b
+    if phase == 0 and pos < end:
+        out.append((pos, end - pos))
+    return out
+
+
+def _params(*objs):
+    out = []
+    for o in objs:
+        if o is None:
+            continue
+        if isinstance(o, torch.nn.Parameter):
+            out.append(o)
+        else:
+            out.extend(o.parameters())
+    return out
+
+
 def default_buckets(model):
-    """one bucket per transformer Block and per diffusion-MLP trunk (backward order = reverse)."""
+    """DP buckets in backward order: [(parameters (a module or a list), module whose fused backward
+    fires the hook)].
+
+    * one per transformer Block and per diffusion-MLP trunk (their fused backwards fire them);
+    * the diffusion heads' remaining parameters (each head's time / cond embeddings and input_proj,
+      the conv_fc trunk of every DiffActLoss: conv, fc, interpolate, refine) + the decoder-output
+      embeddings + decoder_norm: all of them have had their gradients enqueued before the LAST
+      decoder Block's backward starts (its input gradient depends on every head's trunk through
+      decoder_norm; the embedding branches are autograd leaves with higher sequence numbers, which
+      the engine runs first), so that Block's hook launches them too -- 60-140 MB reduced under the
+      remaining 23 Blocks instead of after backward;
+    * decoder_embed + the decoder input embeddings + encoder_norm: enqueued before the LAST encoder
+      Block's backward, launched by its hook.
+    What remains for the tail is the encoder input side (z / action / text projections,
+    proj_cond_x_layer, the encoder embeddings: ~2-3 M parameters), whose backward is the last work."""
     import torch.nn as nn
-    from ..model.autoregressive.diffusion_loss import SimpleMLPAdaLN
+    from ..model.autoregressive.diffusion_action_loss import DiffActLoss
+    from ..model.autoregressive.diffusion_loss import DiffLoss, SimpleMLPAdaLN
     from ..model.autoregressive.mar_con_unified import Block
     out = []
     for m in model.modules():
@@ -294,6 +369,23 @@ def default_buckets(model):
             out.append((m, m))
         elif isinstance(m, SimpleMLPAdaLN):
             out.append((nn.ModuleList([m.res_blocks, m.final_layer]), m))
+    dec = getattr(model, "decoder_blocks", None)
+    enc = getattr(model, "encoder_blocks", None)
+    if dec is not None and len(dec) and enc is not None and len(enc):
+        heads = [h for h in model.modules() if isinstance(h, (DiffLoss, DiffActLoss))]
+        extra = []
+        for h in heads:
+            net = h.net
+            extra += _params(net.time_embed, net.cond_embed, net.input_proj)
+            if isinstance(h, DiffActLoss):
+                extra += _params(h.conv, h.fc, h.interpolate, h.refine)
+        extra += _params(getattr(model, "diffusion_temporal_embed", None),
+                         getattr(model, "diffusion_spatial_embed", None), getattr(model, "decoder_norm", None))
+        out.append((extra, dec[-1]))
+        prelude = _params(getattr(model, "decoder_embed", None), getattr(model, "decoder_temporal_pos_embed", None),
+                          getattr(model, "decoder_spatial_pos_embed", None),
+                          getattr(model, "decoder_text_pos_embed", None), getattr(model, "encoder_norm", None))
+        out.append((prelude, enc[-1]))
     return out
 
 
@@ -318,16 +410,25 @@ class GradReducer:
         self.pending = False
         self._queued = False
         covered = []
+        self.small = []  # per bucket: its ranges below MIN_BUCKET_ELEMS (coalesced across buckets)
+        by_owner = {}
         for i, (m, owner) in enumerate(buckets):
-            # one collective per bucket: a module's params sit in two group regions of the flat
-            # buffer (weight decay, then none); its small no-decay range (LayerNorm / bias, ~40 KB
-            # per Block) goes to the tail, where the no-decay ranges of all modules are contiguous
-            # and reduce as ONE collective after backward
-            rs = [r for r in store.ranges_of(m) if r[1] >= self.MIN_BUCKET_ELEMS]
-            self.buckets.append(rs)
+            # a module's params sit in two group regions of the flat buffer (weight decay, then
+            # none): the large range(s) reduce as one collective each when the hook fires; the small
+            # no-decay ranges (LayerNorm / bias, ~40 KB per Block) are held and merged with their
+            # neighbours from the buckets that fire next (consecutive Blocks' no-decay ranges are
+            # adjacent), then reduced as one collective once the merged run is large enough
+            rs = store.ranges_of(m)
+            self.buckets.append([r for r in rs if r[1] >= self.MIN_BUCKET_ELEMS])
+            self.small.append([r for r in rs if r[1] < self.MIN_BUCKET_ELEMS])
             covered += rs
-            if self.world > 1:
-                owner._uva_bucket_hook = (lambda i=i: self.launch(i))
+            by_owner.setdefault(id(owner), (owner, []))[1].append(i)
+        if self.world > 1:
+            for owner, idx in by_owner.values():
+                owner._uva_bucket_hook = (lambda idx=tuple(idx): [self.launch(i) for i in idx])
+        self.held = []  # small ranges of launched buckets, not yet reduced
+        self.defer_tail = False  # finish() leaves the tail's handles to wait_tail() (the optimizer)
+        self.tail_handles = []
         # complement of all hooked ranges -> the tail bucket (reduced at the end of backward)
         covered.sort()
         tail, pos = [], 0
@@ -339,10 +440,27 @@ class GradReducer:
             tail.append((pos, store.total - pos))
         self.tail = tail
 
+    def wait_tail(self):
+        for h in self.tail_handles:
+            h.wait()
+        self.tail_handles = []
+
+    def tail_segments(self):
+        """the tail ranges widened to 4-element (16-B) boundaries, merged: the AdamW pieces that must
+        wait for the tail's all-reduce (a widened edge only delays a few reduced elements)."""
+        segs = []
+        for o, k in sorted(self.tail):
+            a, b = o // 4 * 4, (o + k + 3) // 4 * 4
+            if segs and a <= segs[-1][1]:
+                segs[-1][1] = max(segs[-1][1], b)
+            else:
+                segs.append([a, b])
+        return [(a, b - a) for a, b in segs]
+
     def coverage(self):
         """per flat element: in how many reduced ranges it lies (must be exactly 1 everywhere)."""
         cnt = torch.zeros(self.store.total, dtype=torch.int32)
-        for rs in self.buckets + [self.tail]:
+        for rs in self.buckets + self.small + [self.tail]:
             for o, k in rs:
                 cnt[o:o + k] += 1
         return cnt
@@ -351,13 +469,35 @@ class GradReducer:
         """a forward pass ran: the next finish() must reduce (even if no bucket hook fires)."""
         self.pending = self.world > 1
 
-    def _launch(self, i):
+    def _launch(self, i, flush=False):
         if i in self.done:
             return
         self.done.add(i)
         grad = self.store.grad
         for o, k in self.buckets[i]:
             self.handles.append(dist.all_reduce(grad[o:o + k], group=self.group, async_op=True))
+        self.held += self.small[i]
+        self._flush_held(flush)
+
+    def _flush_held(self, force):
+        """merge adjacent held small ranges; reduce every merged run that reached MIN_BUCKET_ELEMS
+        (all of them when force)."""
+        if not self.held:
+            return
+        runs = []
+        for o, k in sorted(self.held):
+            if runs and runs[-1][0] + runs[-1][1] == o:
+                runs[-1] = (runs[-1][0], runs[-1][1] + k)
+            else:
+                runs.append((o, k))
+        grad = self.store.grad
+        keep = []
+        for o, k in runs:
+            if force or k >= self.MIN_BUCKET_ELEMS:
+                self.handles.append(dist.all_reduce(grad[o:o + k], group=self.group, async_op=True))
+            else:
+                keep.append((o, k))
+        self.held = keep
 
     def launch(self, i):
         """bucket hook, called by a fused backward once all of bucket i's gradients are enqueued."""
@@ -373,13 +513,18 @@ class GradReducer:
     def finish(self):
         """reduce what is left, then make the compute stream wait (no-op when already done)."""
         self._queued = False
+        self.wait_tail()  # a deferred tail nobody stepped on (backward twice without step)
         if not self.pending:
             return
         for i in range(len(self.buckets)):
             self._launch(i)
+        self._flush_held(True)
         grad = self.store.grad
-        for o, k in self.tail:
-            self.handles.append(dist.all_reduce(grad[o:o + k], group=self.group, async_op=True))
+        tail = [dist.all_reduce(grad[o:o + k], group=self.group, async_op=True) for o, k in self.tail]
+        if self.defer_tail:
+            self.tail_handles = tail
+        else:
+            self.handles += tail
         for h in self.handles:
             h.wait()
         self.handles = []

@@ -163,6 +163,10 @@ class TrainUnifiedVideoActionWorkspace(BaseWorkspace):
                                    language_emb_model=language_emb_model)
         self.ema_model = copy.deepcopy(self.model) if cfg.training.use_ema else None
         self.optimizer = self.model.get_optimizer(**cfg.model.policy.optimizer)
+        # train_step calls optimizer.step() right after backward (no gradient reader between): the
+        # DP tail all-reduce may overlap the AdamW of the already-reduced buckets
+        if hasattr(self.optimizer, "overlap_tail"):
+            self.optimizer.overlap_tail = True
         self.global_step = 0
         self.epoch = 0
 
