@@ -68,7 +68,7 @@ def parse(argv=None):
     ap.add_argument("--cpu-batch", type=int, default=2, help="CPU baseline batch (BASELINE configs[0]: 2)")
     ap.add_argument("--cpu-warmup", type=int, default=5, help="CPU warm-up steps (BASELINE.md §4: 5)")
     ap.add_argument("--cpu-steps", type=int, default=10, help="timed CPU steps, median reported (BASELINE.md §4: 10)")
-    ap.add_argument("--cpu-budget-s", type=float, default=150.0,
+    ap.add_argument("--cpu-budget-s", type=float, default=120.0,
                     help="wall budget of the B=2 leg: fewer timed steps (stated in `sample`) when a step is slow")
     ap.add_argument("--no-trace", action="store_true")
     ap.add_argument("--trace-steps", type=int, default=3)
@@ -291,10 +291,13 @@ def cpu_baseline(args):
         loss.backward()
         opt.step()
         opt.zero_grad()
-        return time.perf_counter() - t0
+        dt = time.perf_counter() - t0
+        print(f"[bench] cpu_baseline B={B} step {dt:.1f} s", file=sys.stderr, flush=True)
+        return dt
 
     B = args.cpu_batch
     t_start = time.perf_counter()
+    hb = _heartbeat("cpu_baseline")
     warm = [one(B)]
     nwarm, nsteps = args.cpu_warmup, args.cpu_steps
     if warm[0] * (nwarm + nsteps) > args.cpu_budget_s:  # keep the default bench within minutes
@@ -316,7 +319,23 @@ def cpu_baseline(args):
         t = one(args.batch)  # the warm-ups above already paged in the weights and kernels
         out["per_gpu_batch"] = {"batch": args.batch, "value": round(args.batch / t, 5), "unit": "samples/s",
                                 "sample": f"one step at B={args.batch} after the B={B} runs ({t:.1f} s)"}
+    hb.set()
     return out
+
+
+def _heartbeat(what, every=45.0):
+    """a progress line on stderr every `every` s until the returned event is set (a single CPU step at
+    the per-GPU batch runs for minutes; a silent process is taken for a hung one)"""
+    import threading
+    ev = threading.Event()
+    t0 = time.perf_counter()
+
+    def beat():
+        while not ev.wait(every):
+            print(f"[bench] {what}: {time.perf_counter() - t0:.0f} s", file=sys.stderr, flush=True)
+
+    threading.Thread(target=beat, daemon=True).start()
+    return ev
 
 
 def host_cpus():
@@ -396,6 +415,9 @@ def run(args):
     from unified_video_action_amd.native import ops
     elapsed, per_step, loss, state = timed_run(args.config, args.batch, args.steps, args.warmup, args.precision,
                                                device, world, rank)
+    if rank == 0:
+        print(f"[bench] {args.config} B={args.batch}: {args.batch * world * args.steps / elapsed:.2f} samples/s",
+              file=sys.stderr, flush=True)
     main = line_for(args.config, args.batch, world, args.steps, elapsed, per_step, loss)
     rows = None
     if not args.no_trace:  # separate short traced pass for the roofline (HIP events per launch)
@@ -419,6 +441,7 @@ def run(args):
             del st
             others.append(dict(line_for(cfg, b, world, args.other_steps, e, ps, lo), steps=args.other_steps,
                                precision=prec))
+            print(f"[bench] {cfg} B={b} {prec}: {others[-1]['value']} samples/s", file=sys.stderr, flush=True)
         from unified_video_action_amd.runtime import RT
         RT.set_precision(args.precision)
     if rank != 0:

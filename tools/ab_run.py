@@ -1,6 +1,7 @@
 """Same-box A/B of two library builds (tools only; the product path never reads an override):
 
     python tools/ab_run.py <path/to/libuva_other.so> <script.py> [args...]
+    python tools/ab_run.py <path/to/libuva_other.so> -m pytest [args...]
 
 binds <lib> through native.lib.use_library() and then runs <script.py> as __main__.  Entry points
 that the other build predates stay unbound and are listed on stderr."""
@@ -16,7 +17,13 @@ if __name__ == "__main__":
         raise SystemExit(__doc__)
     from unified_video_action_amd.native.lib import use_library
     use_library(sys.argv[1])
-    script = sys.argv[2]
-    sys.argv = sys.argv[2:]
-    sys.path.insert(0, os.path.dirname(os.path.abspath(script)))
-    runpy.run_path(script, run_name="__main__")
+    if sys.argv[2] == "-m":  # python tools/ab_run.py <lib> -m pytest ...
+        mod = sys.argv[3]
+        sys.argv = [mod] + sys.argv[4:]
+        sys.path.insert(0, os.getcwd())
+        runpy.run_module(mod, run_name="__main__", alter_sys=True)
+    else:
+        script = sys.argv[2]
+        sys.argv = sys.argv[2:]
+        sys.path.insert(0, os.path.dirname(os.path.abspath(script)))
+        runpy.run_path(script, run_name="__main__")

@@ -178,5 +178,16 @@ __device__ __forceinline__ void xcd_grid2(int& bx, int& by) {
   by = Lp / gx;
 }
 
+// sum over the 16 lanes of a DPP row (lanes 16r .. 16r+15), result in every lane: quad_perm xor 1,
+// xor 2, then row_ror 4 and 8 -- four VALU adds with DPP operands instead of four dependent
+// ds_bpermute round trips through the LDS crossbar (what __shfl_xor lowers to)
+__device__ __forceinline__ float row16_sum(float v) {
+  v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0xB1, 0xF, 0xF, false));
+  v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x4E, 0xF, 0xF, false));
+  v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x124, 0xF, 0xF, false));
+  v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x128, 0xF, 0xF, false));
+  return v;
+}
+
 #define UVA_LAUNCH_CHECK() \
   do { hipError_t _e = hipGetLastError(); if (_e != hipSuccess) return (int)_e; } while (0)

@@ -145,6 +145,11 @@ __global__ __launch_bounds__(TR * 32, 16 / TR) void conv3x3_halo(const bf16* __r
   // 64-channel chunk, for the halo swap); padded halo pitch, taps unrolled: every A-fragment read is
   // base + immediate offset (no per-step address VALU)
   constexpr bool RB = (VAR & 64) != 0 && GN && !R3 && !SPREAD;
+  // PIPE (RB only): the next tap's A fragment (ks, f) is read into the slot right after the two
+  // MFMAs of this tap that consume it, so a tap's LDS reads run under the previous tap's MFMAs
+  // (otherwise every tap opens with the latency of its first reads: the 16 fragment registers are
+  // reused tap after tap and hipcc issues the next tap's reads only after the last MFMA)
+  constexpr bool PIPE = RB && (VAR & 128) != 0;
   static_assert(!SPREAD || ConvHCfg<BN, TR>::ROUNDS <= 8, "one staging round per tap 1..8");
   static_assert(!RB || TR == 8, "the register epilogue writes one 128-pixel GroupNorm unit per tile");
   using G = ConvHCfg<BN, TR, R3, HD, RB>;
@@ -347,11 +352,22 @@ __global__ __launch_bounds__(TR * 32, 16 / TR) void conv3x3_halo(const bf16* __r
     for (int cc = 0; cc < nch; ++cc) {
       const bf16* hcur = halo + (cc & 1) * G::HALO_ELEMS + abase;
       const bool more = cc + 1 < nch;
+      bf16x8 fp[2][G::FM];  // PIPE: the fragments of the current tap, refilled for the next one
+      if constexpr (PIPE) {
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+          for (int f = 0; f < G::FM; ++f) fp[ks][f] = *(const bf16x8*)(hcur + f * CH_W * G::PP + ks * 32);
+      }
 #pragma unroll
       for (int tap = 0; tap < 9; ++tap) {
         const int s = cc * 9 + tap;
         const int cur = tap & 1, nxt = cur ^ 1;  // tap 8's next set is copied to set 0 below
-        if (s + 1 < S) bload(s + 1, bq[nxt]);
+        if constexpr (PIPE) {
+          bload(s + 1 < S ? s + 1 : s, bq[nxt]);  // unconditional: no block boundary inside a chunk
+        } else {
+          if (s + 1 < S) bload(s + 1, bq[nxt]);
+        }
         if (tap == 0 && more) halo_load(cc + 1);
         if (tap == 0 && !more && residual) {
           // rows 0..RQ_PRE-1 into the (now free) halo staging registers (the epilogue's 16-B runs)
@@ -360,6 +376,25 @@ __global__ __launch_bounds__(TR * 32, 16 / TR) void conv3x3_halo(const bf16* __r
           for (int f = 0; f < RQ_PRE; ++f) hreg[f] = *(const bf16x8*)(residual + (pix0 + (long long)f * W) * Co + csr);
         }
         const int kh = tap / 3, kw = tap % 3;
+        if constexpr (PIPE) {
+          const int kh1 = (tap + 1) / 3, kw1 = (tap + 1) % 3;
+          __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+          for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+            for (int f = 0; f < G::FM; ++f) {
+#pragma unroll
+              for (int g = 0; g < G::FN; ++g)
+                acc[f][g] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bq[cur][ks][g], fp[ks][f], acc[f][g], 0, 0, 0);
+              __builtin_amdgcn_sched_group_barrier(0x008, G::FN, 0);
+              if (tap < 8) {
+                fp[ks][f] = *(const bf16x8*)(hcur + ((f + kh1) * CH_W + kw1) * G::PP + ks * 32);
+                __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+              }
+            }
+          __builtin_amdgcn_s_setprio(0);
+          continue;
+        }
         bf16x8 fa[2][G::FM];
 #pragma unroll
         for (int ks = 0; ks < 2; ++ks)
@@ -436,13 +471,10 @@ __global__ __launch_bounds__(TR * 32, 16 / TR) void conv3x3_halo(const bf16* __r
         sa += sb;
         qa += qb;
       }
-#pragma unroll
-      for (int o = 1; o < 16; o <<= 1) {
-        sa += __shfl_xor(sa, o, 64);
-        qa += __shfl_xor(qa, o, 64);
-        sb += __shfl_xor(sb, o, 64);
-        qb += __shfl_xor(qb, o, 64);
-      }
+      sa = row16_sum(sa);
+      qa = row16_sum(qa);
+      sb = row16_sum(sb);
+      qb = row16_sum(qb);
       if (gsz >= 16) {
         sa = xor_lane_sum(sa, 32);
         qa = xor_lane_sum(qa, 32);
@@ -880,13 +912,10 @@ __global__ __launch_bounds__(256, 2) void conv3x3s2_kernel(const bf16* __restric
       sa += sb;
       qa += qb;
     }
-#pragma unroll
-    for (int o = 1; o < 16; o <<= 1) {
-      sa += __shfl_xor(sa, o, 64);
-      qa += __shfl_xor(qa, o, 64);
-      sb += __shfl_xor(sb, o, 64);
-      qb += __shfl_xor(qb, o, 64);
-    }
+    sa = row16_sum(sa);
+    qa = row16_sum(qa);
+    sb = row16_sum(sb);
+    qb = row16_sum(qb);
     if (gsz >= 16) {
       sa = xor_lane_sum(sa, 32);
       qa = xor_lane_sum(qa, 32);
@@ -964,7 +993,10 @@ extern "C" int uva_conv3x3_halo(const void* in, const void* w, void* out, const 
   // GN: 64 = weights in VGPRs, one barrier per chunk (same-box level-0 conv 6.61 -> 6.49 ms with the
   // bias + residual + GN-stats epilogue, 7.02 -> 6.79 ms in the bench).  The other VAR bits are the
   // measured-slower alternatives, compile-time only and not built.
-  if (gn_scale) CH_LAUNCH(128, true, 64, 8);
+#ifndef UVA_CONV_GN_VAR
+#define UVA_CONV_GN_VAR 64
+#endif
+  if (gn_scale) CH_LAUNCH(128, true, UVA_CONV_GN_VAR, 8);
   else CH_LAUNCH(128, false, 12, 8);
 #undef CH_LAUNCH
   UVA_LAUNCH_CHECK();
@@ -1099,11 +1131,8 @@ __global__ __launch_bounds__(256) void conv_in_kernel(const bf16* __restrict__ i
       // group g = f*4 + fk: reduce over the 16 pixel lanes sharing fk
 #pragma unroll
       for (int f = 0; f < 8; ++f) {
-#pragma unroll
-        for (int o = 1; o < 16; o <<= 1) {
-          gs[f] += __shfl_xor(gs[f], o, 64);
-          gq[f] += __shfl_xor(gq[f], o, 64);
-        }
+        gs[f] = row16_sum(gs[f]);
+        gq[f] = row16_sum(gq[f]);
       }
       if (frow == 0) {
 #pragma unroll
