@@ -120,3 +120,18 @@ def test_workspace_setup_from_config(tmp_path, fp32):
     assert ws.model.normalizer["action"].params["scale"][0].item() == pytest.approx(2 / 512)
     from unified_video_action_amd.model.autoregressive.ema_model import EMAModel
     assert isinstance(ws.ema, EMAModel) and ws.ema.power == 0.75
+
+
+def test_topk_fallback_keeps_configured_monitor_key(tmp_path):
+    """a call without the configured monitor key ranks by train_loss in a ranking
+    of its own and leaves monitor_key / mode / format_str alone, so the configured key is used
+    again once it is logged."""
+    from unified_video_action_amd.workspace.train_unified_video_action_workspace import TopKCheckpointManager
+    m = TopKCheckpointManager(str(tmp_path), "test_mean_score", mode="max", k=2)
+    p1 = m.get_ckpt_path({"epoch": 1, "train_loss": 1.0})
+    p2 = m.get_ckpt_path({"epoch": 2, "train_loss": 0.5})
+    assert p1 and p2 and "train_loss" in p1
+    assert m.get_ckpt_path({"epoch": 3, "train_loss": 2.0}) is None  # worse than both kept
+    assert (m.monitor_key, m.mode, m.format_str) == ("test_mean_score", "max", "epoch={epoch:03d}.ckpt")
+    q = m.get_ckpt_path({"epoch": 4, "train_loss": 0.1, "test_mean_score": 0.3})
+    assert q.endswith("epoch=004.ckpt") and m.path_value_map == {q: 0.3}

@@ -71,41 +71,47 @@ def _to_device(x, dev):
 class TopKCheckpointManager:
     """common/checkpoint_util.py:5-60."""
 
+    FALLBACK = ("train_loss", "min", "epoch={epoch:04d}-train_loss={train_loss:.3f}.ckpt")
+
     def __init__(self, save_dir, monitor_key, mode="min", k=1, format_str="epoch={epoch:03d}.ckpt"):
         assert mode in ("max", "min") and k >= 0
         self.save_dir, self.monitor_key, self.mode, self.k, self.format_str = save_dir, monitor_key, mode, k, format_str
-        self.path_value_map = {}
+        self.maps = {monitor_key: {}}  # ranking key -> {path: value}
+        self.path_value_map = self.maps[monitor_key]
 
     def get_ckpt_path(self, data):
         if self.k == 0:
             return None
-        if self.monitor_key not in data:
-            # the reference's monitor keys (test_mean_score, val_action_l2_distances) come from the
-            # env-runner / validation paths this workspace does not run: rank by train_loss instead
-            # (lower is better), with a file name that states it, and say so once
-            if "train_loss" not in data:
+        if self.monitor_key in data:
+            key, mode, fmt = self.monitor_key, self.mode, self.format_str
+        else:
+            # Difference from the reference (which raises KeyError): its monitor keys (test_mean_score,
+            # val_action_l2_distances) come from env-runner / validation paths this workspace does not
+            # run, so a call without the configured key ranks by train_loss (min) under a file name
+            # that says so -- per call, in a ranking of its own: the configured key, once logged,
+            # is used again (INTEGRATION.md §4)
+            if self.FALLBACK[0] not in data:
                 return None
-            if not getattr(self, "_fallback", False):
+            key, mode, fmt = self.FALLBACK
+            if key not in self.maps:
                 print(f"TopKCheckpointManager: '{self.monitor_key}' is not logged by this workspace; "
-                      f"ranking top-k checkpoints by train_loss (min)")
-                self._fallback = True
-                self.monitor_key, self.mode = "train_loss", "min"
-                self.format_str = "epoch={epoch:04d}-train_loss={train_loss:.3f}.ckpt"
-        value = data[self.monitor_key]
-        path = os.path.join(self.save_dir, self.format_str.format(**data))
-        if len(self.path_value_map) < self.k:
-            self.path_value_map[path] = value
+                      f"ranking top-k checkpoints by {key} ({mode}) while it is absent")
+        pv = self.maps.setdefault(key, {})
+        value = data[key]
+        path = os.path.join(self.save_dir, fmt.format(**data))
+        if len(pv) < self.k:
+            pv[path] = value
             return path
-        ranked = sorted(self.path_value_map.items(), key=lambda x: x[1])
+        ranked = sorted(pv.items(), key=lambda x: x[1])
         drop = None
-        if self.mode == "max" and value > ranked[0][1]:
+        if mode == "max" and value > ranked[0][1]:
             drop = ranked[0][0]
-        elif self.mode == "min" and value < ranked[-1][1]:
+        elif mode == "min" and value < ranked[-1][1]:
             drop = ranked[-1][0]
         if drop is None:
             return None
-        del self.path_value_map[drop]
-        self.path_value_map[path] = value
+        del pv[drop]
+        pv[path] = value
         if os.path.exists(drop):
             os.remove(drop)
         return path
