@@ -80,12 +80,17 @@ int uva_conv2d(int dtype, const void* in, const void* w, void* out, const float*
  * uva_pool4x4_relu_bwd: dpre[n][16][16][C] = (post > 0) * gpool[n][16 c + cell] / 16 (the backward
  *      of ReLU -> mean-pool; post = the forward's post-ReLU conv output, gpool any of bf16 / fp32).
  * uva_im2col3x3: cols[n H W][9 Ci] with column ci*9 + kh*3 + kw (nn.Conv2d weight order), zero pad 1.
+ * uva_im2col3x3_tc: the same columns in tap-major order, tap*Ci + ci (16-B vector moves; Ci % 8 for
+ *      bf16, % 4 for fp32; 16-B aligned); the dW product over them is [Co][9][Ci], added into the
+ *      nn.Conv2d-layout fp32 gradient [Co][Ci][3][3] by uva_conv3x3_dw_scatter_add.
  * uva_conv3x3_weight_layout: fp32 [Co][Ci][3][3] -> mode 0 [Co][3][3][Ci] (forward conv operand),
  *      mode 1 [Ci][3][3][Co] flipped (the dX conv), out_dtype bf16 / fp32. */
 int uva_pool4x4_cwh(int dtype, const void* in, void* out, int n, int C, hipStream_t stream);
 int uva_pool4x4_relu_bwd(int dtype, const void* post, int gdtype, const void* gpool, void* dpre, int n, int C,
                          hipStream_t stream);
 int uva_im2col3x3(int dtype, const void* in, void* cols, int n, int H, int W, int Ci, hipStream_t stream);
+int uva_im2col3x3_tc(int dtype, const void* in, void* cols, int n, int H, int W, int Ci, hipStream_t stream);
+int uva_conv3x3_dw_scatter_add(const float* part, float* grad, int Co, int Ci, hipStream_t stream);
 int uva_conv3x3_weight_layout(const float* w, int out_dtype, void* out, int Co, int Ci, int mode, hipStream_t stream);
 int uva_conv3x3_halo_bn(int Nimg, int H, int W, int Ci, int Co);
 int uva_conv3x3_halo(const void* in, const void* w, void* out, const float* bias, const void* residual, int Nimg,

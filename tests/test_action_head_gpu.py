@@ -1,6 +1,6 @@
 """conv_fc action trunk kernels (diffusion_action_loss.py:42-61) vs plain PyTorch fp32:
 Conv2d(D, D, 3, p=1) + ReLU + AdaptiveAvgPool2d((4, 4)) + flatten (c w h) forward and backward
-through ConvReluPoolFn (HIP conv, pool-(c w h), fused pool/ReLU backward, im2col in Conv2d order,
+through ConvReluPoolFn (HIP conv, pool-(c w h), fused pool/ReLU backward, tap-major im2col + dW scatter-add,
 weight layouts), fp32 (1e-5 of scale) and bf16 (2e-2); and the generic GEMM's split-K path for
 tiny-output, long-K products (the Linear(4 -> 16) frame-interpolation dW)."""
 import pytest
@@ -57,6 +57,25 @@ def test_im2col_columns_in_conv2d_weight_order():
     ops.im2col3x3(x, cols, n, H, W, Ci)
     ref = F.unfold(x.permute(0, 3, 1, 2), 3, padding=1)  # [n, Ci*9 (ci, kh, kw), H*W]
     assert torch.equal(cols.reshape(n, H * W, Ci * 9).transpose(1, 2), ref)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_im2col_tap_major_and_dw_scatter_add(dtype):
+    """uva_im2col3x3_tc: cols[p][tap*Ci + ci] == unfold's columns re-ordered tap-major (bit-exact);
+    uva_conv3x3_dw_scatter_add: grad[co][ci][kh][kw] += part[co][kh*3+kw][ci] (bit-exact)."""
+    from unified_video_action_amd.native import ops
+    n, H, W, Ci, Co = 2, 5, 7, 16, 24
+    x = (torch.randn(n, H, W, Ci, device=DEV) * 4).to(dtype)
+    cols = torch.full((n * H * W, 9 * Ci), float("nan"), device=DEV, dtype=dtype)
+    ops.im2col3x3_tc(x, cols, n, H, W, Ci)
+    ref = F.unfold(x.float().permute(0, 3, 1, 2), 3, padding=1)           # [n, (ci, tap), HW]
+    ref = ref.reshape(n, Ci, 9, H * W).permute(0, 3, 2, 1).reshape(n * H * W, 9 * Ci)
+    assert torch.equal(cols.float(), ref)
+    part = torch.randn(Co, 9 * Ci, device=DEV)
+    grad = torch.randn(Co, Ci, 3, 3, device=DEV)
+    want = grad + part.reshape(Co, 3, 3, Ci).permute(0, 3, 1, 2)
+    ops.conv3x3_dw_scatter_add(part, grad)
+    assert torch.equal(grad, want)
 
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])

@@ -15,6 +15,10 @@ sys.path.insert(0, ROOT)
 if __name__ == "__main__":
     if len(sys.argv) < 3:
         raise SystemExit(__doc__)
+    # torch first: it brings its own HIP runtime (libamdhip64), which the library must bind to, as it
+    # does on the product path (a library loaded before torch pulls in /opt/rocm's runtime: two
+    # runtimes in one process, and the second reports hipErrorNoDevice)
+    import torch  # noqa: F401
     from unified_video_action_amd.native.lib import use_library
     use_library(sys.argv[1])
     if sys.argv[2] == "-m":  # python tools/ab_run.py <lib> -m pytest ...

@@ -16,3 +16,4 @@ for i in 1 2; do
 done
 timeout -k 10 900 python -u bench.py > $O/bench.json 2> $O/bench.err || { echo BENCH_FAIL; tail -20 $O/bench.err; exit 1; }
 cat $O/bench.json
+timeout -k 10 300 python -u bench.py --config pusht_joint --batch 64 --steps 5 --warmup 2 --other-configs "" --no-cpu-baseline --h2d-steps 0 --trace-out $O/trace_joint.json > $O/bench_joint.json 2> $O/bench_joint.err || { echo JOINT_FAIL; tail -5 $O/bench_joint.err; exit 1; }

@@ -83,6 +83,47 @@ __global__ __launch_bounds__(256) void im2col3x3_kernel(const T* __restrict__ in
     }
 }
 
+// cols[(img, y, x)][tap * Ci + ci] = in[img][y + kh - 1][x + kw - 1][ci] (tap = kh * 3 + kw; zero
+// outside): one thread per (pixel, tap, 8-channel chunk) moves 16 B, so both the gather reads and the
+// 9x-sized column stream are full-width vector accesses (the (ci, tap) order above writes 9
+// interleaved 2-B columns per thread: 0.59 ms at the PushT-joint B = 64 shape).  The dW product over
+// these columns comes out as [Co][9][Ci] and is added into the nn.Conv2d-layout gradient by
+// conv3x3_dw_scatter_add below.
+template <typename T>
+__global__ __launch_bounds__(256) void im2col3x3_tc_kernel(const T* __restrict__ in, T* __restrict__ cols, int n,
+                                                           int H, int W, int Ci) {
+  constexpr int V = 16 / sizeof(T);  // elements per 16-B chunk
+  const int nc = Ci / V;
+  const long long t = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (t >= (long long)n * H * W * 9 * nc) return;
+  const int c = (int)(t % nc);
+  const long long r = t / nc;
+  const int tap = (int)(r % 9);
+  const long long p = r / 9;
+  const int x = (int)(p % W);
+  const long long q = p / W;
+  const int y = (int)(q % H);
+  const long long img = q / H;
+  const int yy = y + tap / 3 - 1, xx = x + tap % 3 - 1;
+  int4 v = {0, 0, 0, 0};
+  if (yy >= 0 && yy < H && xx >= 0 && xx < W) v = *(const int4*)(in + ((img * H + yy) * W + xx) * Ci + c * V);
+  *(int4*)(cols + (p * 9 + tap) * Ci + c * V) = v;
+}
+
+// grad[co][ci][kh][kw] += part[co][kh * 3 + kw][ci] (fp32): one thread per (co, ci) reads its 9 taps
+// (coalesced over ci) and adds them to its 9 contiguous gradient words
+__global__ __launch_bounds__(256) void conv3x3_dw_scatter_add_kernel(const float* __restrict__ part,
+                                                                     float* __restrict__ grad, int Co, int Ci) {
+  const long long t = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (t >= (long long)Co * Ci) return;
+  const int ci = (int)(t % Ci);
+  const long long co = t / Ci;
+  const float* src = part + co * 9 * Ci + ci;
+  float* dst = grad + t * 9;
+#pragma unroll
+  for (int k = 0; k < 9; ++k) dst[k] += src[(long long)k * Ci];
+}
+
 // nn.Conv2d weight [Co][Ci][3][3] (fp32 master) -> the implicit-GEMM conv's [Co][kh][kw][Ci]
 // (mode 0) or the dX conv's flipped transpose [Ci][kh][kw][Co] = w[co][ci][2-kh][2-kw] (mode 1)
 template <typename T>
@@ -134,6 +175,26 @@ extern "C" int uva_im2col3x3(int dtype, const void* in, void* cols, int n, int H
     im2col3x3_kernel<bf16><<<nblocks(work), 256, 0, s>>>((const bf16*)in, (bf16*)cols, n, H, W, Ci);
   else
     im2col3x3_kernel<float><<<nblocks(work), 256, 0, s>>>((const float*)in, (float*)cols, n, H, W, Ci);
+  UVA_LAUNCH_CHECK();
+  return 0;
+}
+
+extern "C" int uva_im2col3x3_tc(int dtype, const void* in, void* cols, int n, int H, int W, int Ci, hipStream_t s) {
+  if (n <= 0) return 0;
+  const int V = dtype == UVA_DT_BF16 ? 8 : 4;
+  if (Ci % V || (((uintptr_t)in | (uintptr_t)cols) % 16)) return (int)hipErrorInvalidValue;
+  const long long work = (long long)n * H * W * 9 * (Ci / V);
+  if (dtype == UVA_DT_BF16)
+    im2col3x3_tc_kernel<bf16><<<nblocks(work), 256, 0, s>>>((const bf16*)in, (bf16*)cols, n, H, W, Ci);
+  else
+    im2col3x3_tc_kernel<float><<<nblocks(work), 256, 0, s>>>((const float*)in, (float*)cols, n, H, W, Ci);
+  UVA_LAUNCH_CHECK();
+  return 0;
+}
+
+extern "C" int uva_conv3x3_dw_scatter_add(const float* part, float* grad, int Co, int Ci, hipStream_t s) {
+  if (Co <= 0 || Ci <= 0) return 0;
+  conv3x3_dw_scatter_add_kernel<<<nblocks((long long)Co * Ci), 256, 0, s>>>(part, grad, Co, Ci);
   UVA_LAUNCH_CHECK();
   return 0;
 }

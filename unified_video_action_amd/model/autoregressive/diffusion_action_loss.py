@@ -20,8 +20,8 @@ class ConvReluPoolFn(torch.autograd.Function):
     """Conv2d(D, D, 3, p=1) + bias + ReLU + AdaptiveAvgPool2d((4, 4)) + flatten (c w h) of NHWC
     [n, 16, 16, D] (diffusion_action_loss.py:42-47, 113-124); weight in nn.Conv2d layout [Co, Ci, 3, 3].
     No ATen kernels: the weight changes layout in one HIP pass, the pool writes (c w h) directly,
-    the backward fuses the pool's broadcast with the ReLU mask, and dW = dpre^T im2col(x) with the
-    im2col columns in (ci, kh, kw) order accumulates straight into the Conv2d-layout gradient."""
+    the backward fuses the pool's broadcast with the ReLU mask, and dW = dpre^T im2col(x) over tap-major
+    im2col columns (16-B vector gather) is added into the Conv2d-layout gradient by a scatter-add pass."""
 
     @staticmethod
     def forward(ctx, x, weight, bias):
@@ -52,11 +52,14 @@ class ConvReluPoolFn(torch.autograd.Function):
         ops.conv3x3_weight_layout(weight.detach(), wt, 1)
         dx = torch.empty(n, H, W, Ci, dtype=cd, device=g.device)
         ops.conv2d(dpre, wt, dx, n, H, W, Co, Ci, 3, 1, 1, 1, H, W)
-        # dW[co][(ci, kh, kw)] += dpre^T im2col(x)
-        cols = torch.empty(n * H * W, Ci * 9, dtype=cd, device=g.device)
-        ops.im2col3x3(xc, cols, n, H, W, Ci)
-        ops.linear_dw(dpre.reshape(-1, Co), cols, grad_buf(weight).view(Co, Ci * 9), beta=1.0)
+        # dW[co][(kh, kw, ci)] = dpre^T im2col(x) over tap-major columns (16-B vector gather), then
+        # added into the nn.Conv2d-layout gradient [co][ci][kh][kw]
+        cols = torch.empty(n * H * W, 9 * Ci, dtype=cd, device=g.device)
+        ops.im2col3x3_tc(xc, cols, n, H, W, Ci)
+        part = torch.empty(Co, 9 * Ci, dtype=F32, device=g.device)
+        ops.linear_dw(dpre.reshape(-1, Co), cols, part, beta=0.0)
         del cols
+        ops.conv3x3_dw_scatter_add(part, grad_buf(weight))
         ops.colsum(dpre.reshape(-1, Co), grad_buf(bias))
         return as_dtype(dx, ctx.xdt), None, None
 

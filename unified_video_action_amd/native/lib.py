@@ -46,6 +46,7 @@ class UvaLib:
                 f"libuva_hip.so not found at {path}: run __graft_entry__.build() (hipcc gfx950). "
                 "There is no CPU fallback on the product path.")
         self.path = path
+        import torch  # noqa: F401  -- torch's HIP runtime first: the library binds to it, not a second copy
         self._lib = ctypes.CDLL(path)
         self.sigs = parse_header()
         self.unbound = []

@@ -463,6 +463,21 @@ def im2col3x3(x, cols, n, H, W, Ci):
     lib().call("uva_im2col3x3", dt(x), ptr(x), ptr(cols), n, H, W, Ci, stream())
 
 
+def im2col3x3_tc(x, cols, n, H, W, Ci):
+    """tap-major im2col: cols[p][tap*Ci + ci] (uva_im2col3x3_tc)."""
+    assert x.is_contiguous() and cols.is_contiguous() and x.dtype == cols.dtype
+    assert x.numel() == n * H * W * Ci and cols.numel() == n * H * W * Ci * 9
+    lib().call("uva_im2col3x3_tc", dt(x), ptr(x), ptr(cols), n, H, W, Ci, stream())
+
+
+def conv3x3_dw_scatter_add(part, grad):
+    """grad[co][ci][kh][kw] += part[co][kh*3 + kw][ci] (fp32)."""
+    Co, Ci = grad.shape[0], grad.shape[1]
+    assert part.dtype == grad.dtype == torch.float32 and part.is_contiguous() and grad.is_contiguous()
+    assert part.numel() == grad.numel() == Co * Ci * 9
+    lib().call("uva_conv3x3_dw_scatter_add", ptr(part), ptr(grad), Co, Ci, stream())
+
+
 def conv3x3_weight_layout(w, out, mode):
     """fp32 nn.Conv2d weight [Co,Ci,3,3] -> mode 0 [Co,3,3,Ci] / mode 1 flipped [Ci,3,3,Co]"""
     Co, Ci = w.shape[0], w.shape[1]
