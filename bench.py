@@ -68,7 +68,7 @@ def parse(argv=None):
     ap.add_argument("--cpu-batch", type=int, default=2, help="CPU baseline batch (BASELINE configs[0]: 2)")
     ap.add_argument("--cpu-warmup", type=int, default=5, help="CPU warm-up steps (BASELINE.md §4: 5)")
     ap.add_argument("--cpu-steps", type=int, default=10, help="timed CPU steps, median reported (BASELINE.md §4: 10)")
-    ap.add_argument("--cpu-budget-s", type=float, default=120.0,
+    ap.add_argument("--cpu-budget-s", type=float, default=90.0,
                     help="wall budget of the B=2 leg: fewer timed steps (stated in `sample`) when a step is slow")
     ap.add_argument("--no-trace", action="store_true")
     ap.add_argument("--trace-steps", type=int, default=3)

@@ -188,10 +188,37 @@ def rowk_bench():
     dbias = torch.zeros(F, device=dev)
     t = timeit(lambda: ops.act_bwd_bias(pre, g, gx, dbias, "gelu", drop_p=0.1, seed=3))
     print(f"act_bwd_bias gelu+dropout bf16 [{M},{F}]: {t*1e3:.1f} us, {M*F*6/t/1e6:.0f} GB/s")
+    # timm Mlp forward elementwise passes: fc1 GELU + dropout (bf16 -> bf16), fc2 dropout + fp32 residual
+    t = timeit(lambda: ops.act_drop_fwd(pre, gx, "gelu", drop_p=0.1, seed=3))
+    print(f"act_drop_fwd gelu+dropout bf16 [{M},{F}]: {t*1e3:.1f} us, {M*F*4/t/1e6:.0f} GB/s")
+    h = torch.randn(M, D, device=dev).to(torch.bfloat16)
+    t = timeit(lambda: ops.act_drop_fwd(h, dx, "none", drop_p=0.1, seed=3, residual=dxb))
+    print(f"act_drop_fwd dropout+res bf16/f32 [{M},{D}]: {t*1e3:.1f} us, {M*D*10/t/1e6:.0f} GB/s")
 
 
 if __name__ == "__main__" and len(sys.argv) > 1 and sys.argv[1] == "rowk":
     rowk_bench()
+
+
+def resgemm_bench():
+    """The fp32-residual N = 768 forward products of a timm Block as the training step runs them:
+    attention proj (K = 768) and fc2 (K = 3072), bias + dropout 0.1 + fp32 residual, fp32 out."""
+    dev = "cuda"
+    M, N = 32 * 1024, 768
+    for K in (768, 3072):
+        x = torch.randn(M, K, device=dev).to(torch.bfloat16)
+        w = (torch.randn(N, K, device=dev) / K ** 0.5).to(torch.bfloat16)
+        b = torch.randn(N, device=dev)
+        res = torch.randn(M, N, device=dev)
+        y = torch.empty(M, N, device=dev)
+        fl = 2 * M * N * K
+        t = timeit(lambda: ops.linear(x, w, y, bias=b, residual=res, drop_p=0.1, seed=5))
+        print(f"resgemm M={M} N={N} K={K} bias+drop+f32res: {t:.4f} ms {fl/t/1e9:.0f} TF, "
+              f"{(M*K*2 + M*N*8)/t/1e6:.0f} GB/s")
+
+
+if __name__ == "__main__" and len(sys.argv) > 1 and sys.argv[1] == "resgemm":
+    resgemm_bench()
 
 
 def aug_bench():

@@ -33,6 +33,9 @@
 // scale costs nothing inside the loops.
 #include "common.h"
 
+#ifndef UVA_ATT_PIPE
+#define UVA_ATT_PIPE 0
+#endif
 #define AT_LD 72
 #define AT_TILE (64 * AT_LD)
 
@@ -491,6 +494,83 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_kernel(const bf16* __res
     for (int qt = 0; qt < 4; ++qt)
 #pragma unroll
       for (int kt = 0; kt < 2; ++kt) s[qt][kt] = dp[qt][kt] = (f32x4){0.f, 0.f, 0.f, 0.f};
+#if UVA_ATT_PIPE
+    // software-pipelined form: the tile is walked in query halves so that every MFMA run has
+    // independent VALU beside it -- S / dP of queries 32..63 beside the softmax of 0..31, dV / dK of
+    // 0..31 beside the softmax of 32..63 (hipcc otherwise issues the 32 S / dP MFMAs, then all the
+    // softmax VALU, then the 32 dV / dK MFMAs: each wave alternates matrix-only and vector-only runs)
+    auto sdp = [&](int qt) __attribute__((always_inline)) {
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        const bf16x8 a = lds_row_frag(sQ[cur], qt * 16, ks);
+        const bf16x8 e = lds_row_frag(sO[cur], qt * 16, ks);
+#pragma unroll
+        for (int kt = 0; kt < 2; ++kt) {
+          s[qt][kt] = mfma16(a, kf[kt][ks], s[qt][kt]);
+          dp[qt][kt] = mfma16(e, vf[kt][ks], dp[qt][kt]);
+        }
+      }
+    };
+    auto soft = [&](int qt) __attribute__((always_inline)) {
+      const f32x4 Lq = *(const f32x4*)&sL[cur][qt * 16 + 4 * g];
+      const f32x4 Dq = *(const f32x4*)&sD[cur][qt * 16 + 4 * g];
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int kt = 0; kt < 2; ++kt) {
+          const float p = exp2_fast(fmaf(s[qt][kt][r], c, -Lq[r]));
+          if (DROP) {
+            const float pd = keep_bfe(p, mw[kt], qt * 4 + r);
+            s[qt][kt][r] = pd;
+            dp[qt][kt][r] = fmaf(pd, dp[qt][kt][r], -(p * Dq[r]));
+          } else {
+            s[qt][kt][r] = p;
+            dp[qt][kt][r] = p * (dp[qt][kt][r] - Dq[r]);
+          }
+        }
+    };
+    auto dkdv = [&](int ks) __attribute__((always_inline)) {
+      bf16x8 pb[2], sb[2];
+#pragma unroll
+      for (int kt = 0; kt < 2; ++kt) {
+        pb[kt] = pack_pi(s[2 * ks][kt], s[2 * ks + 1][kt]);
+        sb[kt] = pack_pi(dp[2 * ks][kt], dp[2 * ks + 1][kt]);
+      }
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) {
+        const bf16x8 oa = lds_tr_frag(sO[cur], 32 * ks, 32 * ks + 16, dt * 16);
+        const bf16x8 qa = lds_tr_frag(sQ[cur], 32 * ks, 32 * ks + 16, dt * 16);
+#pragma unroll
+        for (int kt = 0; kt < 2; ++kt) {
+          dv[dt][kt] = mfma16(oa, pb[kt], dv[dt][kt]);
+          dk[dt][kt] = mfma16(qa, sb[kt], dk[dt][kt]);
+        }
+      }
+    };
+    sdp(0);
+    sdp(1);
+    __builtin_amdgcn_sched_barrier(0);
+    sdp(2);
+    sdp(3);
+    soft(0);
+    soft(1);
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 1);  // MFMA
+      __builtin_amdgcn_sched_group_barrier(0x002, 6, 1);  // VALU
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    dkdv(0);
+    soft(2);
+    soft(3);
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 2);
+      __builtin_amdgcn_sched_group_barrier(0x002, 6, 2);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    dkdv(1);
+#else
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
@@ -544,6 +624,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_kernel(const bf16* __res
         }
       }
     }
+#endif
     if (more) {
       stage_store(sQ[cur ^ 1], rq);
       stage_store(sO[cur ^ 1], ro);
@@ -644,6 +725,67 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(const bf16* __restr
     for (int kt = 0; kt < 4; ++kt)
 #pragma unroll
       for (int qt = 0; qt < 2; ++qt) s[kt][qt] = dp[kt][qt] = (f32x4){0.f, 0.f, 0.f, 0.f};
+#if UVA_ATT_PIPE
+    // software-pipelined in key halves (as dK / dV): S / dP of keys 32..63 beside the softmax of keys
+    // 0..31, dQ of keys 0..31 beside the softmax of 32..63
+    auto sdp = [&](int kt) __attribute__((always_inline)) {
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        const bf16x8 ka = lds_row_frag(sK[cur], kt * 16, ks);
+        const bf16x8 va = lds_row_frag(sV[cur], kt * 16, ks);
+#pragma unroll
+        for (int qt = 0; qt < 2; ++qt) {
+          s[kt][qt] = mfma16(ka, qf[qt][ks], s[kt][qt]);
+          dp[kt][qt] = mfma16(va, of[qt][ks], dp[kt][qt]);
+        }
+      }
+    };
+    auto soft = [&](int kt) __attribute__((always_inline)) {
+#pragma unroll
+      for (int qt = 0; qt < 2; ++qt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float p = exp2_fast(fmaf(s[kt][qt][r], c, -L[qt]));
+          float dpt = dp[kt][qt][r];
+          if (DROP) dpt = keep_bfe(dpt, mw[qt], kt * 4 + r);
+          s[kt][qt][r] = p * (dpt - Dq[qt]);
+        }
+    };
+    auto dqk = [&](int ks) __attribute__((always_inline)) {
+      bf16x8 sb[2];
+#pragma unroll
+      for (int qt = 0; qt < 2; ++qt) sb[qt] = pack_pi(s[2 * ks][qt], s[2 * ks + 1][qt]);
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) {
+        const bf16x8 ka = lds_tr_frag(sK[cur], 32 * ks, 32 * ks + 16, dt * 16);
+#pragma unroll
+        for (int qt = 0; qt < 2; ++qt) dq[dt][qt] = mfma16(ka, sb[qt], dq[dt][qt]);
+      }
+    };
+    sdp(0);
+    sdp(1);
+    __builtin_amdgcn_sched_barrier(0);
+    sdp(2);
+    sdp(3);
+    soft(0);
+    soft(1);
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 1);
+      __builtin_amdgcn_sched_group_barrier(0x002, 5, 1);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    dqk(0);
+    soft(2);
+    soft(3);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 2);
+      __builtin_amdgcn_sched_group_barrier(0x002, 10, 2);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    dqk(1);
+#else
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
@@ -679,6 +821,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(const bf16* __restr
         for (int qt = 0; qt < 2; ++qt) dq[dt][qt] = mfma16(ka, sb[qt], dq[dt][qt]);
       }
     }
+#endif
     if (more) {
       stage_store(sK[cur ^ 1], rk);
       stage_store(sV[cur ^ 1], rv);

@@ -1214,6 +1214,14 @@ __global__ __launch_bounds__(512, 1) void gemm_8ph(const bf16* __restrict__ A, c
   float bv[8];
   if (!pslab && full) epi_load_bias8(ep, col0, bv);
   const bool plain = !ep.residual && !ep.gate && !ep.aux && ep.act == 0 && ep.drop_thresh == 0 && ep.beta == 0.f;
+  // residual-only epilogues (attention proj / fc2 forward: bias + dropout + fp32 residual) stream
+  // the residual rows through a ring RQ deep (RQ 32-B loads in flight per thread instead of the
+  // general path's one row ahead): the N = 768 products were bound by that stream (404 TFLOP/s
+  // at M32768 N768 K768 with the 128 x 384 tile)
+  // (128 x 384 tile only: with the 256 x 256 tile's 128 accumulator registers still live in the
+  // second chunk's waves, the ring spilled)
+  const bool resonly = BN == 384 && TA != 2 && !pslab && full && ep.residual && !ep.gate && !ep.aux && ep.beta == 0.f &&
+                       ep.res_grad == 0 && ep.res_dt == UVA_DT_F32 && (ep.ldr % 4 == 0) && (roff % 4 == 0);
 #pragma unroll
   for (int chunk = 0; chunk < G::NCH; ++chunk) {
     float gs_s[8], gs_q[8];
@@ -1267,6 +1275,61 @@ __global__ __launch_bounds__(512, 1) void gemm_8ph(const bf16* __restrict__ A, c
               gs_q[e] += o[e] * o[e];
             }
           }
+        }
+      }
+    } else if (BN == 384 && (VAR & 2048) == 0 && resonly && !(VAR & 512)) {
+      constexpr int RQ = NIT < 4 ? NIT : 4;
+      float4 rr[RQ][2];
+      auto rload = [&](int it, int slot) __attribute__((always_inline)) {
+        const int row = rowb + it * RPP;
+        if (it < NIT && row < rowe) {
+          const float* rp = (const float*)ep.residual + roff + (long long)row * ep.ldr + col0;
+          rr[slot][0] = *(const float4*)rp;
+          rr[slot][1] = *(const float4*)(rp + 4);
+        }
+      };
+#pragma unroll
+      for (int u = 0; u < RQ; ++u) rload(u, u);
+      // rolled over groups of RQ rows (a fully unrolled loop hoisted every row's 64-bit addresses and
+      // spilled them), static ring slots inside a group
+#pragma unroll 1
+      for (int it0 = 0; it0 < NIT; it0 += RQ) {
+#pragma unroll
+        for (int u = 0; u < RQ; ++u) {
+          const int it = it0 + u;
+          const int row = rowb + it * RPP;
+          if (it < NIT && row < rowe) {
+            const int rl = it * RPP + rsub;
+            const float4 a = *(const float4*)(T + rl * G::TP + c8 * 8);
+            const float4 b = *(const float4*)(T + rl * G::TP + c8 * 8 + 4);
+            const float v[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+            const float4 r0 = rr[u][0], r1 = rr[u][1];
+            const float res[8] = {r0.x, r0.y, r0.z, r0.w, r1.x, r1.y, r1.z, r1.w};
+            bool keep[8] = {true, true, true, true, true, true, true, true};
+            if (ep.drop_thresh) {
+              const uint64_t d0 = (uint64_t)((long long)z * M * N + (long long)row * N + col0);  // even
+#pragma unroll
+              for (int e = 0; e < 8; e += 2) dropout_keep2(ep.drop_seed, d0 + e, ep.drop_thresh, keep[e], keep[e + 1]);
+            }
+            float o[8];
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+              float t = apply_act(ep.act, ep.alpha * v[e] + bv[e]);
+              if (ep.drop_thresh) t = keep[e] ? t * ep.drop_scale : 0.f;
+              o[e] = t + res[e];
+            }
+            TC* dst = C + coff + (long long)row * ldc + col0;
+            if constexpr (sizeof(TC) == 2) {
+              bf16x8 ov;
+#pragma unroll
+              for (int e = 0; e < 8; ++e) ov[e] = (bf16)o[e];
+              *(bf16x8*)dst = ov;
+            } else {
+              *(float4*)dst = make_float4(o[0], o[1], o[2], o[3]);
+              *(float4*)(dst + 4) = make_float4(o[4], o[5], o[6], o[7]);
+            }
+          }
+          rload(it + RQ, u);
         }
       }
     } else if (TA != 2 && !pslab && full && !(VAR & 512)) {
