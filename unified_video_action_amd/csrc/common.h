@@ -131,10 +131,20 @@ __device__ __forceinline__ float erf_fast(float x) {
   return copysignf(fmaf(-p, e, 1.0f), x);
 }
 __device__ __forceinline__ float gelu_erf(float x) { return 0.5f * x * (1.0f + erf_fast(x * 0.70710678118654752f)); }
+// GELU'(x) = Phi(x) + x phi(x).  erf_fast(x / sqrt 2) evaluates exp(-x^2 / 2) -- phi(x) up to its constant --
+// so the two share one v_exp_f32 (three transcendentals per element -> two: the act backward pass is
+// VALU-bound at 4.3 TB/s)
 __device__ __forceinline__ float gelu_erf_grad(float x) {
-  const float cdf = 0.5f * (1.0f + erf_fast(x * 0.70710678118654752f));
-  const float pdf = 0.39894228040143268f * __builtin_amdgcn_exp2f(-0.72134752044448170f * x * x);
-  return cdf + x * pdf;
+  const float e = __builtin_amdgcn_exp2f(-0.72134752044448170f * x * x);  // exp(-x^2 / 2)
+  const float ax = fabsf(x) * 0.70710678118654752f;
+  const float t = __builtin_amdgcn_rcpf(fmaf(0.3275911f, ax, 1.0f));
+  float p = fmaf(1.061405429f, t, -1.453152027f);
+  p = fmaf(p, t, 1.421413741f);
+  p = fmaf(p, t, -0.284496736f);
+  p = fmaf(p, t, 0.254829592f);
+  p *= t;
+  const float erf_ = copysignf(fmaf(-p, e, 1.0f), x);
+  return fmaf(0.5f, erf_, 0.5f) + x * (0.39894228040143268f * e);
 }
 // sigmoid as v_exp_f32 + v_rcp_f32 (1 ulp each): a plain `x / (1 + e)` compiles to the IEEE division
 // sequence (2 x v_div_scale, v_div_fmas, v_div_fixup, v_rcp + 4 FMAs) -- 3x the VALU work of the

@@ -374,6 +374,18 @@ __global__ __launch_bounds__(TR * 32, 16 / TR) void conv3x3_halo(const bf16* __r
           const int csr = n0 + wn * (G::FN * 16) + (fk & 1) * 16 + (fk >> 1) * 8;
 #pragma unroll
           for (int f = 0; f < RQ_PRE; ++f) hreg[f] = *(const bf16x8*)(residual + (pix0 + (long long)f * W) * Co + csr);
+          if constexpr ((VAR & 256) != 0) {
+            // the remaining rows too, into the GroupNorm scale registers (dead in the last chunk; the
+            // same variables, so the allocator needs no new ones): no residual load is left for the
+            // epilogue to wait on
+            static_assert(G::FM - RQ_PRE <= 2, "two late rows fit gsc");
+#pragma unroll
+            for (int f = RQ_PRE; f < G::FM; ++f) {
+              const f32x4 v = __builtin_bit_cast(f32x4, *(const bf16x8*)(residual + (pix0 + (long long)f * W) * Co + csr));
+#pragma unroll
+              for (int j = 0; j < 4; ++j) gsc[(f - RQ_PRE) * 4 + j] = v[j];
+            }
+          }
         }
         const int kh = tap / 3, kw = tap % 3;
         if constexpr (PIPE) {
@@ -433,7 +445,14 @@ __global__ __launch_bounds__(TR * 32, 16 / TR) void conv3x3_halo(const bf16* __r
     if (residual) {
 #pragma unroll
       for (int f = 0; f < G::FM; ++f)
-        rq[f] = f < RQ_PRE ? hreg[f] : *(const bf16x8*)(residual + (pix0 + (long long)f * W) * Co + cs);
+        if (f < RQ_PRE) {
+          rq[f] = hreg[f];
+        } else if constexpr ((VAR & 256) != 0) {
+          const int o = ((f - RQ_PRE) & 1) * 4;
+          rq[f] = __builtin_bit_cast(bf16x8, (f32x4){gsc[o], gsc[o + 1], gsc[o + 2], gsc[o + 3]});
+        } else {
+          rq[f] = *(const bf16x8*)(residual + (pix0 + (long long)f * W) * Co + cs);
+        }
     }
     float sa = 0.f, sb = 0.f, qa = 0.f, qb = 0.f;
 #pragma unroll

@@ -300,54 +300,38 @@ template <typename TX, typename TY, typename TR>
 __global__ __launch_bounds__(256) void act_drop_fwd_kernel(const TX* __restrict__ x, TY* __restrict__ y,
                                                            const TR* __restrict__ res, long long n8, int act,
                                                            uint32_t thresh, float dscale, uint64_t seed) {
-  // UNR independent 8-element chunks per thread and iteration, all loads issued before any math:
-  // with one chunk per iteration the 16-B load of a wave was its only one in flight and the
-  // [32768, 3072] GELU + dropout pass ran at 3.6 TB/s (latency-bound, not VALU- or HBM-bound)
-  constexpr int UNR = 4;
-  const long long stride = (long long)gridDim.x * blockDim.x;
-  for (long long i0 = (long long)blockIdx.x * blockDim.x + threadIdx.x; i0 < n8; i0 += stride * UNR) {
-    float v[UNR][8], r[UNR][8];
+  GRID_STRIDE(i, n8) {
+    float v[8], r[8];
+    ld8<TX>(x + i * 8, v);
+    if (res) ld8<TR>(res + i * 8, r);
+    switch (act) {
+      case ACT_GELU:
 #pragma unroll
-    for (int u = 0; u < UNR; ++u) {
-      const long long i = i0 + u * stride;
-      if (i < n8) {
-        ld8<TX>(x + i * 8, v[u]);
-        if (res) ld8<TR>(res + i * 8, r[u]);
-      }
+        for (int e = 0; e < 8; ++e) v[e] = gelu_erf(v[e]);
+        break;
+      case ACT_SILU:
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] = silu(v[e]);
+        break;
+      case ACT_RELU:
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] = v[e] > 0.f ? v[e] : 0.f;
+        break;
+      default:
+        break;
     }
+    if (thresh) {
+      bool keep[8];
 #pragma unroll
-    for (int u = 0; u < UNR; ++u) {
-      const long long i = i0 + u * stride;
-      if (i >= n8) break;
-      switch (act) {
-        case ACT_GELU:
+      for (int e = 0; e < 8; e += 2) dropout_keep2(seed, (uint64_t)(i * 8 + e), thresh, keep[e], keep[e + 1]);
 #pragma unroll
-          for (int e = 0; e < 8; ++e) v[u][e] = gelu_erf(v[u][e]);
-          break;
-        case ACT_SILU:
-#pragma unroll
-          for (int e = 0; e < 8; ++e) v[u][e] = silu(v[u][e]);
-          break;
-        case ACT_RELU:
-#pragma unroll
-          for (int e = 0; e < 8; ++e) v[u][e] = v[u][e] > 0.f ? v[u][e] : 0.f;
-          break;
-        default:
-          break;
-      }
-      if (thresh) {
-        bool keep[8];
-#pragma unroll
-        for (int e = 0; e < 8; e += 2) dropout_keep2(seed, (uint64_t)(i * 8 + e), thresh, keep[e], keep[e + 1]);
-#pragma unroll
-        for (int e = 0; e < 8; ++e) v[u][e] = keep[e] ? v[u][e] * dscale : 0.f;
-      }
-      if (res) {
-#pragma unroll
-        for (int e = 0; e < 8; ++e) v[u][e] += r[u][e];
-      }
-      st8<TY>(y + i * 8, v[u]);
+      for (int e = 0; e < 8; ++e) v[e] = keep[e] ? v[e] * dscale : 0.f;
     }
+    if (res) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] += r[e];
+    }
+    st8<TY>(y + i * 8, v);
   }
 }
 
