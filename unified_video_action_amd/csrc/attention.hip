@@ -36,6 +36,9 @@
 #ifndef UVA_ATT_PIPE
 #define UVA_ATT_PIPE 0
 #endif
+#ifndef UVA_ATT_PIPE_DQ
+#define UVA_ATT_PIPE_DQ 0
+#endif
 #define AT_LD 72
 #define AT_TILE (64 * AT_LD)
 
@@ -658,7 +661,10 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_kernel(const bf16* __res
 //   S^T = K Q^T, dP'^T = V dO'^T, dQ^T[d][q] += K^T dS^T  (dS^T packed in pi order as the B operand)
 // =====================================================================================
 template <bool DROP>
-__global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(const bf16* __restrict__ qkv, const bf16* __restrict__ dOs,
+#ifndef UVA_ATT_DQ_OCC
+#define UVA_ATT_DQ_OCC 2
+#endif
+__global__ __launch_bounds__(256, UVA_ATT_DQ_OCC) void attn_bwd_dq_kernel(const bf16* __restrict__ qkv, const bf16* __restrict__ dOs,
                                                              const float* __restrict__ lse2,
                                                              const float* __restrict__ Dvec,
                                                              const uint64_t* __restrict__ MQ, bf16* __restrict__ dqkv,
@@ -725,7 +731,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(const bf16* __restr
     for (int kt = 0; kt < 4; ++kt)
 #pragma unroll
       for (int qt = 0; qt < 2; ++qt) s[kt][qt] = dp[kt][qt] = (f32x4){0.f, 0.f, 0.f, 0.f};
-#if UVA_ATT_PIPE
+#if UVA_ATT_PIPE_DQ
     // software-pipelined in key halves (as dK / dV): S / dP of keys 32..63 beside the softmax of keys
     // 0..31, dQ of keys 0..31 beside the softmax of 32..63
     auto sdp = [&](int kt) __attribute__((always_inline)) {
