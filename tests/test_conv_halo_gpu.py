@@ -18,7 +18,10 @@ def rel_err(a, b):
 
 
 @pytest.mark.parametrize("n,H,W,Ci,Co", [(4, 32, 32, 128, 128), (2, 16, 16, 256, 512), (2, 64, 32, 64, 256),
-                                         (1, 48, 16, 192, 128)])
+                                         (1, 48, 16, 192, 128),
+                                         # Ci = Co = 128 with GN walks tile columns (strip form): strips of
+                                         # 2 and 10 tiles, 3 columns
+                                         (3, 16, 16, 128, 128), (2, 80, 48, 128, 128)])
 @pytest.mark.parametrize("gn", [False, True])
 @pytest.mark.parametrize("residual", [False, True])
 def test_conv_halo_matches_torch(n, H, W, Ci, Co, gn, residual):

@@ -266,9 +266,10 @@ def conv0_bench():
         bias = torch.randn(Co, device=dev)
         part = torch.empty(n * H * H // 128, 32, 2, device=dev)
         fl = 2 * n * H * H * Co * 9 * Ci
-        t = timeit(lambda: ops.conv2d(x, w, out, n, H, H, Ci, Co, 3, 1, 1, 1, H, H, bias=bias, residual=res,
-                                      gn_scale=sc, gn_shift=sh, gn_part=part), iters=10)
-        print(f"gnconv n{n} {H}x{H} C{Ci}: {t:.3f} ms {fl/t/1e9:.0f} TF")
+        for r, tag in ((res, ""), (None, " nores")):
+            t = timeit(lambda: ops.conv2d(x, w, out, n, H, H, Ci, Co, 3, 1, 1, 1, H, H, bias=bias, residual=r,
+                                          gn_scale=sc, gn_shift=sh, gn_part=part), iters=10)
+            print(f"gnconv n{n} {H}x{H} C{Ci}{tag}: {t:.3f} ms {fl/t/1e9:.0f} TF")
 
 
 if __name__ == "__main__" and len(sys.argv) > 1 and sys.argv[1] == "conv0":

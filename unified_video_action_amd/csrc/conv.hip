@@ -753,6 +753,262 @@ __global__ __launch_bounds__(TR * 32, 16 / TR) void conv3x3_halo(const bf16* __r
 }
 
 // =====================================================================================
+// GN conv, strip form (Ci = 128, i.e. two 64-channel chunks): one workgroup walks a vertical strip of
+// 8 x 16 tiles (one tile column of one image, top to bottom) instead of one tile.  Consecutive tiles
+// of a strip share two halo rows: the bottom two rows of tile ty's 10-row halo ARE the top two of tile
+// ty+1's, already GroupNorm'd + SiLU'd in LDS, so each later tile stages 8 new rows (144 of 180 halo
+// pixels) and copies two inside LDS -- 20 % less of the GN+SiLU staging (the kernel's VALU: two
+// transcendentals per element) and of the halo loads.  With two chunks the buffers never alternate
+// away from their chunk (chunk c always lives in buffer c), so both chunks' previous halos are still
+// in LDS when the next tile starts.  Everything per tile is the register-B kernel above (weights
+// streamed from L2 into VGPRs one tap ahead -- across the tile boundary too -- bias-seeded
+// accumulators, register epilogue with bias / residual / GroupNorm partial sums).
+// =====================================================================================
+template <int VAR>
+__global__ __launch_bounds__(256, 2) void conv3x3_gn_strip(const bf16* __restrict__ in, const bf16* __restrict__ wt,
+                                                           bf16* __restrict__ out, const float* __restrict__ bias,
+                                                           const bf16* __restrict__ residual,
+                                                           const float* __restrict__ gn_scale,
+                                                           const float* __restrict__ gn_shift, int gn_silu,
+                                                           float* __restrict__ gn_part, int Nimg, int H, int W) {
+  using G = ConvHCfg<128, 8, false, false, true>;
+  constexpr int Ci = 128, Co = 128, nch = 2, S = 18, K = 9 * Ci;
+  constexpr int NEWP = 8 * CH_W;                               // 144 new halo pixels (rows 2..9)
+  constexpr int ROUNDS_NEW = (NEWP * 8 + G::NTH - 1) / G::NTH;  // 5
+  static_assert(ROUNDS_NEW <= G::ROUNDS, "new-row staging fits the full-staging registers");
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  bf16* halo = (bf16*)smem;
+  const int tiles_x = W / CH_T, tiles_y = H / 8;
+  const int nstrip = Nimg * tiles_x;
+  const int st = ch_xcd_remap(blockIdx.x, nstrip);
+  const int tx = st % tiles_x, n = st / tiles_x;
+  const int ow0 = tx * CH_T;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wn = __builtin_amdgcn_readfirstlane(tid >> 6);  // WM = 1: wave = 32 output channels
+  const int frow = lane & 15, fk = lane >> 4;
+  auto opaque = [](int v) __attribute__((always_inline)) {
+    asm volatile("" : "+v"(v));
+    return v;
+  };
+
+  // ---- halo staging.  full: rows 0..9 (tile 0 of the strip); new: rows 2..9 (later tiles)
+  bf16x8 hreg[G::ROUNDS];
+  float gsc[8], gsh[8];
+  auto gn_load = [&](int cc) __attribute__((always_inline)) {
+    const int hc = opaque(tid) & 7;
+    const float* sc = gn_scale + (long long)n * Ci + cc * 64 + hc * 8;
+    const float* sh = gn_shift + (long long)n * Ci + cc * 64 + hc * 8;
+    const float4 s0 = *(const float4*)sc, s1 = *(const float4*)(sc + 4);
+    const float4 h0 = *(const float4*)sh, h1 = *(const float4*)(sh + 4);
+    gsc[0] = s0.x; gsc[1] = s0.y; gsc[2] = s0.z; gsc[3] = s0.w; gsc[4] = s1.x; gsc[5] = s1.y; gsc[6] = s1.z; gsc[7] = s1.w;
+    gsh[0] = h0.x; gsh[1] = h0.y; gsh[2] = h0.z; gsh[3] = h0.w; gsh[4] = h1.x; gsh[5] = h1.y; gsh[6] = h1.z; gsh[7] = h1.w;
+  };
+  // pixel of staging round i: full p in [0, 180), new p in [36, 180)
+  // (the thread index goes through an empty asm so the per-round pixel geometry is recomputed at each
+  // use instead of being hoisted out of the strip loop into ~40 long-lived registers, which spilled)
+  auto pix_of = [&](bool full, int i) __attribute__((always_inline)) {
+    const int t = opaque(tid);
+    return full ? (t + i * G::NTH) >> 3 : 2 * CH_W + ((t + i * G::NTH) >> 3);
+  };
+  auto halo_load = [&](bool full, int oh0, int cc) __attribute__((always_inline)) {
+    const int hc = opaque(tid) & 7;
+    const int nr = full ? G::ROUNDS : ROUNDS_NEW;
+#pragma unroll
+    for (int i = 0; i < G::ROUNDS; ++i) {
+      if (i < nr) {
+        const int p = min(pix_of(full, i), G::HPIX - 1);
+        const int hy = p / CH_W, hx = p - hy * CH_W;
+        const int ih = min(max(oh0 - 1 + hy, 0), H - 1), iw = min(max(ow0 - 1 + hx, 0), W - 1);
+        hreg[i] = *(const bf16x8*)(in + (((long long)n * H + ih) * W + iw) * Ci + cc * 64 + hc * 8);
+      }
+    }
+    gn_load(cc);
+  };
+  auto halo_store = [&](bool full, int oh0, int hb) __attribute__((always_inline)) {
+    bf16* img = halo + hb * G::HALO_ELEMS;
+    const int hc = opaque(tid) & 7;
+    const int nr = full ? G::ROUNDS : ROUNDS_NEW;
+#pragma unroll
+    for (int i = 0; i < G::ROUNDS; ++i) {
+      const int p = pix_of(full, i);
+      if (i < nr && p < G::HPIX) {
+        const int hy = p / CH_W, hx = p - hy * CH_W;
+        const int ih = oh0 - 1 + hy, iw = ow0 - 1 + hx;
+        if (!full && p >= 8 * CH_W) {
+          // rows 8,9 of the previous tile are rows 0,1 of this one: this thread is the only one that
+          // overwrites this 16-B slot, so moving it first needs no barrier
+          *(bf16x8*)(img + (p - 8 * CH_W) * G::PP + hc * 8) = *(const bf16x8*)(img + p * G::PP + hc * 8);
+        }
+        bf16x8 v = hreg[i];
+        if (ih < 0 || ih >= H || iw < 0 || iw >= W) {
+          v = (bf16x8){};
+        } else {
+#pragma unroll
+          for (int j = 0; j < 8; j += 2) {
+            const f32x2 x = {(float)v[j], (float)v[j + 1]};
+            f32x2 u = x * (f32x2){gsc[j], gsc[j + 1]} + (f32x2){gsh[j], gsh[j + 1]};
+            if (gn_silu) {
+              const f32x2 t = u * (f32x2){-1.4426950408889634f, -1.4426950408889634f};
+              const f32x2 d = (f32x2){__builtin_amdgcn_exp2f(t.x), __builtin_amdgcn_exp2f(t.y)} + (f32x2){1.f, 1.f};
+              u = u * (f32x2){__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y)};
+            }
+            v[j] = (bf16)u.x;
+            v[j + 1] = (bf16)u.y;
+          }
+        }
+        *(bf16x8*)(img + p * G::PP + hc * 8) = v;
+      }
+    }
+  };
+  // ---- weights: B fragment (ks, g) of step s = 16 B at wt[(wn*32 + g*16 + frow) * K + tap*Ci + cc*64 + ks*32 + fk*8]
+  const __amdgpu_buffer_rsrc_t rs_w =
+      __builtin_amdgcn_make_buffer_rsrc((void*)wt, 0, __builtin_amdgcn_readfirstlane(Co * K * 2), 0x00020000);
+  int vb[G::FN];
+#pragma unroll
+  for (int g = 0; g < G::FN; ++g) vb[g] = ((wn * (G::FN * 16) + g * 16 + frow) * K + fk * 8) * 2;
+  bf16x8 bq[2][2][G::FN];
+  auto bload = [&](int s, bf16x8 (&dst)[2][G::FN]) __attribute__((always_inline)) {
+    const int cc = s / 9, tap = s - cc * 9;
+    const int soff = __builtin_amdgcn_readfirstlane((tap * Ci + cc * 64) * 2);
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int g = 0; g < G::FN; ++g)
+        dst[ks][g] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rs_w, vb[g] + ks * 64, soff, 0));
+  };
+  bload(0, bq[0]);
+
+  // ---- tile 0 of the strip: chunk 0's full halo; chunk 1's full halo is staged at tap 8 of chunk 0
+  halo_load(true, 0, 0);
+  halo_store(true, 0, 0);
+  asm volatile("s_waitcnt vmcnt(0)\n\ts_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+
+  const int abase = frow * G::PP + fk * 8;
+  constexpr int RQ_PRE = G::ROUNDS < G::FM ? G::ROUNDS : G::FM;
+  const int cs = wn * (G::FN * 16) + (fk & 1) * 16 + (fk >> 1) * 8;  // the lane's 8-channel output run
+#pragma unroll 1
+  for (int ty = 0; ty < tiles_y; ++ty) {
+    const int oh0 = ty * 8;
+    const bool first = ty == 0, last = ty + 1 == tiles_y;
+    const long long pix0 = ((long long)n * H + oh0) * W + ow0 + frow;
+    f32x4 acc[G::FM][G::FN];  // bias-seeded (re-read per tile from L1: no registers held across tiles)
+#pragma unroll
+    for (int j = 0; j < G::FN; ++j) {
+      f32x4 b0 = (f32x4){0.f, 0.f, 0.f, 0.f};
+      if (bias) {
+        const float4 b = *(const float4*)(bias + wn * (G::FN * 16) + j * 16 + fk * 4);
+        b0 = (f32x4){b.x, b.y, b.z, b.w};
+      }
+#pragma unroll
+      for (int f = 0; f < G::FM; ++f) acc[f][j] = b0;
+    }
+#pragma unroll 1
+    for (int cc = 0; cc < nch; ++cc) {
+      const bf16* hcur = halo + cc * G::HALO_ELEMS + opaque(abase);
+      const bool more = cc + 1 < nch;
+#pragma unroll
+      for (int tap = 0; tap < 9; ++tap) {
+        const int s = cc * 9 + tap;
+        const int cur = tap & 1, nxt = cur ^ 1;
+        if (s + 1 < S) bload(s + 1, bq[nxt]);
+        else if (!last) bload(0, bq[nxt]);  // the next tile's first step: same weights
+        if (tap == 0 && more) halo_load(first, oh0, cc + 1);
+        if (tap == 0 && !more && residual) {
+#pragma unroll
+          for (int f = 0; f < RQ_PRE; ++f) hreg[f] = *(const bf16x8*)(residual + (pix0 + (long long)f * W) * Co + cs);
+        }
+        const int kh = tap / 3, kw = tap % 3;
+        bf16x8 fa[2][G::FM];
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+          for (int f = 0; f < G::FM; ++f)
+            fa[ks][f] = *(const bf16x8*)(hcur + ((f + kh) * CH_W + kw) * G::PP + ks * 32);
+        __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+          for (int f = 0; f < G::FM; ++f)
+#pragma unroll
+            for (int g = 0; g < G::FN; ++g)
+              acc[f][g] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bq[cur][ks][g], fa[ks][f], acc[f][g], 0, 0, 0);
+        __builtin_amdgcn_s_setprio(0);
+      }
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+        for (int g = 0; g < G::FN; ++g) bq[0][ks][g] = bq[1][ks][g];
+      if (more) {
+        // chunk 1's buffer: every wave finished the previous tile's chunk 1 before the tile-start
+        // barrier (for ty > 0 its rows 0,1 were refilled there)
+        halo_store(first, oh0, 1);
+        ch_lds_barrier();
+      }
+    }
+    // ---- register epilogue (as the register-B kernel)
+    bf16x8 rq[G::FM];
+    if (residual) {
+#pragma unroll
+      for (int f = 0; f < G::FM; ++f)
+        rq[f] = f < RQ_PRE ? hreg[f] : *(const bf16x8*)(residual + (pix0 + (long long)f * W) * Co + cs);
+    }
+    float sa = 0.f, sb = 0.f, qa = 0.f, qb = 0.f;
+#pragma unroll
+    for (int f = 0; f < G::FM; ++f) {
+      float v[8];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(acc[f][0][i]), __float_as_uint(acc[f][1][i]),
+                                                        false, false);
+        v[i] = __uint_as_float(r[0]);
+        v[4 + i] = __uint_as_float(r[1]);
+      }
+      if (residual) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] += (float)rq[f][e];
+      }
+      bf16x8 o;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) o[e] = (bf16)v[e];
+      *(bf16x8*)(out + (pix0 + (long long)f * W) * Co + cs) = o;
+      if (gn_part) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float q = (float)o[e], w2 = (float)o[4 + e];
+          sa += q;
+          qa += q * q;
+          sb += w2;
+          qb += w2 * w2;
+        }
+      }
+    }
+    if (gn_part) {
+      // Co = 128: GroupNorm(32) groups of 4 channels, two per lane
+      sa = row16_sum(sa);
+      qa = row16_sum(qa);
+      sb = row16_sum(sb);
+      qb = row16_sum(qb);
+      if (frow == 0) {
+        const long long t128 = (long long)n * (tiles_x * tiles_y) + ty * tiles_x + tx;
+        float* gp = gn_part + (t128 * 32 + cs / 4) * 2;
+        *(float2*)gp = make_float2(sa, qa);
+        *(float2*)(gp + 2) = make_float2(sb, qb);
+      }
+    }
+    if (!last) {
+      // next tile's chunk-0 halo (new rows 2..9; rows 0,1 moved inside LDS); chunk 1's new rows are
+      // loaded at tap 0 of the next tile's chunk 0 and stored after it, as in the single-tile kernel
+      halo_load(false, oh0 + 8, 0);
+      ch_lds_barrier();  // every wave is past its reads of this tile's halos
+      halo_store(false, oh0 + 8, 0);
+      ch_lds_barrier();
+    }
+  }
+}
+
+// =====================================================================================
 // Downsample conv (vaekl.py:59-72: F.pad(x, (0, 1, 0, 1)) then 3x3 / stride 2 / no padding) as a
 // halo-tile kernel.  Output tile 8 x 16 pixels x 128 channels, 256 threads, two workgroups per CU;
 // per 64-channel chunk the 17 x 33-pixel input halo (zero past the bottom / right edge = the pad)
@@ -1015,6 +1271,24 @@ extern "C" int uva_conv3x3_halo(const void* in, const void* w, void* out, const 
 #ifndef UVA_CONV_GN_VAR
 #define UVA_CONV_GN_VAR 64
 #endif
+#ifndef UVA_CONV_GN_STRIP
+#define UVA_CONV_GN_STRIP 0
+#endif
+  if (gn_scale && Ci == 128 && Co == 128 && (UVA_CONV_GN_STRIP)) {
+    // strip form (above): one workgroup per (image, tile column)
+    using GS = ConvHCfg<128, 8, false, false, true>;
+    static bool attr_s = false;
+    if (!attr_s) {
+      (void)hipFuncSetAttribute((const void*)conv3x3_gn_strip<0>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                GS::LDS_BYTES);
+      attr_s = true;
+    }
+    conv3x3_gn_strip<0><<<dim3((unsigned)(Nimg * (W / CH_T))), 256, GS::LDS_BYTES, stream>>>(
+        (const bf16*)in, (const bf16*)w, (bf16*)out, bias, (const bf16*)residual, gn_scale, gn_shift, gn_silu, gn_part,
+        Nimg, H, W);
+    UVA_LAUNCH_CHECK();
+    return 0;
+  }
   if (gn_scale) CH_LAUNCH(128, true, UVA_CONV_GN_VAR, 8);
   else CH_LAUNCH(128, false, 12, 8);
 #undef CH_LAUNCH
