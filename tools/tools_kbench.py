@@ -274,3 +274,29 @@ def conv0_bench():
 
 if __name__ == "__main__" and len(sys.argv) > 1 and sys.argv[1] == "conv0":
     conv0_bench()
+
+
+def blas_bench():
+    """This build's products vs hipBLASLt (torch.matmul) at the Block shapes, per transposition:
+    fwd x w^T, dX dy w (bf16 out both), dW dy^T x (this build: fp32 accumulate into the grad buffer;
+    hipBLASLt: bf16 out, the same FLOPs)."""
+    dev = "cuda"
+    M = 32 * 1024
+    for (N, K) in ((2304, 768), (768, 768), (3072, 768), (768, 3072)):
+        x = torch.randn(M, K, device=dev).to(torch.bfloat16)
+        w = torch.randn(N, K, device=dev).to(torch.bfloat16)
+        dy = torch.randn(M, N, device=dev).to(torch.bfloat16)
+        y = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+        dx = torch.empty(M, K, device=dev, dtype=torch.bfloat16)
+        dw = torch.zeros(N, K, device=dev)
+        fl = 2 * M * N * K
+        r = {}
+        r["fwd"] = (timeit(lambda: ops.linear(x, w, y)), timeit(lambda: torch.matmul(x, w.t())))
+        r["dx"] = (timeit(lambda: ops.linear_dx(dy, w, dx)), timeit(lambda: torch.matmul(dy, w)))
+        r["dw"] = (timeit(lambda: ops.linear_dw(dy, x, dw)), timeit(lambda: torch.matmul(dy.t(), x)))
+        print(f"M={M} N={N} K={K}: " + "  ".join(f"{k} {fl/a/1e9:.0f}/{fl/b/1e9:.0f}" for k, (a, b) in r.items())
+              + "  TF (this build / hipBLASLt)")
+
+
+if __name__ == "__main__" and len(sys.argv) > 1 and sys.argv[1] == "blas":
+    blas_bench()
