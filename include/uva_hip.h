@@ -67,6 +67,11 @@ int uva_gemm(int in_dtype, int out_dtype, int ta, int tb, const void* A, const v
  * 2 = MFMA LDS-DMA 128x128, 3 = MFMA 8-phase (256x256 or 128x384 tiles), splits = split-K slices. */
 long long uva_gemm_plan(int in_dtype, int ta, int tb, int M, int N, int K, int batch, int gn_prologue,
                         long long ws_floats);
+/* Persistent 8-phase form (gemm_8pp: one workgroup per CU walks full tiles; the next tile's first
+ * K-tiles are in flight under this tile's register epilogue) for eligible plain / bias / activation /
+ * dropout products: 1 on, 0 off (default: measured 1-4 % slower than gemm_8ph),
+ * -1 query.  Returns the previous setting. */
+int uva_gemm_set_persist(int on);
 int uva_conv2d(int dtype, const void* in, const void* w, void* out, const float* bias, const void* residual, int Nimg,
                int Hin, int Win, int Ci, int Co, int ks, int stride, int pad_t, int pad_l, int Hout, int Wout,
                const float* gn_scale, const float* gn_shift, int gn_silu, int act, float* gn_part,

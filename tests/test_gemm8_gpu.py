@@ -34,13 +34,26 @@ CASES = [(5376, 3072, 328, 256), (5000, 3000, 136, 256), (6144, 2048, 200, 256),
          # > 256 tiles: several rounds of workgroups (ragged M, K tail)
          (16296, 3072, 328, 256), (16384, 3072, 256, 256),
          # N = 768: the 128x384 tile (ragged M and K tail; full tiles on the fast path)
-         (32000, 768, 328, 384), (32768, 768, 3072, 384)]
+         (32000, 768, 328, 384), (32768, 768, 3072, 384),
+         # persistent form (gemm_8pp: full tiles, K % 64 == 0, K >= 128): 4.5 rounds of 256 workgroups
+         # (the last round half full), and fewer tiles than CUs with K = 128 (two K-tiles)
+         (32768, 2304, 768, 256), (4096, 2304, 128, 384)]
+
+
+@pytest.fixture(params=[False, True], ids=["8ph", "8pp"])
+def persist(request):
+    """every case on gemm_8ph and on the persistent gemm_8pp (used where the shape is eligible: full
+    tiles, K % 64 == 0, K >= 128, no row inputs in the epilogue)"""
+    from unified_video_action_amd.native import ops
+    prev = ops.gemm_set_persist(request.param)
+    yield request.param
+    ops.gemm_set_persist(prev)
 
 
 @pytest.mark.parametrize("odt", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("ta,tb", [(0, 0), (0, 1), (1, 0), (1, 1)])
 @pytest.mark.parametrize("M,N,K,bn", CASES)
-def test_gemm8_layouts(odt, ta, tb, M, N, K, bn):
+def test_gemm8_layouts(odt, ta, tb, M, N, K, bn, persist):
     from unified_video_action_amd.native import ops
     assert ops.gemm_plan(M, N, K, ta, tb) == (3, bn, 1)
     a = torch.randn(M, K, device=DEV).to(torch.bfloat16)
@@ -68,8 +81,8 @@ def test_gemm8_splitk_dw_accumulate(M, N, K, splits):
 
 
 @pytest.mark.parametrize("M,N,K,bn", [(5376, 3072, 256, 256), (16384, 3072, 256, 256),
-                                      (32000, 768, 328, 384), (32768, 768, 768, 384)])
-def test_gemm8_epilogues(M, N, K, bn):
+                                      (32000, 768, 328, 384), (32768, 768, 768, 384), (32768, 2304, 768, 256)])
+def test_gemm8_epilogues(M, N, K, bn, persist):
     from unified_video_action_amd.native import ops
     assert ops.gemm_plan(M, N, K) == (3, bn, 1)
     x = torch.randn(M, K, device=DEV).to(torch.bfloat16)

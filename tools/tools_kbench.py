@@ -291,12 +291,15 @@ def blas_bench():
         dw = torch.zeros(N, K, device=dev)
         fl = 2 * M * N * K
         r = {}
-        r["fwd"] = (timeit(lambda: ops.linear(x, w, y)), timeit(lambda: torch.matmul(x, w.t())))
-        r["dx"] = (timeit(lambda: ops.linear_dx(dy, w, dx)), timeit(lambda: torch.matmul(dy, w)))
+        r["fwd"] = (timeit(lambda: ops.linear(x, w, y), 60), timeit(lambda: torch.matmul(x, w.t()), 60))
+        r["dx"] = (timeit(lambda: ops.linear_dx(dy, w, dx), 60), timeit(lambda: torch.matmul(dy, w), 60))
         r["dw"] = (timeit(lambda: ops.linear_dw(dy, x, dw)), timeit(lambda: torch.matmul(dy.t(), x)))
         print(f"M={M} N={N} K={K}: " + "  ".join(f"{k} {fl/a/1e9:.0f}/{fl/b/1e9:.0f}" for k, (a, b) in r.items())
               + "  TF (this build / hipBLASLt)")
 
 
 if __name__ == "__main__" and len(sys.argv) > 1 and sys.argv[1] == "blas":
+    blas_bench()
+if __name__ == "__main__" and len(sys.argv) > 1 and sys.argv[1] == "blas_pp":
+    ops.gemm_set_persist(True)
     blas_bench()

@@ -1441,6 +1441,295 @@ __global__ __launch_bounds__(512, 1) void gemm_8ph(const bf16* __restrict__ A, c
   }
 }
 
+// UVA_GEMM_PERSIST: the default of the run-time switch uva_gemm_set_persist (0: gemm_8ph only, measured
+// faster; 1: gemm_8pp where eligible); diagnostic bits 2 (one tile per workgroup) and 4 (next tile's DMA
+// after the epilogue)
+#ifndef UVA_GEMM_PERSIST
+#define UVA_GEMM_PERSIST 0
+#endif
+static int g_gemm_persist = UVA_GEMM_PERSIST & 1;
+extern "C" int uva_gemm_set_persist(int on) {
+  const int prev = g_gemm_persist;
+  if (on >= 0) g_gemm_persist = on ? 1 : 0;
+  return prev;
+}
+// =====================================================================================
+// gemm_8pp -- persistent form of gemm_8ph (full tiles, K a multiple of 64 and >= 128, batch 1, no
+// K split; epilogue: alpha, bias, activation, dropout, pre-activation copy).  One workgroup per CU
+// walks tiles pid = i * grid + xcd_remap(block) (the GROUP-8 raster of gemm_8ph inside each round),
+// and at the end of a tile's K loop it
+//   1. issues the NEXT tile's first two K-tiles of LDS-DMA (the LDS images are free: the epilogue
+//      below runs from registers), then
+//   2. finishes this tile from registers: the MFMAs are issued with the operands swapped (B as the
+//      A operand), so a lane holds 4 consecutive output columns of one row, and one
+//      v_permlane16_swap per accumulator word pairs two fragments into 8 consecutive columns:
+//      16-B (bf16) / 2 x 16-B (fp32) row-segment stores, 64 contiguous bytes per row per instruction
+//      across a 16-lane row group.
+// The next tile then waits with a COUNTED vmcnt: its K-tile 0 DMAs are older than the E epilogue
+// stores, so vmcnt(2GA + 2GB + E) retires exactly K-tile 0 and leaves the stores draining under the
+// next K loop (E is the same in every wave: full tiles, unconditional stores).  gemm_8ph instead
+// serialises prologue DMA latency, the LDS-staged epilogue and its store drain with the MFMAs at one
+// workgroup per CU; hipBLASLt's fastest kernels at these shapes are persistent too (rocprofv3 names,
+// profiles/r04/ab_gemm_persist.txt).
+// =====================================================================================
+template <int TA, int TB, int BN, typename TC>
+__global__ __launch_bounds__(512, 1) void gemm_8pp(const bf16* __restrict__ A, const bf16* __restrict__ B,
+                                                   TC* __restrict__ C, int M, int N, int K, long long lda,
+                                                   long long ldb, long long ldc, EpiParams ep) {
+  using G = Gemm8Cfg<BN>;
+  static_assert(TA != 2 && TB != 2, "plain products only");
+  static_assert(G::FN % 2 == 0, "the permlane16 pairing joins two 16-column fragments");
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  bf16* lds = (bf16*)smem;
+  const int tm = M / G::BM, tn = N / BN, ntiles = tm * tn;
+  const int nt = K / 64;
+  const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int wr = wid / G::WN, wc = wid % G::WN;
+  const int w8 = __builtin_amdgcn_readfirstlane(wid);
+  const int grp = __builtin_amdgcn_readfirstlane(wid >> 2);
+  const int G_ = gridDim.x;
+  const int slot = xcd_remap(blockIdx.x, G_);
+  constexpr int GROUP = 8;
+  auto tile_of = [&](int pid, int& m0, int& n0) __attribute__((always_inline)) {
+    const int group = pid / (GROUP * tn), first_m = group * GROUP;
+    const int gsz = min(tm - first_m, GROUP);
+    m0 = (first_m + (pid % (GROUP * tn)) % gsz) * G::BM;
+    n0 = ((pid % (GROUP * tn)) / gsz) * BN;
+  };
+  ConvParams cp0{};
+  ConvRows cr0{};
+  unsigned offA[2][G::GA], offB[2][G::GB];
+  auto offsets = [&](int m0, int n0) __attribute__((always_inline)) {
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+#pragma unroll
+      for (int i = 0; i < G::GA; ++i)
+        offA[h][i] = (unsigned)((const char*)dma8_addr<TA, G::RWA, G::WA, G::GA>(A, lda, m0, M, 0, K, h, i, cp0, cr0) -
+                                (const char*)A);
+#pragma unroll
+      for (int i = 0; i < G::GB; ++i)
+        offB[h][i] = (unsigned)((const char*)dma8_addr<TB, G::RWB, G::WB, G::GB>(B, ldb, n0, N, 0, K, h, i, cp0, cr0) -
+                                (const char*)B);
+    }
+  };
+  const long long stepA = (TA == 1 ? 64 * lda : 64) * 2, stepB = (TB == 1 ? 64 * ldb : 64) * 2;  // bytes
+  const int nrA = __builtin_amdgcn_readfirstlane(
+      (int)(unsigned)min(2ull * (unsigned long long)(TA == 1 ? K : M) * (unsigned long long)lda, 0xffffffffull));
+  const int nrB = __builtin_amdgcn_readfirstlane(
+      (int)(unsigned)min(2ull * (unsigned long long)(TB == 1 ? K : N) * (unsigned long long)ldb, 0xffffffffull));
+  const auto rsA = __builtin_amdgcn_make_buffer_rsrc((void*)A, 0, nrA, 0x00020000);
+  const auto rsB = __builtin_amdgcn_make_buffer_rsrc((void*)B, 0, nrB, 0x00020000);
+  auto img_a = [&](int buf, int h) { return lds + buf * G::STAGE + h * G::A_HALF; };
+  auto img_b = [&](int buf, int h) { return lds + buf * G::STAGE + 2 * G::A_HALF + h * G::B_HALF; };
+  auto stage = [&](auto qc, int t) __attribute__((always_inline)) {
+    constexpr int q = decltype(qc)::value;
+    const int buf = t & 1;
+    if constexpr (q == 0 || q == 3) {
+      constexpr int h = q == 0 ? 0 : 1;
+      bf16* img = img_a(buf, h);
+      const int so = (int)(unsigned)(t * stepA);
+#pragma unroll
+      for (int i = 0; i < G::GA; ++i)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rsA, (__attribute__((address_space(3))) void*)(img + (w8 * G::GA + i) * 512),
+                                                 16, (int)offA[h][i], so, 0, 0);
+    } else {
+      constexpr int h = q - 1;
+      bf16* img = img_b(buf, h);
+      const int so = (int)(unsigned)(t * stepB);
+#pragma unroll
+      for (int i = 0; i < G::GB; ++i)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rsB, (__attribute__((address_space(3))) void*)(img + (w8 * G::GB + i) * 512),
+                                                 16, (int)offB[h][i], so, 0, 0);
+    }
+  };
+  using Q0 = std::integral_constant<int, 0>;
+  using Q1 = std::integral_constant<int, 1>;
+  using Q2 = std::integral_constant<int, 2>;
+  using Q3 = std::integral_constant<int, 3>;
+  auto stage01 = [&]() __attribute__((always_inline)) {
+    stage(Q1{}, 0);
+    stage(Q0{}, 0);
+    stage(Q2{}, 0);
+    stage(Q3{}, 0);
+    stage(Q1{}, 1);
+    stage(Q0{}, 1);
+    stage(Q2{}, 1);
+    stage(Q3{}, 1);
+  };
+  // epilogue vector-memory instructions per wave (every one unconditional), for the counted wait
+  constexpr int E1 = G::FM * (G::FN / 2) * (sizeof(TC) == 2 ? 1 : 2);
+  constexpr int W0 = 2 * G::GA + 2 * G::GB;
+  constexpr int WE = (W0 + E1) > 63 ? 63 : (W0 + E1), WEA = (W0 + 2 * E1) > 63 ? 63 : (W0 + 2 * E1);
+  const bool has_aux = ep.aux != nullptr;
+
+  int pid = slot;
+  if (pid >= ntiles) return;
+  int m0, n0;
+  tile_of(pid, m0, n0);
+  offsets(m0, n0);
+  stage01();
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(W0) : "memory");
+  bool first = true;
+  const int li = lane & 15, g4 = lane >> 4;
+  const int csub = (g4 & 1) * 16 + (g4 >> 1) * 8;  // the lane's 8 columns inside a 32-column fragment pair
+  for (;;) {
+    if (!first) {
+      // K-tile 0 of this tile was issued before the previous tile's E epilogue stores
+      if constexpr ((UVA_GEMM_PERSIST & 4) != 0) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(W0) : "memory");
+      else if (has_aux) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(WEA) : "memory");
+      else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(WE) : "memory");
+    }
+    first = false;
+    f32x4 acc[G::FM][G::FN];
+#pragma unroll
+    for (int i = 0; i < G::FM; ++i)
+#pragma unroll
+      for (int j = 0; j < G::FN; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    bf16x8 fa[G::HA][2], fb0[G::HB][2], fb1[G::HB][2];
+#pragma unroll
+    for (int g = 0; g < G::HB; ++g)
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) fb0[g][ks] = frag8<TB, G::WB>(img_b(0, 0), wc * (G::RWB / 2) + g * 16, ks);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if (grp == 1) __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+
+#define GEMM8P_QUAD(AH, BH, FB)                                                                           \
+  __builtin_amdgcn_s_setprio(1);                                                                          \
+  _Pragma("unroll") for (int f = 0; f < G::HA; ++f)                                                       \
+  _Pragma("unroll") for (int g = 0; g < G::HB; ++g)                                                       \
+  _Pragma("unroll") for (int ks = 0; ks < 2; ++ks)                                                        \
+    acc[AH * G::HA + f][BH * G::HB + g] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(                       \
+        FB[g][ks], fa[f][ks], acc[AH * G::HA + f][BH * G::HB + g], 0, 0, 0);                              \
+  __builtin_amdgcn_s_setprio(0)
+#define GEMM8P_BEGIN()                                  \
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");    \
+  asm volatile("" ::: "memory");                        \
+  __builtin_amdgcn_s_barrier();                         \
+  __builtin_amdgcn_sched_barrier(0)
+#define GEMM8P_END()            \
+  __builtin_amdgcn_s_barrier(); \
+  asm volatile("" ::: "memory")
+
+    float bv[G::FN / 2][8];
+    for (int t = 0; t < nt; ++t) {
+      const int buf = t & 1;
+      const bool pf = t + 2 < nt;
+      // phase 0: read A-h0 ; DMA B-h0(t+2) ; MFMA (A0, B0)
+#pragma unroll
+      for (int f = 0; f < G::HA; ++f)
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) fa[f][ks] = frag8<TA, G::WA>(img_a(buf, 0), wr * (G::RWA / 2) + f * 16, ks);
+      if (pf) stage(Q1{}, t + 2);
+      if (t == nt - 1) {
+        // the epilogue's bias columns, a K-tile ahead of their use (retired by phase 2's vmcnt(0))
+#pragma unroll
+        for (int p = 0; p < G::FN / 2; ++p) epi_load_bias8(ep, n0 + wc * G::RWB + p * 32 + csub, bv[p]);
+      }
+      GEMM8P_BEGIN();
+      GEMM8P_QUAD(0, 0, fb0);
+      GEMM8P_END();
+      // phase 1: read B-h1 ; DMA A-h0(t+2) ; MFMA (A0, B1)
+#pragma unroll
+      for (int g = 0; g < G::HB; ++g)
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) fb1[g][ks] = frag8<TB, G::WB>(img_b(buf, 1), wc * (G::RWB / 2) + g * 16, ks);
+      if (pf) stage(Q0{}, t + 2);
+      GEMM8P_BEGIN();
+      GEMM8P_QUAD(0, 1, fb1);
+      GEMM8P_END();
+      // phase 2: read A-h1 ; DMA B-h1(t+2) ; retire tile t+1 ; MFMA (A1, B0)
+#pragma unroll
+      for (int f = 0; f < G::HA; ++f)
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) fa[f][ks] = frag8<TA, G::WA>(img_a(buf, 1), wr * (G::RWA / 2) + f * 16, ks);
+      if (pf) {
+        stage(Q2{}, t + 2);
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(G::GA + 2 * G::GB) : "memory");
+      } else {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      GEMM8P_BEGIN();
+      GEMM8P_QUAD(1, 0, fb0);
+      GEMM8P_END();
+      // phase 3: read B-h0 of tile t+1 ; DMA A-h1(t+2) ; MFMA (A1, B1)
+      if (t + 1 < nt) {
+#pragma unroll
+        for (int g = 0; g < G::HB; ++g)
+#pragma unroll
+          for (int ks = 0; ks < 2; ++ks)
+            fb0[g][ks] = frag8<TB, G::WB>(img_b(buf ^ 1, 0), wc * (G::RWB / 2) + g * 16, ks);
+      }
+      if (pf) stage(Q3{}, t + 2);
+      GEMM8P_BEGIN();
+      GEMM8P_QUAD(1, 1, fb1);
+      GEMM8P_END();
+    }
+#undef GEMM8P_QUAD
+#undef GEMM8P_BEGIN
+#undef GEMM8P_END
+    if (grp == 0) __builtin_amdgcn_s_barrier();  // re-align: every wave has retired its last LDS read
+    asm volatile("" ::: "memory");
+
+    const int cm0 = m0, cn0 = n0;
+    // ---- next tile: its first two K-tiles go out now, under this tile's epilogue.  After the last
+    //      tile the current one is restaged instead (drained before the exit): an issue that depends on
+    //      a branch leaves a join in front of the epilogue, where hipcc's wait-count merge would make
+    //      the bias wait drain the DMAs too
+    pid += G_;
+    const bool more = pid < ntiles;
+    if (more) {
+      tile_of(pid, m0, n0);
+      offsets(m0, n0);
+    }
+    if constexpr (!(UVA_GEMM_PERSIST & 4)) stage01();
+    asm volatile("" ::: "memory");
+    // ---- register epilogue (no LDS): 8 consecutive columns per lane per fragment pair
+    EpiRow none;
+#pragma unroll
+    for (int i = 0; i < G::FM; ++i) {
+      const int row = cm0 + wr * G::RWA + i * 16 + li;
+#pragma unroll
+      for (int p = 0; p < G::FN / 2; ++p) {
+        float v[8];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const auto x = __builtin_amdgcn_permlane16_swap(__float_as_uint(acc[i][2 * p][r]),
+                                                          __float_as_uint(acc[i][2 * p + 1][r]), false, false);
+          v[r] = __uint_as_float(x[0]);
+          v[4 + r] = __uint_as_float(x[1]);
+        }
+        const int col = cn0 + wc * G::RWB + p * 32 + csub;
+        float o[8];
+        epi_apply_row8<TC>(C, (long long)row * ldc + col, ep, bv[p], none, row, col, 0, M, N, v, o);
+      }
+    }
+    if constexpr ((UVA_GEMM_PERSIST & 4) != 0) {  // diagnostic: next tile's DMA after the epilogue
+      asm volatile("" ::: "memory");
+      stage01();
+    }
+    if (!more) break;
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the restaged DMAs land before the LDS is released
+}
+
+// number of compute units of the current device (persistent grids)
+static int device_cus() {
+  static int n = 0;
+  if (n == 0) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
+  }
+  return n;
+}
+
 template <typename TC>
 __global__ __launch_bounds__(256) void splitk_reduce(const float* __restrict__ part, int splits, TC* __restrict__ C,
                                                      int M, int N, long long ldc, EpiParams ep) {
@@ -1591,7 +1880,6 @@ static Plan8 plan_8ph(int ta, int M, int N, int K, int batch, bool gn_prologue, 
   return p;
 }
 
-// gemm_8pp routing: -1 = from UVA_8PP (default 0), 0 off, 1 on (uva_gemm_set_8pp)
 // 8-phase 256-row kernel: returns 1 if launched, 0 if the shape is not for it, <0 on error
 template <typename TC>
 static int launch_8ph(int ta, int tb, const void* A, const void* B, void* C, int M, int N, int K, long long lda,
@@ -1620,6 +1908,25 @@ static int launch_8ph(int ta, int tb, const void* A, const void* B, void* C, int
   };
   const bool fast = ta != 2 && M % (bn == 384 ? 128 : 256) == 0 && N % bn == 0 && K % 64 == 0 && batch == 1 &&
                     span(ta, M, K, lda) < 4.0e9 && span(tb, N, K, ldb) < 4.0e9;
+  // persistent form (gemm_8pp): full tiles, one K range, an epilogue without row inputs
+  const bool persist = g_gemm_persist && fast && splits == 1 && K >= 128 && ep.residual == nullptr &&
+                       ep.gate == nullptr && ep.beta == 0.f && ep.res_grad == 0 && ldc % 8 == 0 &&
+                       (((uintptr_t)C | (uintptr_t)ep.aux | (uintptr_t)ep.bias) % 16) == 0;
+  if (persist) {
+    // (UVA_GEMM_PERSIST & 2: diagnostic, one tile per workgroup)
+    const unsigned g = (UVA_GEMM_PERSIST & 2) ? (unsigned)nblk : (unsigned)std::min<long long>(nblk, (long long)device_cus());
+#define G8P(a, b, BNV)                                                                                        do {                                                                                                          static bool attr = false;                                                                                   const int lb = Gemm8Cfg<BNV>::LDS_BYTES;                                                                    if (!attr) {                                                                                                  (void)hipFuncSetAttribute((const void*)gemm_8pp<a, b, BNV, TC>, hipFuncAttributeMaxDynamicSharedMemorySize, lb);       attr = true;                                                                                              }                                                                                                           gemm_8pp<a, b, BNV, TC><<<dim3(g), 512, lb, s>>>((const bf16*)A, (const bf16*)B, (TC*)C, M, N, K, lda, ldb, ldc, ep);   } while (0)
+#define G8PC(a, b) do { if (bn == 384) G8P(a, b, 384); else G8P(a, b, 256); } while (0)
+    if (ta == 0 && tb == 0) G8PC(0, 0);
+    else if (ta == 0 && tb == 1) G8PC(0, 1);
+    else if (ta == 1 && tb == 0) G8PC(1, 0);
+    else if (ta == 1 && tb == 1) G8PC(1, 1);
+    else return -(int)hipErrorInvalidValue;
+#undef G8PC
+#undef G8P
+    UVA_LAUNCH_CHECK();
+    return 1;
+  }
 #define G8(a, b, BNV) do { if (fast) G8X(a, b, BNV, 256); else G8X(a, b, BNV, 0); } while (0)
 #define G8B(a, b) G8(a, b, 256)
 #define G8C(a, b) do { if (bn == 384) G8(a, b, 384); else G8B(a, b); } while (0)

@@ -84,6 +84,12 @@ def gemm_plan(M, N, K, ta=0, tb=0, batch=1, splitk=True, gn_prologue=False, dtyp
     return code & 15, (code >> 4) & 4095, code >> 16
 
 
+def gemm_set_persist(on):
+    """route eligible full-tile products to the persistent gemm_8pp (True) or gemm_8ph (False);
+    returns the previous setting (tests / kernel benchmarks)"""
+    return bool(lib().query("uva_gemm_set_persist", int(bool(on))))
+
+
 def linear(x, w, out, bias=None, act="none", aux=None, residual=None, drop_p=0.0, seed=0, beta=0.0, gate=None):
     """out[M,N] = epi(x[M,K] @ w[N,K]^T) -- nn.Linear forward."""
     M, K = x.shape
