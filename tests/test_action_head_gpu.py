@@ -125,7 +125,9 @@ def test_im2col_tap_major_and_dw_scatter_add(dtype):
 
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
-@pytest.mark.parametrize("M,N,K", [(16, 4, 49152), (64, 2, 20000), (4, 16, 8192)])
+@pytest.mark.parametrize("M,N,K", [(16, 4, 49152), (64, 2, 20000), (4, 16, 8192),
+                                   # z_proj / DiffLoss input_proj dW: MFMA split-K with up to 128 slices
+                                   (768, 16, 65536), (1024, 16, 32768)])
 def test_generic_gemm_splitk_tiny_output_long_k(dtype, M, N, K):
     """dW of the frame interpolation: [M, N] (+)= dY^T X over K rows; beta = 1 accumulates."""
     from unified_video_action_amd.native import ops

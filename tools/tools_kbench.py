@@ -303,3 +303,18 @@ if __name__ == "__main__" and len(sys.argv) > 1 and sys.argv[1] == "blas":
 if __name__ == "__main__" and len(sys.argv) > 1 and sys.argv[1] == "blas_pp":
     ops.gemm_set_persist(True)
     blas_bench()
+
+
+def skinny_bench():
+    """skinny-output dW products (z_proj [768 x 16], DiffLoss input_proj [1024 x 16]) over K = tokens"""
+    dev = "cuda"
+    for (M, N, K) in ((768, 16, 65536), (1024, 16, 65536), (768, 16, 32768)):
+        dy = torch.randn(K, M, device=dev).to(torch.bfloat16)
+        x = torch.randn(K, N, device=dev).to(torch.bfloat16)
+        dw = torch.zeros(M, N, device=dev)
+        t = timeit(lambda: ops.linear_dw(dy, x, dw), 50)
+        print(f"skinny dW M={M} N={N} K={K}: {t*1e3:.1f} us  {K*M*2/t/1e6:.0f} GB/s of dY  plan {ops.gemm_plan(M, N, K, 1, 1)}")
+
+
+if __name__ == "__main__" and len(sys.argv) > 1 and sys.argv[1] == "skinny":
+    skinny_bench()

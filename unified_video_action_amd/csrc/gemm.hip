@@ -1967,7 +1967,11 @@ static int launch_mfma(int ta, int tb, const void* A, const void* B, void* C, in
     splits = (512 + nblk - 1) / nblk;
     int kmax = K / (minks * MB_K);
     if (splits > kmax) splits = kmax;
-    if (splits > 16) splits = 16;
+    // skinny outputs (the z_proj / DiffLoss input_proj dW, [768 | 1024] x 16 over K = tokens): the
+    // few 128x128 tiles need many more K slices to fill the chip (16 slices: 96 workgroups, 96 us for
+    // 100 MB of dY; the partial slabs stay small)
+    const int scap = (N <= 64 || M <= 64) ? 128 : 16;
+    if (splits > scap) splits = scap;
     while (splits > 1 && (long long)splits * M * N > ws_floats) --splits;
   }
   int kps = K;
