@@ -129,6 +129,12 @@ __device__ __forceinline__ void conv_vm_wait(int n) {
 // (non-GN; no register staging, zeros from the buffer descriptor's range check).  Compile-time
 // alternatives measured slower and not built: 16 the next chunk's halo staging spread over taps
 // 1..ROUNDS; 2 one halo buffer + a 3-slot weight ring.
+#ifndef UVA_CONV_ILV_T0
+#define UVA_CONV_ILV_T0 2      // ILV: first tap that stages a round (the halo loads issue at tap 0)
+#endif
+#ifndef UVA_CONV_ILV_RATIO
+#define UVA_CONV_ILV_RATIO 2   // ILV: staging VALU instructions placed after each MFMA
+#endif
 template <int BN, bool GN, int VAR, int TR>
 __global__ __launch_bounds__(TR * 32, 16 / TR) void conv3x3_halo(const bf16* __restrict__ in, const bf16* __restrict__ wt,
                                                        bf16* __restrict__ out, const float* __restrict__ bias,
@@ -150,6 +156,11 @@ __global__ __launch_bounds__(TR * 32, 16 / TR) void conv3x3_halo(const bf16* __r
   // (otherwise every tap opens with the latency of its first reads: the 16 fragment registers are
   // reused tap after tap and hipcc issues the next tap's reads only after the last MFMA)
   constexpr bool PIPE = RB && (VAR & 128) != 0;
+  // ILV (RB only): the next chunk's GN + SiLU staging is cut into its ROUNDS rounds, one per tap
+  // 2..ROUNDS+1, each interleaved instruction by instruction with that tap's 32 MFMAs
+  // (sched_group_barrier), so the staging VALU issues in the MFMAs' shadow instead of as a burst
+  // after tap 8 (PMC: VALU and MFMA co-execute in 2-3 % of the cycles with the burst)
+  constexpr bool ILV = RB && !PIPE && (VAR & 1024) != 0;
   static_assert(!SPREAD || ConvHCfg<BN, TR>::ROUNDS <= 8, "one staging round per tap 1..8");
   static_assert(!RB || TR == 8, "the register epilogue writes one 128-pixel GroupNorm unit per tile");
   using G = ConvHCfg<BN, TR, R3, HD, RB>;
@@ -239,6 +250,29 @@ __global__ __launch_bounds__(TR * 32, 16 / TR) void conv3x3_halo(const bf16* __r
   auto halo_store = [&](int hb) __attribute__((always_inline)) {
 #pragma unroll
     for (int i = 0; i < G::ROUNDS; ++i) halo_store_round(hb, i);
+  };
+  // ILV: the same round without branches (one basic block with the MFMAs it is interleaved with):
+  // out-of-image pixels by select, the pixel index clamped (a clamped thread rewrites pixel HPIX-1
+  // with the value its owner stores), SiLU by a uniform select
+  auto halo_store_round_bf = [&](int hb, int i) __attribute__((always_inline)) {
+    bf16* img = halo + hb * G::HALO_ELEMS;
+    const int p = min((tid + i * G::NTH) >> 3, G::HPIX - 1);
+    const int hy = p / CH_W, hx = p - hy * CH_W;
+    const int ih = oh0 - 1 + hy, iw = ow0 - 1 + hx;
+    const bool inb = ih >= 0 && ih < H && iw >= 0 && iw < W;
+    bf16x8 v = hreg[i];
+#pragma unroll
+    for (int j = 0; j < 8; j += 2) {
+      const f32x2 x = {(float)v[j], (float)v[j + 1]};
+      const f32x2 u = x * (f32x2){gsc[j], gsc[j + 1]} + (f32x2){gsh[j], gsh[j + 1]};
+      const f32x2 t = u * (f32x2){-1.4426950408889634f, -1.4426950408889634f};
+      const f32x2 d = (f32x2){__builtin_amdgcn_exp2f(t.x), __builtin_amdgcn_exp2f(t.y)} + (f32x2){1.f, 1.f};
+      const f32x2 us = u * (f32x2){__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y)};
+      const float a = gn_silu ? us.x : u.x, b = gn_silu ? us.y : u.y;
+      v[j] = inb ? (bf16)a : (bf16)0.f;
+      v[j + 1] = inb ? (bf16)b : (bf16)0.f;
+    }
+    *(bf16x8*)(img + p * G::PP + hc * 8) = v;
   };
 
   // ---- HD: halo by LDS-DMA through a per-image buffer descriptor. LDS pixel block b (8 pixels)
@@ -349,6 +383,64 @@ __global__ __launch_bounds__(TR * 32, 16 / TR) void conv3x3_halo(const bf16* __r
     static_assert(G::FN == 2, "the permlane16 pairing joins the wave's two 16-channel fragments");
     const long long pix0 = ((long long)n * H + oh0) * W + ow0 + frow;  // pixel (row 0, column frow)
     const int c0 = n0 + wn * (G::FN * 16) + fk * 4;
+    auto chunk_ilv = [&](int cc, auto stc) __attribute__((always_inline)) {
+      constexpr bool STG = decltype(stc)::value;  // a next chunk exists: stage it under these taps
+      const bf16* hcur = halo + (cc & 1) * G::HALO_ELEMS + abase;
+#pragma unroll
+      for (int tap = 0; tap < 9; ++tap) {
+        const int s = cc * 9 + tap;
+        const int cur = tap & 1, nxt = cur ^ 1;
+        // unconditional (the last step reloads its own fragments): no branch join before the
+        // staging's first use of hreg, where hipcc's merged wait count would drain this load too
+        bload(s + 1 < S ? s + 1 : s, bq[nxt]);
+        if constexpr (STG) {
+          if (tap == 0) halo_load(cc + 1);
+        } else {
+          if (tap == 0 && residual) {
+            const int csr = n0 + wn * (G::FN * 16) + (fk & 1) * 16 + (fk >> 1) * 8;
+#pragma unroll
+            for (int f = 0; f < RQ_PRE; ++f) hreg[f] = *(const bf16x8*)(residual + (pix0 + (long long)f * W) * Co + csr);
+          }
+        }
+        const int kh = tap / 3, kw = tap % 3;
+        bf16x8 fa[2][G::FM];
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+          for (int f = 0; f < G::FM; ++f)
+            fa[ks][f] = *(const bf16x8*)(hcur + ((f + kh) * CH_W + kw) * G::PP + ks * 32);
+        __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+          for (int f = 0; f < G::FM; ++f)
+#pragma unroll
+            for (int g = 0; g < G::FN; ++g)
+              acc[f][g] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bq[cur][ks][g], fa[ks][f], acc[f][g], 0, 0, 0);
+        if constexpr (STG) {
+          if (tap >= UVA_CONV_ILV_T0 && tap - UVA_CONV_ILV_T0 < G::ROUNDS) {
+            halo_store_round_bf((cc + 1) & 1, tap - UVA_CONV_ILV_T0);
+#pragma unroll
+            for (int k = 0; k < 28; ++k) {
+              __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);                  // one MFMA
+              __builtin_amdgcn_sched_group_barrier(0x002, UVA_CONV_ILV_RATIO, 0);  // VALU of the staging round
+            }
+            __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
+          }
+        }
+        __builtin_amdgcn_s_setprio(0);
+      }
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+        for (int g = 0; g < G::FN; ++g) bq[0][ks][g] = bq[1][ks][g];
+      if constexpr (STG) ch_lds_barrier();
+    };
+    if constexpr (ILV) {
+      int cc = 0;
+      for (; cc + 1 < nch; ++cc) chunk_ilv(cc, std::true_type{});
+      chunk_ilv(cc, std::false_type{});
+    } else
     for (int cc = 0; cc < nch; ++cc) {
       const bf16* hcur = halo + (cc & 1) * G::HALO_ELEMS + abase;
       const bool more = cc + 1 < nch;
@@ -1269,7 +1361,7 @@ extern "C" int uva_conv3x3_halo(const void* in, const void* w, void* out, const 
   // bias + residual + GN-stats epilogue, 7.02 -> 6.79 ms in the bench).  The other VAR bits are the
   // measured-slower alternatives, compile-time only and not built.
 #ifndef UVA_CONV_GN_VAR
-#define UVA_CONV_GN_VAR 64
+#define UVA_CONV_GN_VAR 1088
 #endif
 #ifndef UVA_CONV_GN_STRIP
 #define UVA_CONV_GN_STRIP 0
