@@ -1101,6 +1101,252 @@ __global__ __launch_bounds__(256, 2) void conv3x3_gn_strip(const bf16* __restric
 }
 
 // =====================================================================================
+// GN conv, persistent form (PT; Ci = Co = 128): 2 workgroups per CU walk tiles
+// pid = i * grid + xcd_remap(block).  The register-B / interleaved-staging tile body of
+// conv3x3_halo, plus: during a tile's LAST chunk the NEXT tile's chunk 0 is loaded (tap 0) and its
+// GN + SiLU staging interleaved with the MFMAs (taps 2..7) into halo buffer 0 -- free since chunk 0's
+// barrier -- so a tile starts with its halo already in LDS instead of the load-latency + staging
+// burst + barrier every single-tile workgroup opens with.  The residual rows reuse the staging
+// registers as they free up (row r at tap 3 + r; rows 6, 7 in the GroupNorm scale registers at tap
+// 8).  After the grid's last tile the current tile is restaged (harmless: nothing reads it).
+// =====================================================================================
+__global__ __launch_bounds__(256, 2) void conv3x3_gn_pt(const bf16* __restrict__ in, const bf16* __restrict__ wt,
+                                                        bf16* __restrict__ out, const float* __restrict__ bias,
+                                                        const bf16* __restrict__ residual,
+                                                        const float* __restrict__ gn_scale,
+                                                        const float* __restrict__ gn_shift, int gn_silu,
+                                                        float* __restrict__ gn_part, int Nimg, int H, int W) {
+  using G = ConvHCfg<128, 8, false, false, true>;
+  constexpr int Ci = 128, Co = 128, S = 18, K = 9 * Ci;
+  static_assert(G::ROUNDS == 6 && G::FM == 8 && G::FN == 2, "tile geometry of the register-B body");
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  bf16* halo = (bf16*)smem;
+  const int tiles_x = W / CH_T, tiles_y = H / 8, ntiles = Nimg * tiles_x * tiles_y;
+  const int G_ = gridDim.x;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wn = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int frow = lane & 15, fk = lane >> 4;
+  // the thread index goes through an empty asm at each use: otherwise hipcc hoists every round's
+  // pixel geometry (and the residual row addresses) out of the tile loop into long-lived registers
+  auto opaque = [](int v) __attribute__((always_inline)) {
+    asm volatile("" : "+v"(v));
+    return v;
+  };
+  struct Tile {
+    int n, oh0, ow0;
+  };
+  auto tile_of = [&](int pid) __attribute__((always_inline)) {
+    Tile t;
+    const int tx = pid % tiles_x, ty = (pid / tiles_x) % tiles_y;
+    t.n = pid / (tiles_x * tiles_y);
+    t.oh0 = ty * 8;
+    t.ow0 = tx * CH_T;
+    return t;
+  };
+  bf16x8 hreg[G::ROUNDS];
+  float gsc[8], gsh[8];
+  auto halo_load = [&](const Tile& t, int cc) __attribute__((always_inline)) {
+    const int tid = opaque(threadIdx.x), hc = tid & 7;
+#pragma unroll
+    for (int i = 0; i < G::ROUNDS; ++i) {
+      const int p = min((tid + i * G::NTH) >> 3, G::HPIX - 1);
+      const int hy = p / CH_W, hx = p - hy * CH_W;
+      const int ih = min(max(t.oh0 - 1 + hy, 0), H - 1), iw = min(max(t.ow0 - 1 + hx, 0), W - 1);
+      hreg[i] = *(const bf16x8*)(in + (((long long)t.n * H + ih) * W + iw) * Ci + cc * 64 + hc * 8);
+    }
+    const float* sc = gn_scale + (long long)t.n * Ci + cc * 64 + hc * 8;
+    const float* sh = gn_shift + (long long)t.n * Ci + cc * 64 + hc * 8;
+    const float4 s0 = *(const float4*)sc, s1 = *(const float4*)(sc + 4);
+    const float4 h0 = *(const float4*)sh, h1 = *(const float4*)(sh + 4);
+    gsc[0] = s0.x; gsc[1] = s0.y; gsc[2] = s0.z; gsc[3] = s0.w; gsc[4] = s1.x; gsc[5] = s1.y; gsc[6] = s1.z; gsc[7] = s1.w;
+    gsh[0] = h0.x; gsh[1] = h0.y; gsh[2] = h0.z; gsh[3] = h0.w; gsh[4] = h1.x; gsh[5] = h1.y; gsh[6] = h1.z; gsh[7] = h1.w;
+  };
+  // branch-free staging round (as conv3x3_halo's ILV round)
+  auto stage_round = [&](const Tile& t, int hb, int i) __attribute__((always_inline)) {
+    const int tid = opaque(threadIdx.x), hc = tid & 7;
+    bf16* img = halo + hb * G::HALO_ELEMS;
+    const int p = min((tid + i * G::NTH) >> 3, G::HPIX - 1);
+    const int hy = p / CH_W, hx = p - hy * CH_W;
+    const int ih = t.oh0 - 1 + hy, iw = t.ow0 - 1 + hx;
+    const bool inb = ih >= 0 && ih < H && iw >= 0 && iw < W;
+    bf16x8 v = hreg[i];
+#pragma unroll
+    for (int j = 0; j < 8; j += 2) {
+      const f32x2 x = {(float)v[j], (float)v[j + 1]};
+      const f32x2 u = x * (f32x2){gsc[j], gsc[j + 1]} + (f32x2){gsh[j], gsh[j + 1]};
+      const f32x2 tt = u * (f32x2){-1.4426950408889634f, -1.4426950408889634f};
+      const f32x2 d = (f32x2){__builtin_amdgcn_exp2f(tt.x), __builtin_amdgcn_exp2f(tt.y)} + (f32x2){1.f, 1.f};
+      const f32x2 us = u * (f32x2){__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y)};
+      const float a = gn_silu ? us.x : u.x, b = gn_silu ? us.y : u.y;
+      v[j] = inb ? (bf16)a : (bf16)0.f;
+      v[j + 1] = inb ? (bf16)b : (bf16)0.f;
+    }
+    *(bf16x8*)(img + p * G::PP + hc * 8) = v;
+  };
+  const __amdgpu_buffer_rsrc_t rs_w =
+      __builtin_amdgcn_make_buffer_rsrc((void*)wt, 0, __builtin_amdgcn_readfirstlane(Co * K * 2), 0x00020000);
+  int vb[G::FN];
+#pragma unroll
+  for (int g = 0; g < G::FN; ++g) vb[g] = ((wn * (G::FN * 16) + g * 16 + frow) * K + fk * 8) * 2;
+  bf16x8 bq[2][2][G::FN];
+  auto bload = [&](int s, bf16x8 (&dst)[2][G::FN]) __attribute__((always_inline)) {
+    const int cc = s / 9, tap = s - cc * 9;
+    const int soff = __builtin_amdgcn_readfirstlane((tap * Ci + cc * 64) * 2);
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int g = 0; g < G::FN; ++g)
+        dst[ks][g] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rs_w, vb[g] + ks * 64, soff, 0));
+  };
+  const int abase = frow * G::PP + fk * 8;
+  const int cs = wn * (G::FN * 16) + (fk & 1) * 16 + (fk >> 1) * 8;  // the lane's 8-channel output run
+
+  int pid = ch_xcd_remap(blockIdx.x, G_);
+  if (pid >= ntiles) return;
+  Tile cur = tile_of(pid);
+  bload(0, bq[0]);
+  halo_load(cur, 0);
+#pragma unroll
+  for (int i = 0; i < G::ROUNDS; ++i) stage_round(cur, 0, i);
+  asm volatile("s_waitcnt vmcnt(0)\n\ts_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+
+  for (;;) {
+    const int npid = pid + G_;
+    const bool more = npid < ntiles;
+    const Tile nxt = tile_of(more ? npid : pid);
+    const long long pix0 = ((long long)cur.n * H + cur.oh0) * W + cur.ow0 + frow;
+    f32x4 acc[G::FM][G::FN];
+#pragma unroll
+    for (int j = 0; j < G::FN; ++j) {
+      f32x4 b0 = (f32x4){0.f, 0.f, 0.f, 0.f};
+      if (bias) {
+        const float4 b = *(const float4*)(bias + wn * (G::FN * 16) + j * 16 + fk * 4);
+        b0 = (f32x4){b.x, b.y, b.z, b.w};
+      }
+#pragma unroll
+      for (int f = 0; f < G::FM; ++f) acc[f][j] = b0;
+    }
+    // LAST = 0: chunk 0, staging this tile's chunk 1 into buffer 1
+    // LAST = 1: chunk 1, staging the next tile's chunk 0 into buffer 0 + the residual rows
+    auto chunk = [&](auto lc) __attribute__((always_inline)) {
+      constexpr int LAST = decltype(lc)::value;
+      const bf16* hcur = halo + LAST * G::HALO_ELEMS + opaque(abase);
+#pragma unroll
+      for (int tap = 0; tap < 9; ++tap) {
+        const int s = LAST * 9 + tap;
+        const int cb = tap & 1, nb = cb ^ 1;
+        bload(s + 1 < S ? s + 1 : 0, bq[nb]);  // after the last step: the next tile's step 0
+        // chunk 0: this tile's chunk 1 loads at tap 0 (staged at taps 2..7), the NEXT tile's chunk 0
+        // at tap 8 (staged during chunk 1's taps 1..6), so the residual rows can follow the staging
+        // rounds as they free their registers: row r at tap r + 2, rows 6, 7 at tap 7
+        if constexpr (!LAST) {
+          if (tap == 0) halo_load(cur, 1);
+          if (tap == 8) halo_load(nxt, 0);
+        } else {
+          if (tap >= 2 && tap < 8 && residual)
+            hreg[tap - 2] = *(const bf16x8*)(residual + (pix0 + (long long)(tap - 2) * W) * Co + opaque(cs));
+          if (tap == 7 && residual) {
+#pragma unroll
+            for (int f = 6; f < 8; ++f) {
+              const f32x4 v = __builtin_bit_cast(f32x4, *(const bf16x8*)(residual + (pix0 + (long long)f * W) * Co + cs));
+#pragma unroll
+              for (int j = 0; j < 4; ++j) gsc[(f - 6) * 4 + j] = v[j];
+            }
+          }
+        }
+        const int kh = tap / 3, kw = tap % 3;
+        bf16x8 fa[2][G::FM];
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+          for (int f = 0; f < G::FM; ++f)
+            fa[ks][f] = *(const bf16x8*)(hcur + ((f + kh) * CH_W + kw) * G::PP + ks * 32);
+        __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+          for (int f = 0; f < G::FM; ++f)
+#pragma unroll
+            for (int g = 0; g < G::FN; ++g)
+              acc[f][g] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bq[cb][ks][g], fa[ks][f], acc[f][g], 0, 0, 0);
+        constexpr int T0 = LAST ? 1 : 2;
+        if (tap >= T0 && tap - T0 < G::ROUNDS) {
+          if constexpr (LAST) stage_round(nxt, 0, tap - T0);
+          else stage_round(cur, 1, tap - T0);
+#pragma unroll
+          for (int k = 0; k < 28; ++k) {
+            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+            __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);
+          }
+          __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
+        }
+        __builtin_amdgcn_s_setprio(0);
+      }
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+        for (int g = 0; g < G::FN; ++g) bq[0][ks][g] = bq[1][ks][g];
+      // chunk 0: buffer 1 staged, every wave done with buffer 0 (restaged during chunk 1);
+      // chunk 1: the next tile's buffer 0 staged, every wave done with buffer 1
+      ch_lds_barrier();
+    };
+    chunk(std::integral_constant<int, 0>{});
+    chunk(std::integral_constant<int, 1>{});
+
+    // ---- register epilogue (as conv3x3_halo's register-B form, Co = 128: two groups per lane)
+    float sa = 0.f, sb = 0.f, qa = 0.f, qb = 0.f;
+#pragma unroll
+    for (int f = 0; f < G::FM; ++f) {
+      float v[8];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(acc[f][0][i]), __float_as_uint(acc[f][1][i]),
+                                                        false, false);
+        v[i] = __uint_as_float(r[0]);
+        v[4 + i] = __uint_as_float(r[1]);
+      }
+      if (residual) {
+        const bf16x8 rq = f < 6 ? hreg[f]
+                                : __builtin_bit_cast(bf16x8, (f32x4){gsc[(f - 6) * 4], gsc[(f - 6) * 4 + 1],
+                                                                     gsc[(f - 6) * 4 + 2], gsc[(f - 6) * 4 + 3]});
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] += (float)rq[e];
+      }
+      bf16x8 o;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) o[e] = (bf16)v[e];
+      *(bf16x8*)(out + (pix0 + (long long)f * W) * Co + cs) = o;
+      if (gn_part) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float q = (float)o[e], w2 = (float)o[4 + e];
+          sa += q;
+          qa += q * q;
+          sb += w2;
+          qb += w2 * w2;
+        }
+      }
+    }
+    if (gn_part) {
+      sa = row16_sum(sa);
+      qa = row16_sum(qa);
+      sb = row16_sum(sb);
+      qb = row16_sum(qb);
+      if (frow == 0) {
+        float* gp = gn_part + ((long long)pid * 32 + cs / 4) * 2;  // Co = 128: tile = pid
+        *(float2*)gp = make_float2(sa, qa);
+        *(float2*)(gp + 2) = make_float2(sb, qb);
+      }
+    }
+    if (!more) break;
+    pid = npid;
+    cur = nxt;
+  }
+}
+
+// =====================================================================================
 // Downsample conv (vaekl.py:59-72: F.pad(x, (0, 1, 0, 1)) then 3x3 / stride 2 / no padding) as a
 // halo-tile kernel.  Output tile 8 x 16 pixels x 128 channels, 256 threads, two workgroups per CU;
 // per 64-channel chunk the 17 x 33-pixel input halo (zero past the bottom / right edge = the pad)
@@ -1366,6 +1612,28 @@ extern "C" int uva_conv3x3_halo(const void* in, const void* w, void* out, const 
 #ifndef UVA_CONV_GN_STRIP
 #define UVA_CONV_GN_STRIP 0
 #endif
+#ifndef UVA_CONV_GN_PT
+#define UVA_CONV_GN_PT 0
+#endif
+  if (gn_scale && Ci == 128 && Co == 128 && (UVA_CONV_GN_PT)) {
+    // persistent form (above): two workgroups per CU
+    using GS = ConvHCfg<128, 8, false, false, true>;
+    static bool attr_p = false;
+    static int cus = 0;
+    if (!attr_p) {
+      (void)hipFuncSetAttribute((const void*)conv3x3_gn_pt, hipFuncAttributeMaxDynamicSharedMemorySize, GS::LDS_BYTES);
+      int dev = 0;
+      (void)hipGetDevice(&dev);
+      if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
+      attr_p = true;
+    }
+    const long long grid = std::min<long long>(nblk, 2LL * cus);
+    conv3x3_gn_pt<<<dim3((unsigned)grid), 256, GS::LDS_BYTES, stream>>>(
+        (const bf16*)in, (const bf16*)w, (bf16*)out, bias, (const bf16*)residual, gn_scale, gn_shift, gn_silu, gn_part,
+        Nimg, H, W);
+    UVA_LAUNCH_CHECK();
+    return 0;
+  }
   if (gn_scale && Ci == 128 && Co == 128 && (UVA_CONV_GN_STRIP)) {
     // strip form (above): one workgroup per (image, tile column)
     using GS = ConvHCfg<128, 8, false, false, true>;
