@@ -1613,10 +1613,12 @@ extern "C" int uva_conv3x3_halo(const void* in, const void* w, void* out, const 
 #define UVA_CONV_GN_STRIP 0
 #endif
 #ifndef UVA_CONV_GN_PT
-#define UVA_CONV_GN_PT 0
+#define UVA_CONV_GN_PT 1
 #endif
-  if (gn_scale && Ci == 128 && Co == 128 && (UVA_CONV_GN_PT)) {
-    // persistent form (above): two workgroups per CU
+  if (gn_scale && Ci == 128 && Co == 128 && residual == nullptr && (UVA_CONV_GN_PT)) {
+    // persistent form (above): two workgroups per CU.  Without a residual only: with one, its late
+    // rows cost what the next tile's early halo saves (level 0 6.61 vs 6.64 ms; without: 6.25 ->
+    // 6.15-6.19 ms, level 1 1.575 -> 1.55 ms; profiles/r04/ab_gnconv_persistent.txt)
     using GS = ConvHCfg<128, 8, false, false, true>;
     static bool attr_p = false;
     static int cus = 0;
