@@ -400,6 +400,15 @@ __global__ __launch_bounds__(TR * 32, 16 / TR) void conv3x3_halo(const bf16* __r
             const int csr = n0 + wn * (G::FN * 16) + (fk & 1) * 16 + (fk >> 1) * 8;
 #pragma unroll
             for (int f = 0; f < RQ_PRE; ++f) hreg[f] = *(const bf16x8*)(residual + (pix0 + (long long)f * W) * Co + csr);
+            if constexpr ((VAR & 256) != 0) {
+              // rows RQ_PRE.. into the GroupNorm scale registers (no staging in the last chunk)
+#pragma unroll
+              for (int f = RQ_PRE; f < G::FM; ++f) {
+                const f32x4 v = __builtin_bit_cast(f32x4, *(const bf16x8*)(residual + (pix0 + (long long)f * W) * Co + csr));
+#pragma unroll
+                for (int j = 0; j < 4; ++j) gsc[(f - RQ_PRE) * 4 + j] = v[j];
+              }
+            }
           }
         }
         const int kh = tap / 3, kw = tap % 3;
