@@ -69,7 +69,8 @@ def main(fetch_dir, write_dir, out_path):
             res[tag] = int(tot / nk) if tag in MEAN else int(tot)
     res["_note"] = ("per-launch HBM bytes = (2*FETCH_SIZE + WRITE_SIZE)*1024 (gfx950 FETCH_SIZE half-count "
                     "correction, MI355X_MICROARCH.md §HBM), rocprofv3 --pmc passes of bench.py --steps 1; "
-                    "multi-kernel tags summed (tools_traffic.py)")
+                    "multi-kernel attention tags summed, GN-conv tags the mean of their residual / no-residual "
+                    "kernels (tools_traffic.py)")
     json.dump(res, open(out_path, "w"), indent=1)
     print(json.dumps(res, indent=1))
 
