@@ -318,3 +318,42 @@ def skinny_bench():
 
 if __name__ == "__main__" and len(sys.argv) > 1 and sys.argv[1] == "skinny":
     skinny_bench()
+
+
+def cold_bench():
+    """the small-N Block products as the step runs them: hot (repeated) vs cold (a 1 GiB write between
+    calls evicts L2 and MALL); per-call HIP events around the product only"""
+    dev = "cuda"
+    M = 32768
+    flush = torch.empty(1 << 28, device=dev)
+    cases = []
+    for (N, K) in ((768, 768), (768, 3072), (3072, 768), (768, 2304)):
+        dy = torch.randn(M, N, device=dev).to(torch.bfloat16)
+        w = torch.randn(N, K, device=dev).to(torch.bfloat16)
+        x = torch.randn(M, K, device=dev).to(torch.bfloat16)
+        dx = torch.empty(M, K, device=dev, dtype=torch.bfloat16)
+        dw = torch.zeros(N, K, device=dev)
+        cases.append((f"dx  NN M{M} N{K} K{N}", lambda dy=dy, w=w, dx=dx: ops.linear_dx(dy, w, dx), 2 * M * N * K))
+        cases.append((f"dW  TT M{N} N{K} K{M}", lambda dy=dy, x=x, dw=dw: ops.linear_dw(dy, x, dw), 2 * M * N * K))
+        cases.append((f"fwd NT M{M} N{N} K{K}", lambda x=x, w=w, dy=dy: ops.linear(x, w, dy), 2 * M * N * K))
+    for name, fn, fl in cases:
+        res = []
+        for cold in (False, True):
+            ts = []
+            for i in range(12):
+                if cold:
+                    flush.fill_(float(i))
+                s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                s.record()
+                fn()
+                e.record()
+                torch.cuda.synchronize()
+                if i >= 2:
+                    ts.append(s.elapsed_time(e))
+            t = sorted(ts)[len(ts) // 2]
+            res.append(f"{'cold' if cold else 'hot '} {t*1e3:6.1f} us {fl/t/1e9:5.0f} TF")
+        print(f"{name}: " + "  ".join(res))
+
+
+if __name__ == "__main__" and len(sys.argv) > 1 and sys.argv[1] == "cold":
+    cold_bench()
