@@ -1,0 +1,13 @@
+# attention with s_setprio around the MFMA blocks (UVA_ATT_PRIO=1) vs in-tree
+set -o pipefail
+export TMPDIR=/tmp
+O=gpurun_out/r04x
+mkdir -p $O
+timeout -k 10 300 python -u tools/ab_run.py abx/libuva_aprio.so -m pytest tests/test_attention_gpu.py -x -q --timeout 200 --timeout-method thread > $O/t.log 2>&1 || { echo "TESTS_FAIL"; grep -E "^E  |FAILED|Error" $O/t.log | head -20; tail -3 $O/t.log; exit 1; }
+echo "aprio $(tail -1 $O/t.log)"
+for i in 1 2 3; do
+  for L in new aprio; do
+    if [ $L = new ]; then PY=python; else PY="python tools/ab_run.py abx/libuva_$L.so"; fi
+    echo "== $L"; timeout -k 10 200 $PY tools/tools_kbench.py attn 2>&1 | grep "H=12 p=" || exit 1
+  done
+done

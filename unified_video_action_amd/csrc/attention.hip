@@ -39,6 +39,22 @@
 #ifndef UVA_ATT_PIPE_DQ
 #define UVA_ATT_PIPE_DQ 0
 #endif
+// UVA_ATT_PRIO: s_setprio(1) around the MFMA blocks, so that on a SIMD the wave in its matrix phase
+// wins the issue slots over the co-resident wave's softmax / staging phase (the GN conv measured
+// 37 % slower without its equivalent)
+// forward: on (0.162-0.168 vs 0.166-0.171 ms at B32/N1024/H12); backward: off (p = 0.1: 0.70 vs
+// 0.49 ms -- the barrier the builtin puts in hipcc's schedule splits the dropout-bit / softmax
+// interleave), profiles/r04/ab_attn_setprio.txt
+#ifndef UVA_ATT_PRIO
+#define UVA_ATT_PRIO 1
+#endif
+#ifndef UVA_ATT_PRIO_BWD
+#define UVA_ATT_PRIO_BWD 0
+#endif
+#define ATT_PRIO_HI() do { if (UVA_ATT_PRIO) __builtin_amdgcn_s_setprio(1); } while (0)
+#define ATT_PRIO_LO() do { if (UVA_ATT_PRIO) __builtin_amdgcn_s_setprio(0); } while (0)
+#define ATT_PRIO_HI_BWD() do { if (UVA_ATT_PRIO_BWD) __builtin_amdgcn_s_setprio(1); } while (0)
+#define ATT_PRIO_LO_BWD() do { if (UVA_ATT_PRIO_BWD) __builtin_amdgcn_s_setprio(0); } while (0)
 #define AT_LD 72
 #define AT_TILE (64 * AT_LD)
 
@@ -283,6 +299,7 @@ __global__ __launch_bounds__(256, OCC) void attn_fwd_kernel(const bf16* __restri
     for (int kt = 0; kt < NKT; ++kt)
 #pragma unroll
       for (int qt = 0; qt < 2; ++qt) s[kt][qt] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    ATT_PRIO_HI();
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
 #pragma unroll
@@ -292,6 +309,7 @@ __global__ __launch_bounds__(256, OCC) void attn_fwd_kernel(const bf16* __restri
         for (int qt = 0; qt < 2; ++qt) s[kt][qt] = mfma16(kf, qf[qt][ks], s[kt][qt]);
       }
     }
+    ATT_PRIO_LO();
     // row max (lane: NKT*4 keys of its query; the 4 quads of a query meet through two shuffles)
     float mx[2];
     bool need = false;
@@ -335,6 +353,7 @@ __global__ __launch_bounds__(256, OCC) void attn_fwd_kernel(const bf16* __restri
         }
       rs[qt] += (ps[0] + ps[1]) + (ps[2] + ps[3]);
     }
+    ATT_PRIO_HI();
 #pragma unroll
     for (int ks = 0; ks < KT / 32; ++ks) {
       bf16x8 pf[2];
@@ -347,6 +366,7 @@ __global__ __launch_bounds__(256, OCC) void attn_fwd_kernel(const bf16* __restri
         for (int qt = 0; qt < 2; ++qt) o[qt][dt] = mfma16(vf, pf[qt], o[qt][dt]);
       }
     }
+    ATT_PRIO_LO();
     if (more) {
 #pragma unroll
       for (int hh = 0; hh < NH; ++hh) {
@@ -574,6 +594,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_kernel(const bf16* __res
     __builtin_amdgcn_sched_barrier(0);
     dkdv(1);
 #else
+    ATT_PRIO_HI_BWD();
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
@@ -586,6 +607,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_kernel(const bf16* __res
           dp[qt][kt] = mfma16(e, vf[kt][ks], dp[qt][kt]);
         }
       }
+    ATT_PRIO_LO_BWD();
     // P = exp2(S c - L);  Pd = keep P;  dS = P (keep dP' - D)      (s <- Pd, dp <- dS)
 #pragma unroll
     for (int qt = 0; qt < 4; ++qt) {
@@ -608,6 +630,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_kernel(const bf16* __res
         }
     }
     // dV^T[d][key] += dO'^T Pd ; dK^T[d][key] += Q^T dS      (k = q, permuted by pi)
+    ATT_PRIO_HI_BWD();
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
       bf16x8 pb[2], sb[2];
@@ -627,6 +650,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_kernel(const bf16* __res
         }
       }
     }
+    ATT_PRIO_LO_BWD();
 #endif
     if (more) {
       stage_store(sQ[cur ^ 1], rq);
@@ -792,6 +816,7 @@ __global__ __launch_bounds__(256, UVA_ATT_DQ_OCC) void attn_bwd_dq_kernel(const 
     __builtin_amdgcn_sched_barrier(0);
     dqk(1);
 #else
+    ATT_PRIO_HI_BWD();
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
@@ -804,6 +829,7 @@ __global__ __launch_bounds__(256, UVA_ATT_DQ_OCC) void attn_bwd_dq_kernel(const 
           dp[kt][qt] = mfma16(va, of[qt][ks], dp[kt][qt]);
         }
       }
+    ATT_PRIO_LO_BWD();
 #pragma unroll
     for (int qt = 0; qt < 2; ++qt)
 #pragma unroll
@@ -815,6 +841,7 @@ __global__ __launch_bounds__(256, UVA_ATT_DQ_OCC) void attn_bwd_dq_kernel(const 
           if (DROP) dpt = keep_bfe(dpt, mw[qt], kt * 4 + r);
           s[kt][qt][r] = p * (dpt - Dq[qt]);
         }
+    ATT_PRIO_HI_BWD();
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
       bf16x8 sb[2];
@@ -827,6 +854,7 @@ __global__ __launch_bounds__(256, UVA_ATT_DQ_OCC) void attn_bwd_dq_kernel(const 
         for (int qt = 0; qt < 2; ++qt) dq[dt][qt] = mfma16(ka, sb[qt], dq[dt][qt]);
       }
     }
+    ATT_PRIO_LO_BWD();
 #endif
     if (more) {
       stage_store(sK[cur ^ 1], rk);
