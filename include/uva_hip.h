@@ -148,6 +148,9 @@ int uva_softmax_bwd(int dtype, const void* P, const void* dPd, void* dS, long lo
 int uva_cast(int sdt, const void* src, long long lds, int ddt, void* dst, long long ldd, long long rows, int cols,
              hipStream_t stream);
 int uva_act_fwd(int xdt, const void* x, int ydt, void* y, long long n, int act, hipStream_t stream);
+/* dst[c][r] = src[r][c], bf16 [rows][cols] (rows, cols % 8 == 0, 16-B aligned): the transposed bf16
+ * weight copies of the Block's width-768 dX products (functional.py compute_weight_t). */
+int uva_transpose_bf16(const void* src, void* dst, int rows, int cols, hipStream_t stream);
 /* y = residual + dropout(act(x)) over n contiguous elements (n % 8 == 0, 16-B aligned), dropout
  * index = flat element index (the GEMM epilogue's / uva_act_bwd's mask).  timm Mlp forward
  * (mar_con_unified.py:201-249: fc1 -> GELU -> drop, fc2 -> drop -> + residual) when fc1 / fc2 run

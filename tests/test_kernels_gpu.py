@@ -361,3 +361,39 @@ def test_act_drop_fwd_matches_backward_mask_and_torch(rows, cols):
     keep = torch.empty(rows, cols, device=DEV)
     ops.act_bwd(None, torch.ones(rows, cols, device=DEV), keep, "none", drop_p=0.1, seed=78)
     assert torch.allclose(out, res + x.float() * keep, rtol=1e-6, atol=1e-6)
+
+
+@pytest.mark.parametrize("R,C", [(768, 2304), (2304, 768), (3072, 768), (768, 768), (72, 136)])
+def test_transpose_bf16_and_dx_through_transposed_weight(R, C):
+    """uva_transpose_bf16 (64 x 64 LDS tiles, ragged edges) is an exact transpose, and the Block's dX
+    through the transposed weight copy (functional.linear_dx_w: a forward-layout GEMM) equals the
+    dX GEMM to bf16 output rounding (the same bf16 operands, fp32 accumulation in another order)."""
+    from unified_video_action_amd.native import ops
+    from unified_video_action_amd.model.autoregressive import functional as fn
+    from unified_video_action_amd.runtime import RT
+    torch.manual_seed(R + C)
+    w = torch.randn(R, C, device="cuda").to(torch.bfloat16)
+    t = torch.empty(C, R, device="cuda", dtype=torch.bfloat16)
+    ops.transpose_bf16(w, t)
+    assert torch.equal(t, w.t().contiguous())
+    if R % 8 or C % 384 or C >= 1024:
+        return
+    # dX = dy @ W for nn.Linear(C -> R): W [R, C], dy [M, R], dX [M, C]
+    RT.set_precision("bf16")
+    M = 2048
+    p = torch.nn.Parameter((torch.randn(R, C, device="cuda") * 0.05))
+    dy = (torch.randn(M, R, device="cuda")).to(torch.bfloat16)
+    a = torch.empty(M, C, device="cuda", dtype=torch.bfloat16)
+    b = torch.empty(M, C, device="cuda", dtype=torch.bfloat16)
+    prev = RT.dx_wt_layout
+    try:
+        RT.dx_wt_layout = True
+        fn.linear_dx_w(dy, p, a)
+        RT.dx_wt_layout = False
+        fn.linear_dx_w(dy, p, b)
+    finally:
+        RT.dx_wt_layout = prev
+    ref = dy.float() @ p.detach().to(torch.bfloat16).float()
+    scale = ref.abs().max().item()
+    assert (a.float() - ref).abs().max().item() < 1e-2 * scale
+    assert (a.float() - b.float()).abs().max().item() < 1e-2 * scale

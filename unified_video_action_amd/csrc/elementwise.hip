@@ -292,6 +292,56 @@ extern "C" int uva_cast(int sdt, const void* src, long long lds, int ddt, void* 
   return 0;
 }
 
+// dst[c][r] = src[r][c] for a bf16 [rows][cols] matrix: 64 x 64 tiles through LDS (16-B loads and
+// stores, 8 consecutive elements per thread each way).  The transposed bf16 weight copies that
+// turn the Block's width-768 dX products (x @ W -> x @ (W^T)^T) into the forward GEMM layout
+// (K-contiguous B), 17-27 % faster on the 128 x 384 tile than the transposed-B read path.
+__global__ __launch_bounds__(256) void transpose_bf16_kernel(const bf16* __restrict__ src, bf16* __restrict__ dst,
+                                                             int rows, int cols) {
+  __shared__ bf16 t[64][64 + 8];
+  const int r0 = blockIdx.y * 64, c0 = blockIdx.x * 64;
+  const int tid = threadIdx.x;
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int id = tid + i * 256, rr = id >> 3, cc = (id & 7) * 8;
+    const int r = r0 + rr, c = c0 + cc;
+    bf16x8 v;
+    if (r < rows && c + 8 <= cols) {
+      v = *(const bf16x8*)(src + (long long)r * cols + c);
+    } else {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = (r < rows && c + e < cols) ? src[(long long)r * cols + c + e] : (bf16)0.f;
+    }
+#pragma unroll
+    for (int e = 0; e < 8; ++e) t[rr][cc + e] = v[e];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int id = tid + i * 256, cc = id >> 3, rr = (id & 7) * 8;  // output row = src column
+    const int c = c0 + cc, r = r0 + rr;
+    bf16x8 v;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = t[rr + e][cc];
+    if (c < cols && r + 8 <= rows) {
+      *(bf16x8*)(dst + (long long)c * rows + r) = v;
+    } else if (c < cols) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e)
+        if (r + e < rows) dst[(long long)c * rows + r + e] = v[e];
+    }
+  }
+}
+
+extern "C" int uva_transpose_bf16(const void* src, void* dst, int rows, int cols, hipStream_t s) {
+  if (rows <= 0 || cols <= 0) return 0;
+  if ((rows % 8) || (cols % 8) || (((uintptr_t)src | (uintptr_t)dst) % 16)) return (int)hipErrorInvalidValue;
+  transpose_bf16_kernel<<<dim3((cols + 63) / 64, (rows + 63) / 64), 256, 0, s>>>((const bf16*)src, (bf16*)dst, rows,
+                                                                                 cols);
+  UVA_LAUNCH_CHECK();
+  return 0;
+}
+
 // y = residual + drop(act(x)), 8 consecutive elements per thread (16-B bf16 / 2 x 16-B fp32
 // accesses), dropout index = flat element index (= row * cols + col of a contiguous [rows][cols]:
 // the GEMM epilogue's and act_bwd's mask).  The forward of timm Mlp when its GEMMs run bias-only

@@ -48,6 +48,32 @@ def compute_weight(p):
     return sh
 
 
+def compute_weight_t(p):
+    """transposed compute-dtype copy [in, out] of an fp32 [out, in] weight, rebuilt once per
+    parameter generation (the optimizer bumps RT.param_gen; RT.dx_wt_layout routes the dX products
+    through it)"""
+    w = compute_weight(p)
+    key = (p._version, p.data_ptr(), RT.param_gen)
+    t = getattr(p, "_uva_shadow_t", None)
+    if t is None or getattr(p, "_uva_shadow_t_ver", None) != key:
+        if t is None or t.shape != (w.shape[1], w.shape[0]):
+            t = torch.empty(w.shape[1], w.shape[0], dtype=w.dtype, device=w.device)
+        ops.transpose_bf16(w, t)
+        p._uva_shadow_t = t
+        p._uva_shadow_t_ver = key
+    return t
+
+
+def linear_dx_w(dy, p, dx):
+    """dX = dy @ W of nn.Linear(W: [out, in]).  bf16 with RT.dx_wt_layout and an output 768 wide:
+    through the transposed weight copy as a forward-layout GEMM (K-contiguous B operand: 17-27 %
+    faster on the 128 x 384 tile than the transposed-B read path); otherwise the dX GEMM."""
+    if cdt() == torch.bfloat16 and RT.dx_wt_layout and dx.shape[1] % 384 == 0 and dx.shape[1] < 1024:
+        ops.linear(dy, compute_weight_t(p), dx)
+    else:
+        ops.linear_dx(dy, compute_weight(p), dx)
+
+
 def grad_buf(p):
     if p.grad is None:
         p.grad = torch.zeros_like(p)
@@ -309,7 +335,7 @@ class BlockFn(torch.autograd.Function):
         # dX of the LN-fed GEMMs in the compute dtype (autocast: the matmul's input grad is half
         # precision before the cast back to the fp32 LayerNorm output); LN backward reads it as is
         dh2 = torch.empty(M, D, dtype=c if RT.ln_dy_lowp else F32, device=dev)
-        ops.linear_dx(dpre1, compute_weight(fc1w), dh2)
+        linear_dx_w(dpre1, fc1w, dh2)
         del dpre1
         g1 = torch.empty(M, D, dtype=F32, device=dev)
         ops.layernorm_bwd(x1, n2w.detach(), dh2, m2, r2, g1, accum=False, dw=grad_buf(n2w), db=grad_buf(n2b),
@@ -320,7 +346,7 @@ class BlockFn(torch.autograd.Function):
         ops.act_bwd_bias(None, g1, dprep, grad_buf(projb), "none", drop_p=p_proj, seed=seeds[1])
         ops.linear_dw(dprep, o, grad_buf(projw))
         do = torch.empty(M, D, dtype=c, device=dev)
-        ops.linear_dx(dprep, compute_weight(projw), do)
+        linear_dx_w(dprep, projw, do)
         del dprep
         if flash:
             dqkv = torch.empty(M, 3 * D, dtype=c, device=dev)
@@ -332,7 +358,7 @@ class BlockFn(torch.autograd.Function):
         ops.linear_dw(dqkv, h1, grad_buf(qkvw))
         ops.colsum(dqkv, grad_buf(qkvb))
         dh1 = torch.empty(M, D, dtype=c if RT.ln_dy_lowp else F32, device=dev)
-        ops.linear_dx(dqkv, compute_weight(qkvw), dh1)
+        linear_dx_w(dqkv, qkvw, dh1)
         del dqkv
         gx = torch.empty(M, D, dtype=F32, device=dev)
         ops.layernorm_bwd(x, n1w.detach(), dh1, m1, r1, gx, accum=False, dw=grad_buf(n1w), db=grad_buf(n1b),

@@ -180,6 +180,14 @@ def softmax_bwd(P, dPd, dS, L, scale, drop_p=0.0, seed=0):
                int(seed) & 0xFFFFFFFFFFFFFFFF, stream())
 
 
+def transpose_bf16(src, dst):
+    """dst [C, R] = src [R, C]^T (bf16, contiguous)"""
+    R, C = src.shape
+    assert src.dtype == dst.dtype == torch.bfloat16 and src.is_contiguous() and dst.is_contiguous()
+    assert tuple(dst.shape) == (C, R)
+    lib().call("uva_transpose_bf16", ptr(src), ptr(dst), R, C, stream())
+
+
 def cast(src, dst):
     if src.dim() == 1 or (src.is_contiguous() and dst.is_contiguous()):
         rows, cols = 1, src.numel()

@@ -1,5 +1,6 @@
 """Process-wide runtime settings of the HIP path: compute precision and the per-call
 dropout seeds (counter-based masks need a distinct seed per op per step)."""
+import os
 import itertools
 
 import torch
@@ -38,6 +39,9 @@ class _Runtime:
         # bumped whenever HIP kernels rewrite parameters in place (optimizer / EMA steps): caches
         # keyed on parameters (non-static compute shadows, the sampler's captured graphs) compare it
         self.param_gen = 0
+        # dX products of width-768 outputs through transposed bf16 weight copies (forward-layout GEMM)
+        # (UVA_DX_WT=0 switches it off: A/B runs of bench.py)
+        self.dx_wt_layout = os.environ.get("UVA_DX_WT", "1") != "0"
 
     def set_precision(self, name):
         name = str(name).lower()
