@@ -1,7 +1,7 @@
 # full GPU check of the current tree: -m gpu suite, smoke, default bench (driver command)
 set -o pipefail
 export TMPDIR=/tmp
-O=gpurun_out/r04m
+O=gpurun_out/${OUTDIR:-r04m}
 mkdir -p $O
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $O/pytest_gpu.log 2>&1 || { echo TESTS_FAIL; grep -E "^E  |FAILED|Error" $O/pytest_gpu.log | head -30; tail -5 $O/pytest_gpu.log; exit 1; }
 tail -1 $O/pytest_gpu.log
