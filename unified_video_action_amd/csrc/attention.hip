@@ -409,7 +409,7 @@ __global__ __launch_bounds__(256, OCC) void attn_fwd_kernel(const bf16* __restri
 // =====================================================================================
 __global__ __launch_bounds__(256) void attn_bwd_pre_kernel(const bf16* __restrict__ out, const bf16* __restrict__ dout,
                                                            float* __restrict__ Dvec, bf16* __restrict__ dOs,
-                                                           long long rows, int N, int H, float dsc) {
+                                                           long long rows, int N, int H, float dsc, float dmul) {
   const long long t = (long long)blockIdx.x * 256 + threadIdx.x;
   const long long row = t >> 3;  // (b*N + q)*H + h
   const int sub = threadIdx.x & 7;
@@ -435,7 +435,7 @@ __global__ __launch_bounds__(256) void attn_bwd_pre_kernel(const bf16* __restric
     const int h = (int)(row % H);
     const long long bq = row / H;
     const long long b = bq / N, q = bq % N;
-    Dvec[(b * H + h) * N + q] = v;
+    Dvec[(b * H + h) * N + q] = v * dmul;
   }
 }
 
@@ -449,7 +449,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_kernel(const bf16* __res
                                                                const float* __restrict__ lse2,
                                                                const float* __restrict__ Dvec,
                                                                const uint64_t* __restrict__ MK, bf16* __restrict__ dqkv,
-                                                               int N, int H, float scale, float c) {
+                                                               int N, int H, float scale, float c, float vsc) {
   __shared__ __attribute__((aligned(16))) bf16 sQ[2][AT_TILE];
   __shared__ __attribute__((aligned(16))) bf16 sO[2][AT_TILE];
   __shared__ __attribute__((aligned(16))) float sL[2][64];
@@ -672,7 +672,8 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_kernel(const bf16* __res
     for (int dt = 0; dt < 4; ++dt) {
       bf16x4 a = {(bf16)(dk[dt][kt][0] * scale), (bf16)(dk[dt][kt][1] * scale), (bf16)(dk[dt][kt][2] * scale),
                   (bf16)(dk[dt][kt][3] * scale)};
-      bf16x4 e = {(bf16)dv[dt][kt][0], (bf16)dv[dt][kt][1], (bf16)dv[dt][kt][2], (bf16)dv[dt][kt][3]};
+      bf16x4 e = {(bf16)(dv[dt][kt][0] * vsc), (bf16)(dv[dt][kt][1] * vsc), (bf16)(dv[dt][kt][2] * vsc),
+                  (bf16)(dv[dt][kt][3] * vsc)};
       *(bf16x4*)(krow + dt * 16 + 4 * g) = a;
       *(bf16x4*)(vrow + dt * 16 + 4 * g) = e;
     }
@@ -929,27 +930,31 @@ extern "C" int uva_attn_bwd(const void* qkv, const void* out, const void* dout, 
                             hipStream_t s) {
   if (N % 64 != 0) return (int)hipErrorInvalidValue;
   const bool drop = drop_p > 0.f;
-  if (drop && (mask == nullptr || workspace == nullptr)) return (int)hipErrorInvalidValue;
+  if (drop && mask == nullptr) return (int)hipErrorInvalidValue;
   uint32_t th;
   float ds;
   uva_drop_params(drop_p, &th, &ds);
   const long long rows = (long long)B * N * H;
-  bf16* dOs = drop ? (bf16*)workspace : nullptr;
+  // the dropout scale 1/(1-p) is not applied to dO: dP' = dsc dO V^T, so dS = dsc P (keep dP - D / dsc),
+  // i.e. the loops run on the unscaled dO with D' = D / dsc, and dsc goes on dK, dQ, dV once at the
+  // end (no scaled dO copy: one [B N H 64] bf16 write + its re-reads per layer saved)
+  (void)workspace;
   attn_bwd_pre_kernel<<<(unsigned)((rows * 8 + 255) / 256), 256, 0, s>>>((const bf16*)out, (const bf16*)dout, Dvec,
-                                                                         dOs, rows, N, H, ds);
+                                                                         nullptr, rows, N, H, ds, 1.0f / ds);
   const int nt = N / 64;
   const uint64_t* MQ = (const uint64_t*)mask;
   const uint64_t* MK = drop ? MQ + (long long)B * H * N * nt : nullptr;
-  const bf16* dO = drop ? dOs : (const bf16*)dout;
+  const bf16* dO = (const bf16*)dout;
   dim3 grid((N + 127) / 128, B * H);
   const float c = scale * 1.4426950408889634f;
+  const float sk = scale * ds;
   if (drop) {
-    attn_bwd_dkdv_kernel<true><<<grid, 256, 0, s>>>((const bf16*)qkv, dO, lse2, Dvec, MK, (bf16*)dqkv, N, H, scale, c);
-    attn_bwd_dq_kernel<true><<<grid, 256, 0, s>>>((const bf16*)qkv, dO, lse2, Dvec, MQ, (bf16*)dqkv, N, H, scale, c);
+    attn_bwd_dkdv_kernel<true><<<grid, 256, 0, s>>>((const bf16*)qkv, dO, lse2, Dvec, MK, (bf16*)dqkv, N, H, sk, c, ds);
+    attn_bwd_dq_kernel<true><<<grid, 256, 0, s>>>((const bf16*)qkv, dO, lse2, Dvec, MQ, (bf16*)dqkv, N, H, sk, c);
   } else {
     attn_bwd_dkdv_kernel<false><<<grid, 256, 0, s>>>((const bf16*)qkv, dO, lse2, Dvec, nullptr, (bf16*)dqkv, N, H,
-                                                     scale, c);
-    attn_bwd_dq_kernel<false><<<grid, 256, 0, s>>>((const bf16*)qkv, dO, lse2, Dvec, nullptr, (bf16*)dqkv, N, H, scale,
+                                                     sk, c, ds);
+    attn_bwd_dq_kernel<false><<<grid, 256, 0, s>>>((const bf16*)qkv, dO, lse2, Dvec, nullptr, (bf16*)dqkv, N, H, sk,
                                                    c);
   }
   UVA_LAUNCH_CHECK();
