@@ -29,8 +29,9 @@
 // A fused single pass with dQ summed by fp32 atomics was measured slower at this shape: d = 64
 // gives only 640 FLOP per atomic byte, so the 0.8 GB of dQ adds per layer ran at the chip's
 // atomic rate (+0.28 ms per layer), more than the recomputed S/dP of the dQ kernel costs.
-// dO' = dO / (1 - p) is prepared by the pre kernel (with D = rowsum(dO * O)), so the dropout
-// scale costs nothing inside the loops.
+// The dropout scale dsc = 1 / (1 - p) never enters the loops: they run on the unscaled dO with
+// D' = rowsum(dO * O) / dsc from the pre kernel (dS = dsc P (keep dP - D')), and dsc multiplies dK,
+// dQ and dV once when they are stored.
 #include "common.h"
 
 #ifndef UVA_ATT_PIPE
