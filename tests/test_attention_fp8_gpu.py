@@ -56,10 +56,11 @@ def _ref_attention(qkv, scale, mask_keep=None, p=0.0):
     return (P @ v).permute(0, 2, 1, 3), lse
 
 
-@pytest.mark.parametrize("N", [1088, 1024])
-def test_quant_matches_torch_e4m3_and_layouts(N):
+@pytest.mark.parametrize("N,H", [(1088, 3), (1024, 3), (1088, 12), (1024, 12)])
+def test_quant_matches_torch_e4m3_and_layouts(N, H):
+    """H = 12 runs the row form of the pass (one workgroup per 64-row tile over all heads)"""
     from unified_video_action_amd.native import ops
-    B, H = 2, 3
+    B = 2
     x = _qkv(B, N, H, 1)
     want, s = _torch_round(x)
     ws = ops.attn_fp8_workspace(B, N, H, DEV)
@@ -78,6 +79,9 @@ def test_quant_matches_torch_e4m3_and_layouts(N):
     sv = s[:, :, 2].repeat_interleave(64, dim=1)  # [B,N,H]
     vt = v8t[:, :, :, pos].permute(0, 3, 1, 2) * sv[..., None]  # [B,N,H,64]
     torch.testing.assert_close(vt, want[:, :, 2].float(), rtol=0, atol=0)
+    off = (3 * B * N * H * 64 + 255) // 256 * 256
+    sc = ws[off: off + 4 * B * 3 * H * (N // 64)].view(torch.float32).reshape(B, 3, H, N // 64)
+    torch.testing.assert_close(sc, s.permute(0, 2, 3, 1), rtol=0, atol=0)
 
 
 @pytest.mark.parametrize("N,drop", [(1088, 0.0), (1024, 0.0), (1088, 0.1), (1024, 0.1)])

@@ -26,6 +26,10 @@
 #include "common.h"
 
 #define A8_MAX 448.0f
+// quantisation pass in its row form for H = 12 (attn_quant_fp8_rows_kernel)
+#ifndef UVA_A8_QUANT_ROWS
+#define UVA_A8_QUANT_ROWS 0
+#endif
 
 typedef __attribute__((ext_vector_type(8))) int i32x8;  // 32 e4m3 values: one lane's 32x32x64 operand
 
@@ -111,6 +115,114 @@ __global__ __launch_bounds__(256) void attn_quant_fp8_kernel(bf16* __restrict__ 
     *(int4*)dst = *(const int4*)(tr + d * 64 + c16);
   }
   if (tid == 0) sc[((long long)(b * 3 + t) * H + h) * (N / 64) + tile] = s;
+}
+
+// smallest e with amax * 2^-e <= 448 (e = 0 for an all-zero tile)
+__device__ __forceinline__ int a8_exponent(float amax) {
+  int e = 0;
+  if (amax > 0.f) {
+    e = (int)ceilf(log2f(amax / A8_MAX));
+    while (ldexpf(amax, -e) > A8_MAX) ++e;
+    while (ldexpf(amax, -(e - 1)) <= A8_MAX) --e;
+  }
+  return e;
+}
+
+typedef __attribute__((ext_vector_type(2))) unsigned short u16x2;
+__device__ __forceinline__ uint32_t pk_max_u16(uint32_t a, uint32_t b) {
+  return __builtin_bit_cast(uint32_t, __builtin_elementwise_max(__builtin_bit_cast(u16x2, a), __builtin_bit_cast(u16x2, b)));
+}
+
+// Row form of the same pass for H heads known at compile time (mar_base: 12): one workgroup per
+// (64-row tile, q|k|v, batch) walks all H heads of the tile.  The per-(tile, head) workgroups of
+// attn_quant_fp8_kernel each move only 8 KiB behind one load round trip and a barrier; here every
+// thread issues its 2H 16-B loads up front (8 lanes cover one 128-B head row, a wave-instruction 8
+// rows), the H block maxima come out of one cross-wave exchange (|x| as bf16 bit patterns, two
+// heads per dword, v_pk_max_u16), and the V^T transposes of all heads share one barrier.  Outputs
+// are bit-identical to attn_quant_fp8_kernel.
+template <int H>
+__global__ __launch_bounds__(256) void attn_quant_fp8_rows_kernel(bf16* __restrict__ qkv, uint8_t* __restrict__ qk8,
+                                                                  uint8_t* __restrict__ v8t, float* __restrict__ sc,
+                                                                  int N) {
+  static_assert(H % 2 == 0, "two heads per reduction word");
+  __shared__ uint32_t red[4][H / 2];
+  __shared__ __attribute__((aligned(16))) uint8_t tr[H][64 * 64];
+  const int tile = blockIdx.x, t = blockIdx.y, b = blockIdx.z;
+  const int tid = threadIdx.x, w = tid >> 6, l = tid & 63;
+  const int r0 = w * 16 + (l >> 3), c = (l & 7) * 8;  // rows r0, r0 + 8; columns c .. c + 7 of every head
+  const long long ld = 3LL * H * 64;
+  bf16* base = qkv + ((long long)b * N + tile * 64 + r0) * ld + (long long)t * H * 64 + c;
+  uint4 x[H][2];
+#pragma unroll
+  for (int h = 0; h < H; ++h)
+#pragma unroll
+    for (int k = 0; k < 2; ++k) x[h][k] = *(const uint4*)(base + k * 8 * ld + h * 64);
+  uint32_t m2[H / 2];
+#pragma unroll
+  for (int i = 0; i < H / 2; ++i) {
+    uint32_t a = 0, bb = 0;
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      a = pk_max_u16(a, pk_max_u16(x[2 * i][k].x & 0x7FFF7FFFu, x[2 * i][k].y & 0x7FFF7FFFu));
+      a = pk_max_u16(a, pk_max_u16(x[2 * i][k].z & 0x7FFF7FFFu, x[2 * i][k].w & 0x7FFF7FFFu));
+      bb = pk_max_u16(bb, pk_max_u16(x[2 * i + 1][k].x & 0x7FFF7FFFu, x[2 * i + 1][k].y & 0x7FFF7FFFu));
+      bb = pk_max_u16(bb, pk_max_u16(x[2 * i + 1][k].z & 0x7FFF7FFFu, x[2 * i + 1][k].w & 0x7FFF7FFFu));
+    }
+    a = max(a & 0xFFFFu, a >> 16);
+    bb = max(bb & 0xFFFFu, bb >> 16);
+    uint32_t v = a | (bb << 16);
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) v = pk_max_u16(v, (uint32_t)__shfl_xor((int)v, o, 64));
+    m2[i] = v;
+  }
+  if (l == 0) {
+#pragma unroll
+    for (int i = 0; i < H / 2; ++i) red[w][i] = m2[i];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < H / 2; ++i) m2[i] = pk_max_u16(pk_max_u16(red[0][i], red[1][i]), pk_max_u16(red[2][i], red[3][i]));
+  const long long q0 = (long long)b * N + tile * 64 + r0;
+#pragma unroll
+  for (int h = 0; h < H; ++h) {
+    const uint32_t bits = (h & 1) ? (m2[h >> 1] >> 16) : (m2[h >> 1] & 0xFFFFu);
+    const int e = a8_exponent(__uint_as_float(bits << 16));
+    const float inv = ldexpf(1.f, -e), s = ldexpf(1.f, e);
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const bf16x8 xv = __builtin_bit_cast(bf16x8, x[h][k]);
+      const int w0 = pack4_fp8((float)xv[0] * inv, (float)xv[1] * inv, (float)xv[2] * inv, (float)xv[3] * inv);
+      const int w1 = pack4_fp8((float)xv[4] * inv, (float)xv[5] * inv, (float)xv[6] * inv, (float)xv[7] * inv);
+      bf16x8 yv;
+      yv[0] = (bf16)(__builtin_amdgcn_cvt_f32_fp8(w0, 0) * s);
+      yv[1] = (bf16)(__builtin_amdgcn_cvt_f32_fp8(w0, 1) * s);
+      yv[2] = (bf16)(__builtin_amdgcn_cvt_f32_fp8(w0, 2) * s);
+      yv[3] = (bf16)(__builtin_amdgcn_cvt_f32_fp8(w0, 3) * s);
+      yv[4] = (bf16)(__builtin_amdgcn_cvt_f32_fp8(w1, 0) * s);
+      yv[5] = (bf16)(__builtin_amdgcn_cvt_f32_fp8(w1, 1) * s);
+      yv[6] = (bf16)(__builtin_amdgcn_cvt_f32_fp8(w1, 2) * s);
+      yv[7] = (bf16)(__builtin_amdgcn_cvt_f32_fp8(w1, 3) * s);
+      *(bf16x8*)(base + k * 8 * ld + h * 64) = yv;
+      if (t < 2) {
+        *(int2*)(qk8 + ((q0 + 8 * k) * 2 + t) * (H * 64) + h * 64 + c) = (int2){w0, w1};
+      } else {
+        const int pos = v8_pos(r0 + 8 * k);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          tr[h][(c + j) * 64 + pos] = (uint8_t)((unsigned)w0 >> (8 * j));
+          tr[h][(c + 4 + j) * 64 + pos] = (uint8_t)((unsigned)w1 >> (8 * j));
+        }
+      }
+    }
+    if (tid == h) sc[((long long)(b * 3 + t) * H + h) * (N / 64) + tile] = s;
+  }
+  if (t == 2) {  // workgroup-uniform
+    __syncthreads();
+    const int d = tid >> 2, c16 = (tid & 3) * 16;
+#pragma unroll
+    for (int h = 0; h < H; ++h)
+      *(int4*)(v8t + (((long long)b * H + h) * 64 + d) * N + tile * 64 + c16) = *(const int4*)(&tr[h][d * 64 + c16]);
+  }
 }
 
 // LDS images (no padding: LDS-DMA writes 1 KiB lane-linear pieces), 16-B chunk c of row r stored
@@ -310,7 +422,10 @@ extern "C" int uva_attn_quant_fp8(void* qkv, void* workspace, int B, int N, int 
   uint8_t* qk8 = (uint8_t*)workspace;
   uint8_t* v8t = qk8 + 2LL * B * N * H * 64;
   float* sc = (float*)((uint8_t*)workspace + (3LL * B * N * H * 64 + 255) / 256 * 256);
-  attn_quant_fp8_kernel<<<dim3(N / 64, 3, B * H), 256, 0, s>>>((bf16*)qkv, qk8, v8t, sc, N, H);
+  if (H == 12 && UVA_A8_QUANT_ROWS)
+    attn_quant_fp8_rows_kernel<12><<<dim3(N / 64, 3, B), 256, 0, s>>>((bf16*)qkv, qk8, v8t, sc, N);
+  else
+    attn_quant_fp8_kernel<<<dim3(N / 64, 3, B * H), 256, 0, s>>>((bf16*)qkv, qk8, v8t, sc, N, H);
   UVA_LAUNCH_CHECK();
   return 0;
 }

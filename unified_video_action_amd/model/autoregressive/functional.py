@@ -64,11 +64,22 @@ def compute_weight_t(p):
     return t
 
 
+def linear_bias(x, p, b, out):
+    """out = x W^T + b for an epilogue-free bf16 product: hipBLASLt's bias-epilogue GEMM when
+    RT.blas_plain (bias rounded to bf16 first, as autocast's F.linear does), else gemm_8ph"""
+    if (RT.blas_plain & 1) and out.dtype == torch.bfloat16 and x.dtype == torch.bfloat16:
+        torch.addmm(compute_weight(b), x, compute_weight(p).t(), out=out)
+    else:
+        ops.linear(x, compute_weight(p), out, bias=b.detach())
+
+
 def linear_dx_w(dy, p, dx):
     """dX = dy @ W of nn.Linear(W: [out, in]).  bf16 with RT.dx_wt_layout and an output 768 wide:
     through the transposed weight copy as a forward-layout GEMM (K-contiguous B operand: 17-27 %
     faster on the 128 x 384 tile than the transposed-B read path); otherwise the dX GEMM."""
-    if cdt() == torch.bfloat16 and RT.dx_wt_layout and dx.shape[1] % 384 == 0 and dx.shape[1] < 1024:
+    if (RT.blas_plain & 2) and cdt() == torch.bfloat16 and dx.dtype == torch.bfloat16:
+        torch.mm(dy, compute_weight(p), out=dx)
+    elif cdt() == torch.bfloat16 and RT.dx_wt_layout and dx.shape[1] % 384 == 0 and dx.shape[1] < 1024:
         ops.linear(dy, compute_weight_t(p), dx)
     else:
         ops.linear_dx(dy, compute_weight(p), dx)
@@ -255,7 +266,7 @@ class BlockFn(torch.autograd.Function):
         r1 = torch.empty(M, dtype=F32, device=dev)
         ops.layernorm_fwd(x, n1w.detach(), n1b.detach(), h1, m1, r1)
         qkv = torch.empty(M, 3 * D, dtype=c, device=dev)
-        ops.linear(h1, compute_weight(qkvw), qkv, bias=qkvb.detach())
+        linear_bias(h1, qkvw, qkvb, qkv)
         flash = use_flash(N, D // H)
         if flash:
             o = torch.empty(M, D, dtype=c, device=dev)
@@ -289,10 +300,10 @@ class BlockFn(torch.autograd.Function):
         if c == torch.bfloat16 and RT.mlp_split_epilogue:
             # bias-only GEMMs (autocast: fc1 / fc2 outputs are bf16 before GELU / dropout / the fp32
             # residual add) + one elementwise pass each; same dropout masks (flat element index)
-            ops.linear(h2, compute_weight(fc1w), pre1, bias=fc1b.detach())
+            linear_bias(h2, fc1w, fc1b, pre1)
             ops.act_drop_fwd(pre1, a, "gelu", drop_p=p_proj, seed=seeds[2])
             t2 = torch.empty(M, D, dtype=c, device=dev)
-            ops.linear(a, compute_weight(fc2w), t2, bias=fc2b.detach())
+            linear_bias(a, fc2w, fc2b, t2)
             ops.act_drop_fwd(t2, x2, "none", drop_p=p_proj, seed=seeds[3], residual=x1)
             del t2
         else:
@@ -327,7 +338,10 @@ class BlockFn(torch.autograd.Function):
             ops.colsum(dpre1, grad_buf(fc1b))
         else:
             da = torch.empty(M, Hd, dtype=c, device=dev)
-            ops.linear_dx(dpre2, compute_weight(fc2w), da)
+            if (RT.blas_plain & 2) and da.dtype == torch.bfloat16:
+                torch.mm(dpre2, compute_weight(fc2w), out=da)
+            else:
+                ops.linear_dx(dpre2, compute_weight(fc2w), da)
             ops.act_bwd_bias(pre1, da, dpre1, grad_buf(fc1b), "gelu", drop_p=p_proj, seed=seeds[2])
             del da
         del dpre2

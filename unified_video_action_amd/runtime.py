@@ -42,6 +42,10 @@ class _Runtime:
         # dX products of width-768 outputs through transposed bf16 weight copies (forward-layout GEMM)
         # (UVA_DX_WT=0 switches it off: A/B runs of bench.py)
         self.dx_wt_layout = os.environ.get("UVA_DX_WT", "1") != "0"
+        # the Block's epilogue-free products (qkv / fc1 / fc2 forward with a bias, fc2 dX) as plain
+        # library GEMMs (hipBLASLt through torch.addmm / mm); every fused-epilogue product and all dW
+        # products stay on gemm_8ph.  Bit mask (UVA_BLAS_PLAIN: A/B runs): 1 forward, 2 dX products
+        self.blas_plain = int(os.environ.get("UVA_BLAS_PLAIN", "0"))
 
     def set_precision(self, name):
         name = str(name).lower()
