@@ -26,7 +26,8 @@
 #include "common.h"
 
 #define A8_MAX 448.0f
-// quantisation pass in its row form for H = 12 (attn_quant_fp8_rows_kernel)
+// quantisation pass in its row form for H = 12 (attn_quant_fp8_rows_kernel): measured level at
+// B32/N1024 (0.058 ms) and slower at B56/N1088 (0.176 vs 0.158 ms), profiles/r04/ab_blas_noslp_quantrows.txt
 #ifndef UVA_A8_QUANT_ROWS
 #define UVA_A8_QUANT_ROWS 0
 #endif
