@@ -459,8 +459,12 @@ class AdaLNTrunkFn(torch.autograd.Function):
         dout = as_dtype(gout, c)
         ops.linear_dw(dout, hf, grad_buf(lw))
         ops.colsum(dout, grad_buf(lb))
-        dhf = torch.empty(R, W, dtype=F32, device=dev)
-        ops.linear_dx(dout, compute_weight(lw), dhf)
+        lowp = bool(RT.blas_plain & 4) and c == torch.bfloat16  # bf16 dX on hipBLASLt (autocast's dtype)
+        dhf = torch.empty(R, W, dtype=c if lowp else F32, device=dev)
+        if lowp:
+            torch.mm(dout, compute_weight(lw), out=dhf)
+        else:
+            ops.linear_dx(dout, compute_weight(lw), dhf)
         dfmod = torch.empty(R, 2 * W, dtype=c, device=dev)
         dx = torch.empty(R, W, dtype=F32, device=dev)
         ops.layernorm_bwd(xf, None, dhf, meanf, rstdf, dx, accum=False, scale=fmod[:, W:], ldm=2 * W,
@@ -484,11 +488,17 @@ class AdaLNTrunkFn(torch.autograd.Function):
                 ops.colsum(dpre1, grad_buf(b1))
             else:
                 da = torch.empty(R, W, dtype=c, device=dev)
-                ops.linear_dx(dhm2, compute_weight(w2), da)
+                if lowp:
+                    torch.mm(dhm2, compute_weight(w2), out=da)
+                else:
+                    ops.linear_dx(dhm2, compute_weight(w2), da)
                 ops.act_bwd_bias(pre1, da, dpre1, grad_buf(b1), "silu")
             ops.linear_dw(dpre1, h, grad_buf(w1))
-            dh = torch.empty(R, W, dtype=F32, device=dev)
-            ops.linear_dx(dpre1, compute_weight(w1), dh)
+            dh = torch.empty(R, W, dtype=c if lowp else F32, device=dev)
+            if lowp:
+                torch.mm(dpre1, compute_weight(w1), out=dh)
+            else:
+                ops.linear_dx(dpre1, compute_weight(w1), dh)
             dxn = torch.empty(R, W, dtype=F32, device=dev)
             _ln_mod_bwd(x, lnw, lnb, mod, W, dh, mean, rstd, dxn, dmod, dx)
             ops.linear_dw(dmod, sy, grad_buf(modw))
