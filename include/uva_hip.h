@@ -72,6 +72,17 @@ long long uva_gemm_plan(int in_dtype, int ta, int tb, int M, int N, int K, int b
  * dropout products: 1 on, 0 off (default: measured 1-4 % slower than gemm_8ph),
  * -1 query.  Returns the previous setting. */
 int uva_gemm_set_persist(int on);
+/* Persistent 4-wave GEMM (gemm4.hip: one workgroup of 4 waves per CU, 256 x 256 / 256 x 192 block tiles,
+ * 128 x 128 / 128 x 96 per wave with AGPR accumulators, 4-slot LDS-DMA ring of 32-deep K substeps,
+ * register epilogue) for the K-contiguous (ta = tb = 0) products with a bias-only epilogue, batch 1,
+ * K % 128 == 0: uva_gemm routes them here (timm Block qkv / fc1 / fc2 forwards and the dX products
+ * through transposed weight copies, mar_con_unified.py:201-249).
+ * uva_gemm4_set(on, force): measurement switch (tests / tools): on = 0 sends those products back to the
+ * 8-phase kernel; force = tile configuration (0: 256x256, 1: 256x192; -1 automatic); -2 leaves a value
+ * unchanged; returns the previous (on | (force + 1) << 1).
+ * uva_gemm4_plan: cfg | grid << 8 the dispatcher would launch, -1 = not eligible (no device work). */
+int uva_gemm4_set(int on, int force);
+long long uva_gemm4_plan(int M, int N, int K);
 int uva_conv2d(int dtype, const void* in, const void* w, void* out, const float* bias, const void* residual, int Nimg,
                int Hin, int Win, int Ci, int Co, int ks, int stride, int pad_t, int pad_l, int Hout, int Wout,
                const float* gn_scale, const float* gn_shift, int gn_silu, int act, float* gn_part,

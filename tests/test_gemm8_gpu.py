@@ -23,7 +23,11 @@ def rel_err(a, b):
 def _seed():
     from unified_video_action_amd.native import ops  # fails loudly without the .so
     torch.manual_seed(0)
+    # the K-contiguous bias-only products go to the 4-wave kernel by default (tests/test_gemm4_gpu.py);
+    # this file pins gemm_8ph itself
+    prev = ops.gemm4_set(0)
     yield
+    ops.gemm4_set(prev[0])
 
 
 def _stored(op, t_flag):

@@ -1,0 +1,19 @@
+"""One-shot launches of a single product on the current route (for rocprofv3 --pmc passes; tools only).
+python tools/gemm4_one.py N K [iters]  (M = 32768, bias, bf16 out)"""
+import sys
+
+import torch
+
+sys.path.insert(0, ".")
+from unified_video_action_amd.native import ops  # noqa: E402
+
+N, K = int(sys.argv[1]), int(sys.argv[2])
+it = int(sys.argv[3]) if len(sys.argv) > 3 else 5
+M = 32768
+x = (torch.rand(M, K, device="cuda") * 2 - 1).to(torch.bfloat16)
+w = (torch.rand(N, K, device="cuda") * 2 - 1).to(torch.bfloat16)
+b = torch.rand(N, device="cuda")
+y = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
+for _ in range(it):
+    ops.linear(x, w, y, bias=b)
+torch.cuda.synchronize()

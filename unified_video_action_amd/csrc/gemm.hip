@@ -1948,10 +1948,22 @@ static int launch_8ph(int ta, int tb, const void* A, const void* B, void* C, int
   return 1;
 }
 
+extern "C" int uva_gemm4_try(int out_dtype, const void* A, const void* B, void* C, int M, int N, int K,
+                             long long lda, long long ldb, long long ldc, const float* bias, float alpha,
+                             hipStream_t s);
+
 template <typename TC>
 static int launch_mfma(int ta, int tb, const void* A, const void* B, void* C, int M, int N, int K, long long lda,
                        long long ldb, long long ldc, int batch, const BatchStrides& bs, const EpiParams& ep,
                        const ConvParams& cp, float* ws, long long ws_floats, hipStream_t s) {
+  // K-contiguous products with a bias-only epilogue: the persistent 4-wave kernel (gemm4.hip)
+  if (ta == 0 && tb == 0 && batch == 1 && !ep.residual && !ep.aux && !ep.gate && ep.act == 0 &&
+      ep.drop_thresh == 0 && ep.beta == 0.f && ep.res_grad == 0) {
+    const int r = uva_gemm4_try(sizeof(TC) == 2 ? UVA_DT_BF16 : UVA_DT_F32, A, B, C, M, N, K, lda, ldb, ldc, ep.bias,
+                                ep.alpha, s);
+    if (r < 0) return -r;
+    if (r > 0) return 0;
+  }
   {
     int r = launch_8ph<TC>(ta, tb, A, B, C, M, N, K, lda, ldb, ldc, batch, bs, ep, cp, ws, ws_floats, s);
     if (r < 0) return -r;

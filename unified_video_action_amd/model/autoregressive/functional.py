@@ -50,8 +50,8 @@ def compute_weight(p):
 
 def compute_weight_t(p):
     """transposed compute-dtype copy [in, out] of an fp32 [out, in] weight, rebuilt once per
-    parameter generation (the optimizer bumps RT.param_gen; RT.dx_wt_layout routes the dX products
-    through it)"""
+    parameter generation (the optimizer bumps RT.param_gen): the bf16 dX products run on it as
+    forward-layout (K-contiguous) GEMMs"""
     w = compute_weight(p)
     key = (p._version, p.data_ptr(), RT.param_gen)
     t = getattr(p, "_uva_shadow_t", None)
@@ -65,21 +65,16 @@ def compute_weight_t(p):
 
 
 def linear_bias(x, p, b, out):
-    """out = x W^T + b for an epilogue-free bf16 product: hipBLASLt's bias-epilogue GEMM when
-    RT.blas_plain (bias rounded to bf16 first, as autocast's F.linear does), else gemm_8ph"""
-    if (RT.blas_plain & 1) and out.dtype == torch.bfloat16 and x.dtype == torch.bfloat16:
-        torch.addmm(compute_weight(b), x, compute_weight(p).t(), out=out)
-    else:
-        ops.linear(x, compute_weight(p), out, bias=b.detach())
+    """out = x W^T + b for an epilogue-free product (the bf16 ones run on the persistent 4-wave kernel,
+    csrc/gemm4.hip)"""
+    ops.linear(x, compute_weight(p), out, bias=b.detach())
 
 
 def linear_dx_w(dy, p, dx):
-    """dX = dy @ W of nn.Linear(W: [out, in]).  bf16 with RT.dx_wt_layout and an output 768 wide:
-    through the transposed weight copy as a forward-layout GEMM (K-contiguous B operand: 17-27 %
-    faster on the 128 x 384 tile than the transposed-B read path); otherwise the dX GEMM."""
-    if (RT.blas_plain & 2) and cdt() == torch.bfloat16 and dx.dtype == torch.bfloat16:
-        torch.mm(dy, compute_weight(p), out=dx)
-    elif cdt() == torch.bfloat16 and RT.dx_wt_layout and dx.shape[1] % 384 == 0 and dx.shape[1] < 1024:
+    """dX = dy @ W of nn.Linear(W: [out, in]).  bf16: through the transposed weight copy as a
+    forward-layout GEMM (both operands K-contiguous: the 4-wave kernel); fp32 (parity mode): the
+    dX GEMM on the stored weight."""
+    if cdt() == torch.bfloat16:
         ops.linear(dy, compute_weight_t(p), dx)
     else:
         ops.linear_dx(dy, compute_weight(p), dx)
@@ -338,10 +333,7 @@ class BlockFn(torch.autograd.Function):
             ops.colsum(dpre1, grad_buf(fc1b))
         else:
             da = torch.empty(M, Hd, dtype=c, device=dev)
-            if (RT.blas_plain & 2) and da.dtype == torch.bfloat16:
-                torch.mm(dpre2, compute_weight(fc2w), out=da)
-            else:
-                ops.linear_dx(dpre2, compute_weight(fc2w), da)
+            linear_dx_w(dpre2, fc2w, da)
             ops.act_bwd_bias(pre1, da, dpre1, grad_buf(fc1b), "gelu", drop_p=p_proj, seed=seeds[2])
             del da
         del dpre2
@@ -459,12 +451,8 @@ class AdaLNTrunkFn(torch.autograd.Function):
         dout = as_dtype(gout, c)
         ops.linear_dw(dout, hf, grad_buf(lw))
         ops.colsum(dout, grad_buf(lb))
-        lowp = bool(RT.blas_plain & 4) and c == torch.bfloat16  # bf16 dX on hipBLASLt (autocast's dtype)
-        dhf = torch.empty(R, W, dtype=c if lowp else F32, device=dev)
-        if lowp:
-            torch.mm(dout, compute_weight(lw), out=dhf)
-        else:
-            ops.linear_dx(dout, compute_weight(lw), dhf)
+        dhf = torch.empty(R, W, dtype=F32, device=dev)
+        ops.linear_dx(dout, compute_weight(lw), dhf)
         dfmod = torch.empty(R, 2 * W, dtype=c, device=dev)
         dx = torch.empty(R, W, dtype=F32, device=dev)
         ops.layernorm_bwd(xf, None, dhf, meanf, rstdf, dx, accum=False, scale=fmod[:, W:], ldm=2 * W,
@@ -488,17 +476,11 @@ class AdaLNTrunkFn(torch.autograd.Function):
                 ops.colsum(dpre1, grad_buf(b1))
             else:
                 da = torch.empty(R, W, dtype=c, device=dev)
-                if lowp:
-                    torch.mm(dhm2, compute_weight(w2), out=da)
-                else:
-                    ops.linear_dx(dhm2, compute_weight(w2), da)
+                ops.linear_dx(dhm2, compute_weight(w2), da)
                 ops.act_bwd_bias(pre1, da, dpre1, grad_buf(b1), "silu")
             ops.linear_dw(dpre1, h, grad_buf(w1))
-            dh = torch.empty(R, W, dtype=c if lowp else F32, device=dev)
-            if lowp:
-                torch.mm(dpre1, compute_weight(w1), out=dh)
-            else:
-                ops.linear_dx(dpre1, compute_weight(w1), dh)
+            dh = torch.empty(R, W, dtype=F32, device=dev)
+            ops.linear_dx(dpre1, compute_weight(w1), dh)
             dxn = torch.empty(R, W, dtype=F32, device=dev)
             _ln_mod_bwd(x, lnw, lnb, mod, W, dh, mean, rstd, dxn, dmod, dx)
             ops.linear_dw(dmod, sy, grad_buf(modw))

@@ -90,6 +90,20 @@ def gemm_set_persist(on):
     return bool(lib().query("uva_gemm_set_persist", int(bool(on))))
 
 
+def gemm4_set(on=-2, force=-2):
+    """measurement switch of the persistent 4-wave kernel (tests / kernel benchmarks): on = 0 routes the
+    K-contiguous bias-only products back to gemm_8ph; force = tile configuration (-1 automatic); -2
+    leaves a value unchanged.  Returns the previous (on, force)."""
+    prev = lib().query("uva_gemm4_set", int(on), int(force))
+    return prev & 1, (prev >> 1) - 1
+
+
+def gemm4_plan(M, N, K):
+    """(configuration, grid) of the 4-wave kernel for an eligible K-contiguous product, None otherwise"""
+    code = lib().query("uva_gemm4_plan", M, N, K)
+    return None if code < 0 else (code & 255, code >> 8)
+
+
 def linear(x, w, out, bias=None, act="none", aux=None, residual=None, drop_p=0.0, seed=0, beta=0.0, gate=None):
     """out[M,N] = epi(x[M,K] @ w[N,K]^T) -- nn.Linear forward."""
     M, K = x.shape

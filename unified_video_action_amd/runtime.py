@@ -1,6 +1,5 @@
 """Process-wide runtime settings of the HIP path: compute precision and the per-call
 dropout seeds (counter-based masks need a distinct seed per op per step)."""
-import os
 import itertools
 
 import torch
@@ -39,15 +38,6 @@ class _Runtime:
         # bumped whenever HIP kernels rewrite parameters in place (optimizer / EMA steps): caches
         # keyed on parameters (non-static compute shadows, the sampler's captured graphs) compare it
         self.param_gen = 0
-        # dX products of width-768 outputs through transposed bf16 weight copies (forward-layout GEMM)
-        # (UVA_DX_WT=0 switches it off: A/B runs of bench.py)
-        self.dx_wt_layout = os.environ.get("UVA_DX_WT", "1") != "0"
-        # the Block's epilogue-free products (qkv / fc1 / fc2 forward with a bias, fc2 dX) as plain
-        # library GEMMs (hipBLASLt through torch.addmm / mm); every fused-epilogue product and all dW
-        # products stay on gemm_8ph.  Bit mask (UVA_BLAS_PLAIN: A/B runs): 1 forward, 2 dX products,
-        # 4 the DiffLoss trunk's dX products in bf16 (autocast's input-grad dtype) on hipBLASLt.
-        # 3 measured +0.7 % on the bench (256.3 vs 254.5 samples/s, profiles/r04/ab_blas_noslp_quantrows.txt)
-        self.blas_plain = int(os.environ.get("UVA_BLAS_PLAIN", "3"))
 
     def set_precision(self, name):
         name = str(name).lower()
