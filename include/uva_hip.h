@@ -272,7 +272,8 @@ int uva_attn_fwd_fp8(const void* workspace, void* out, float* lse2, const void* 
  *      row log-sum-exp, Dvec: [B,H,N] scratch, dqkv: [B,N,3,H,64].  N % 64 == 0.
  * uva_attn_dropmask: keep-mask bit planes (uva_attn_mask_bytes bytes) of the counter-hash
  *      dropout (p, seed) -- generated once per step, consumed by fwd and bwd (drop_p > 0).
- * uva_attn_bwd: workspace of uva_attn_bwd_workspace bytes (dO/(1-p) when drop_p > 0, else none). */
+ * uva_attn_bwd: workspace of uva_attn_bwd_workspace bytes (0 in this build: the loops run on the unscaled dO;
+ * the query stays for ABI stability). */
 long long uva_attn_mask_bytes(int B, int N, int H);
 long long uva_attn_bwd_workspace(int B, int N, int H, float drop_p);
 int uva_attn_dropmask(void* mask, int B, int N, int H, float drop_p, unsigned long long seed, hipStream_t stream);

@@ -97,7 +97,9 @@ def _tiny_worker(rank, world, port, q, defer=False):
     assert not red.tail_handles
     for h in handles:
         h.remove()
-    q.put((rank, (store.grad / world).clone()))
+    # a numpy copy: a torch tensor crosses the queue as a shared-memory fd that the parent can only
+    # attach while this process is alive (it may exit first)
+    q.put((rank, (store.grad / world).numpy().copy()))
     dist.destroy_process_group()
 
 
@@ -110,7 +112,7 @@ def test_grad_reducer_world2_matches_single_process(defer):
     procs = [ctx.Process(target=_tiny_worker, args=(r, world, port, q, defer)) for r in range(world)]
     for p in procs:
         p.start()
-    res = dict(q.get(timeout=100) for _ in range(world))
+    res = {r: torch.from_numpy(a) for r, a in (q.get(timeout=100) for _ in range(world))}
     for p in procs:
         p.join(timeout=30)
     assert torch.allclose(res[0], res[1])

@@ -405,12 +405,12 @@ __global__ __launch_bounds__(256, OCC) void attn_fwd_kernel(const bf16* __restri
 }
 
 // =====================================================================================
-// backward prologue: D[bh][q] = sum_d dO*O; dO' = dO * dsc when dropping (so the keep scale
-// costs nothing in the loops).  8 lanes per (b, q, h) row of 64, 16-B loads.
+// backward prologue: D'[bh][q] = dmul * sum_d dO*O (dmul = 1 / dsc when dropping: the loops run on the
+// unscaled dO, see uva_attn_bwd).  8 lanes per (b, q, h) row of 64, 16-B loads.
 // =====================================================================================
 __global__ __launch_bounds__(256) void attn_bwd_pre_kernel(const bf16* __restrict__ out, const bf16* __restrict__ dout,
-                                                           float* __restrict__ Dvec, bf16* __restrict__ dOs,
-                                                           long long rows, int N, int H, float dsc, float dmul) {
+                                                           float* __restrict__ Dvec, long long rows, int N, int H,
+                                                           float dmul) {
   const long long t = (long long)blockIdx.x * 256 + threadIdx.x;
   const long long row = t >> 3;  // (b*N + q)*H + h
   const int sub = threadIdx.x & 7;
@@ -422,12 +422,6 @@ __global__ __launch_bounds__(256) void attn_bwd_pre_kernel(const bf16* __restric
     const bf16x8 d = *(const bf16x8*)(dout + e);
 #pragma unroll
     for (int j = 0; j < 8; ++j) v += (float)o[j] * (float)d[j];
-    if (dOs) {
-      bf16x8 sc;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) sc[j] = (bf16)((float)d[j] * dsc);
-      *(bf16x8*)(dOs + e) = sc;
-    }
   }
   v += __shfl_xor(v, 1, 64);
   v += __shfl_xor(v, 2, 64);
@@ -889,7 +883,8 @@ extern "C" long long uva_attn_mask_bytes(int B, int N, int H) {
 }
 
 extern "C" long long uva_attn_bwd_workspace(int B, int N, int H, float drop_p) {
-  return drop_p > 0.f ? (long long)B * N * H * 64 * 2 : 0;  // dO / (1 - p), bf16
+  (void)B; (void)N; (void)H; (void)drop_p;
+  return 0;  // the loops run on the unscaled dO (no scaled copy)
 }
 
 extern "C" int uva_attn_dropmask(void* mask, int B, int N, int H, float drop_p, unsigned long long seed,
@@ -941,7 +936,7 @@ extern "C" int uva_attn_bwd(const void* qkv, const void* out, const void* dout, 
   // end (no scaled dO copy: one [B N H 64] bf16 write + its re-reads per layer saved)
   (void)workspace;
   attn_bwd_pre_kernel<<<(unsigned)((rows * 8 + 255) / 256), 256, 0, s>>>((const bf16*)out, (const bf16*)dout, Dvec,
-                                                                         nullptr, rows, N, H, ds, 1.0f / ds);
+                                                                         rows, N, H, 1.0f / ds);
   const int nt = N / 64;
   const uint64_t* MQ = (const uint64_t*)mask;
   const uint64_t* MK = drop ? MQ + (long long)B * H * N * nt : nullptr;

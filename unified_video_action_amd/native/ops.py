@@ -26,26 +26,39 @@ def stream():
     return torch.cuda.current_stream().cuda_stream
 
 
-# ---- live kernel tracing (bench.py roofline): HIP events around selected launches ----------
+# ---- live kernel tracing (bench.py roofline / per-step accounting): HIP events around launches ----
 TRACE = None  # dict tag -> list[(start_event, end_event, flops)] when enabled
 
 
 class _traced:
+    """events around one library call on the current stream; only the outermost of nested scopes
+    records, so every launch is counted once (the explicitly tagged ops carry shapes and FLOPs, every
+    other entry point is tagged by its C-ABI name through _call)"""
     __slots__ = ("tag", "flops", "ev")
+    depth = 0
 
     def __init__(self, tag, flops):
-        self.tag, self.flops = tag, flops
+        self.tag, self.flops, self.ev = tag, flops, None
 
     def __enter__(self):
-        if TRACE is not None:
+        if TRACE is not None and _traced.depth == 0:
             self.ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
             self.ev[0].record()
+        _traced.depth += 1
         return self
 
     def __exit__(self, *a):
-        if TRACE is not None:
+        _traced.depth -= 1
+        if self.ev is not None:
             self.ev[1].record()
-            TRACE.setdefault(self.tag, []).append((self.ev[0], self.ev[1], self.flops))
+            if TRACE is not None:
+                TRACE.setdefault(self.tag, []).append((self.ev[0], self.ev[1], self.flops))
+
+
+def _call(name, *args):
+    """lib().call under a trace scope tagged by the entry point's name (no FLOP count)"""
+    with _traced(name[4:] if name.startswith("uva_") else name, 0.0):
+        return lib().call(name, *args)
 
 
 def _ld(t):
@@ -65,7 +78,7 @@ def gemm(A, B, C, M, N, K, lda, ldb, ldc, ta=0, tb=0, batch=1, inner=1, sA=(0, 0
         assert aux.dtype == C.dtype
     with _traced(f"gemm[{'NT'[ta]}{'NT'[tb]}] {'bf16' if dt(A) else 'f32'} M{M} N{N} K{K} b{batch}",
                  2.0 * M * N * K * batch):
-        lib().call("uva_gemm", dt(A), dt(C), ta, tb, ptr(A), ptr(B), ptr(C), M, N, K, lda, ldb, ldc, batch, inner,
+        _call("uva_gemm", dt(A), dt(C), ta, tb, ptr(A), ptr(B), ptr(C), M, N, K, lda, ldb, ldc, batch, inner,
                    sA[0], sA[1], sB[0], sB[1], sC[0], sC[1], ptr(bias), ptr(residual), ldr, sR[0], sR[1], ptr(aux),
                    ACT[act] if isinstance(act, str) else act, float(alpha), float(beta), float(drop_p),
                    int(seed) & 0xFFFFFFFFFFFFFFFF, dt(residual) if residual is not None else 0, ptr(gate), ldg,
@@ -156,13 +169,13 @@ def workspace(n_floats, device):
 def colsum(x, out, accum=True):
     rows, cols = x.shape
     ws = workspace(lib().query("uva_colsum_workspace", rows, cols), x.device)
-    lib().call("uva_colsum", dt(x), ptr(x), _ld(x), ptr(out), rows, cols, int(accum), ptr(ws), stream())
+    _call("uva_colsum", dt(x), ptr(x), _ld(x), ptr(out), rows, cols, int(accum), ptr(ws), stream())
 
 
 def layernorm_fwd(x, w, b, y, mean, rstd, eps=1e-6, scale=None, shift=None, ldm=0):
     rows, D = x.shape
     assert x.is_contiguous() and y.is_contiguous()
-    lib().call("uva_layernorm_fwd", dt(x), dt(y), ptr(x), ptr(w), ptr(b), ptr(scale), ptr(shift), ldm, ptr(y),
+    _call("uva_layernorm_fwd", dt(x), dt(y), ptr(x), ptr(w), ptr(b), ptr(scale), ptr(shift), ldm, ptr(y),
                ptr(mean), ptr(rstd), rows, D, float(eps), stream())
 
 
@@ -176,7 +189,7 @@ def layernorm_bwd(x, w, dy, mean, rstd, dx, accum, dw=None, db=None, scale=None,
     ws = None
     if dw is not None:
         ws = workspace(lib().query("uva_layernorm_bwd_workspace", rows, D), x.device)
-    lib().call("uva_layernorm_bwd", dt(x), odt, ptr(x), ptr(w), ptr(b), ptr(scale), ldm, ptr(dy), dt(dy), ptr(mean),
+    _call("uva_layernorm_bwd", dt(x), odt, ptr(x), ptr(w), ptr(b), ptr(scale), ldm, ptr(dy), dt(dy), ptr(mean),
                ptr(rstd),
                ptr(dx_base), ptr(dx), int(accum), ptr(dscale), ptr(dshift), ptr(dw), ptr(db), int(accum_wb), ptr(ws), rows, D,
                stream())
@@ -184,13 +197,13 @@ def layernorm_bwd(x, w, dy, mean, rstd, dx, accum, dw=None, db=None, scale=None,
 
 def softmax_fwd(S, P, Pd, L, scale, drop_p=0.0, seed=0):
     rows = S.numel() // L
-    lib().call("uva_softmax_fwd", dt(S), ptr(S), ptr(P), ptr(Pd), rows, L, float(scale), float(drop_p),
+    _call("uva_softmax_fwd", dt(S), ptr(S), ptr(P), ptr(Pd), rows, L, float(scale), float(drop_p),
                int(seed) & 0xFFFFFFFFFFFFFFFF, stream())
 
 
 def softmax_bwd(P, dPd, dS, L, scale, drop_p=0.0, seed=0):
     rows = P.numel() // L
-    lib().call("uva_softmax_bwd", dt(P), ptr(P), ptr(dPd), ptr(dS), rows, L, float(scale), float(drop_p),
+    _call("uva_softmax_bwd", dt(P), ptr(P), ptr(dPd), ptr(dS), rows, L, float(scale), float(drop_p),
                int(seed) & 0xFFFFFFFFFFFFFFFF, stream())
 
 
@@ -199,7 +212,7 @@ def transpose_bf16(src, dst):
     R, C = src.shape
     assert src.dtype == dst.dtype == torch.bfloat16 and src.is_contiguous() and dst.is_contiguous()
     assert tuple(dst.shape) == (C, R)
-    lib().call("uva_transpose_bf16", ptr(src), ptr(dst), R, C, stream())
+    _call("uva_transpose_bf16", ptr(src), ptr(dst), R, C, stream())
 
 
 def cast(src, dst):
@@ -209,11 +222,11 @@ def cast(src, dst):
     else:
         rows, cols = src.shape
         lds, ldd = _ld(src), _ld(dst)
-    lib().call("uva_cast", dt(src), ptr(src), lds, dt(dst), ptr(dst), ldd, rows, cols, stream())
+    _call("uva_cast", dt(src), ptr(src), lds, dt(dst), ptr(dst), ldd, rows, cols, stream())
 
 
 def act_fwd(x, y, act):
-    lib().call("uva_act_fwd", dt(x), ptr(x), dt(y), ptr(y), x.numel(), ACT[act], stream())
+    _call("uva_act_fwd", dt(x), ptr(x), dt(y), ptr(y), x.numel(), ACT[act], stream())
 
 
 def act_drop_fwd(x, y, act="none", drop_p=0.0, seed=0, residual=None):
@@ -221,14 +234,14 @@ def act_drop_fwd(x, y, act="none", drop_p=0.0, seed=0, residual=None):
     assert x.is_contiguous() and y.is_contiguous() and x.numel() == y.numel()
     if residual is not None:
         assert residual.is_contiguous() and residual.numel() == x.numel()
-    lib().call("uva_act_drop_fwd", dt(x), ptr(x), dt(y), ptr(y), dt(residual) if residual is not None else 0,
+    _call("uva_act_drop_fwd", dt(x), ptr(x), dt(y), ptr(y), dt(residual) if residual is not None else 0,
                ptr(residual), x.numel(), ACT[act], float(drop_p), int(seed) & 0xFFFFFFFFFFFFFFFF, stream())
 
 
 def act_bwd(pre, dy, dx, act, drop_p=0.0, seed=0, accum=False):
     """dx (+)= dy * dropout_mask * act'(pre); 2-D views (pre contiguous)."""
     rows, cols = dy.shape
-    lib().call("uva_act_bwd", dt(pre) if pre is not None else F32, ptr(pre), dt(dy), ptr(dy), _ld(dy), dt(dx),
+    _call("uva_act_bwd", dt(pre) if pre is not None else F32, ptr(pre), dt(dy), ptr(dy), _ld(dy), dt(dx),
                ptr(dx), _ld(dx), rows, cols, ACT[act], float(drop_p), int(seed) & 0xFFFFFFFFFFFFFFFF, int(accum),
                stream())
 
@@ -237,19 +250,19 @@ def act_bwd_bias(pre, dy, dx, dbias, act, drop_p=0.0, seed=0, accum=False, accum
     """act_bwd + dbias (+)= column sums of dx (one pass: the nn.Linear bias gradient)."""
     rows, cols = dy.shape
     ws = workspace(lib().query("uva_act_bwd_bias_workspace", rows, cols), dy.device)
-    lib().call("uva_act_bwd_bias", dt(pre) if pre is not None else F32, ptr(pre), dt(dy), ptr(dy), _ld(dy), dt(dx),
+    _call("uva_act_bwd_bias", dt(pre) if pre is not None else F32, ptr(pre), dt(dy), ptr(dy), _ld(dy), dt(dx),
                ptr(dx), _ld(dx), rows, cols, ACT[act], float(drop_p), int(seed) & 0xFFFFFFFFFFFFFFFF, int(accum),
                ptr(dbias), int(accum_bias), ptr(ws), stream())
 
 
 def gate_bwd(dout, h, gate, dh, dgate):
     rows, cols = dout.shape
-    lib().call("uva_gate_bwd", ptr(dout), dt(h), ptr(h), dt(gate), ptr(gate), _ld(gate), dt(dh), ptr(dh),
+    _call("uva_gate_bwd", ptr(dout), dt(h), ptr(h), dt(gate), ptr(gate), _ld(gate), dt(dh), ptr(dh),
                ptr(dgate), rows, cols, stream())
 
 
 def fill(t, v):
-    lib().call("uva_fill", ptr(t), t.numel(), float(v), stream())
+    _call("uva_fill", ptr(t), t.numel(), float(v), stream())
 
 
 def _tables_arg(tables):
@@ -260,19 +273,19 @@ def _tables_arg(tables):
 def q_sample(x0, noise, t, tables, xt):
     rows, C = x0.shape
     arr = _tables_arg(tables)
-    lib().call("uva_q_sample", ptr(x0), ptr(noise), ptr(t), ctypes.cast(arr, ctypes.c_void_p), dt(xt), ptr(xt),
+    _call("uva_q_sample", ptr(x0), ptr(noise), ptr(t), ctypes.cast(arr, ctypes.c_void_p), dt(xt), ptr(xt),
                rows, C, stream())
 
 
 def timestep_features(t, freqs, out):
     rows = t.numel()
-    lib().call("uva_timestep_features", ptr(t), ptr(freqs), dt(out), ptr(out), rows, freqs.numel(), stream())
+    _call("uva_timestep_features", ptr(t), ptr(freqs), dt(out), ptr(out), rows, freqs.numel(), stream())
 
 
 def diffusion_loss(x0, noise, t, out, tables, loss_row, dl):
     rows, C = x0.shape
     arr = _tables_arg(tables)
-    lib().call("uva_diffusion_loss", ptr(x0), ptr(noise), ptr(t), dt(out), ptr(out), _ld(out),
+    _call("uva_diffusion_loss", ptr(x0), ptr(noise), ptr(t), dt(out), ptr(out), _ld(out),
                ctypes.cast(arr, ctypes.c_void_p), ptr(loss_row), ptr(dl), rows, C, stream())
 
 
@@ -288,7 +301,7 @@ def sampler_persistent(pack, mod, coef, noise, x0, x_out, work, clip=True, eps=1
             raise ValueError("sampler_persistent: contiguous operands required")
     if mod.shape[:2] != (S, R) or coef.shape != (S, 8) or x0.shape != (R, C) or x_out.shape != (R, C):
         raise ValueError("sampler_persistent: shape mismatch")
-    lib().call("uva_sampler_persistent", R, C, W, depth, S, int(clip), float(eps), ptr(pack["w1"]), ptr(pack["b1"]),
+    _call("uva_sampler_persistent", R, C, W, depth, S, int(clip), float(eps), ptr(pack["w1"]), ptr(pack["b1"]),
                ptr(pack["w2"]), ptr(pack["b2"]), ptr(pack["lnw"]), ptr(pack["lnb"]), ptr(pack["win"]),
                ptr(pack["bin"]), ptr(pack["wf"]), ptr(pack["bfin"]), ptr(mod), mod.shape[2], ptr(coef), ptr(noise),
                ptr(x0), ptr(x_out), ptr(work), work.numel(), stream())
@@ -296,7 +309,7 @@ def sampler_persistent(pack, mod, coef, noise, x0, x_out, work, clip=True, eps=1
 
 def sampler_persistent_test_hook(no_publish=True):
     """tests only: the next uva_sampler_persistent launch publishes no phase (forces the give-up path)."""
-    lib().call("uva_sampler_persistent_test_hook", int(bool(no_publish)))
+    _call("uva_sampler_persistent_test_hook", int(bool(no_publish)))
 
 
 PERSISTENT_SAMPLER_CUS = 64  # workgroups of uva_sampler_persistent, one per CU, all co-resident
@@ -316,7 +329,7 @@ def sampler_persistent_workspace(W, device):
 def sampler_persistent_status(work):
     """1 if a spin of the last persistent sampler run on `work` gave up (results invalid); syncs."""
     flag = ctypes.c_uint(0)
-    lib().call("uva_sampler_persistent_status", ptr(work), ctypes.cast(ctypes.pointer(flag), ctypes.c_void_p),
+    _call("uva_sampler_persistent_status", ptr(work), ctypes.cast(ctypes.pointer(flag), ctypes.c_void_p),
                stream())
     return flag.value
 
@@ -332,7 +345,7 @@ def p_sample_step(out, x, noise, coef, x_new, x_net=None, clip=True):
     if x_net is not None and (not x_net.is_contiguous() or x_net.shape != x.shape):
         raise ValueError("p_sample_step: x_net must be contiguous [rows, C]")
     k = (ctypes.c_float * 8)(*coef)
-    lib().call("uva_p_sample_step", dt(out), ptr(out), out.stride(0), ptr(x), ptr(noise),
+    _call("uva_p_sample_step", dt(out), ptr(out), out.stride(0), ptr(x), ptr(noise),
                ctypes.cast(k, ctypes.c_void_p), ptr(x_new), dt(x_net) if x_net is not None else 0,
                ptr(x_net), int(clip), rows, C, stream())
 
@@ -356,23 +369,23 @@ def sampler_linear(A, W, out, bias=None, act="none", ln=False, lnw=None, lnb=Non
         ldm = shift.stride(0)
     ldg = gate.stride(0) if gate is not None else 0
     ldr = residual.stride(0) if residual is not None else 0
-    lib().call("uva_sampler_linear", int(ln), ptr(A), A.stride(0), ptr(lnw), ptr(lnb), ptr(shift), ptr(scale), ldm,
+    _call("uva_sampler_linear", int(ln), ptr(A), A.stride(0), ptr(lnw), ptr(lnb), ptr(shift), ptr(scale), ldm,
                float(eps), ptr(W), ptr(bias), ACT[act], ptr(gate), ldg, ptr(residual), ldr, dt(out), ptr(out),
                out.stride(0), R, N, K, stream())
 
 
 def weighted_mean(l, w, res):
-    lib().call("uva_weighted_mean", ptr(l), ptr(w), l.numel(), ptr(res), stream())
+    _call("uva_weighted_mean", ptr(l), ptr(w), l.numel(), ptr(res), stream())
 
 
 def loss_grad(dl, w, wsum, g_up, dout):
     rows, C2 = dl.shape
-    lib().call("uva_loss_grad", ptr(dl), ptr(w), ptr(wsum), ptr(g_up), dt(dout), ptr(dout), _ld(dout), rows, C2,
+    _call("uva_loss_grad", ptr(dl), ptr(w), ptr(wsum), ptr(g_up), dt(dout), ptr(dout), _ld(dout), rows, C2,
                stream())
 
 
 def adamw_ema(p, g, m, v, ema, p_bf16, n_decay, lr, b1, b2, eps, wd, step, grad_scale, ema_decay):
-    lib().call("uva_adamw_ema", ptr(p), ptr(g), ptr(m), ptr(v), ptr(ema), ptr(p_bf16), p.numel(), int(n_decay),
+    _call("uva_adamw_ema", ptr(p), ptr(g), ptr(m), ptr(v), ptr(ema), ptr(p_bf16), p.numel(), int(n_decay),
                float(lr), float(b1), float(b2), float(eps), float(wd), int(step), float(grad_scale),
                float(ema_decay), stream())
 
@@ -381,7 +394,7 @@ def ema_update(ema, p, decay):
     """ema = decay * ema + (1 - decay) * p over two flat fp32 buffers (uva_ema_update)."""
     if ema.dtype != torch.float32 or p.dtype != torch.float32 or ema.numel() != p.numel():
         raise ValueError("ema_update: two fp32 buffers of equal size")
-    lib().call("uva_ema_update", ptr(ema), ptr(p), ema.numel(), float(decay), stream())
+    _call("uva_ema_update", ptr(ema), ptr(p), ema.numel(), float(decay), stream())
 
 
 def attn_mask_alloc(B, N, H, device):
@@ -393,7 +406,7 @@ def attn_dropmask(B, N, H, drop_p, seed, device, out=None):
     attn_fwd and attn_bwd of the same step."""
     mask = attn_mask_alloc(B, N, H, device) if out is None else out
     assert mask.numel() == lib().query("uva_attn_mask_bytes", B, N, H) and mask.dtype == torch.uint8
-    lib().call("uva_attn_dropmask", ptr(mask), B, N, H, float(drop_p), int(seed) & 0xFFFFFFFFFFFFFFFF, stream())
+    _call("uva_attn_dropmask", ptr(mask), B, N, H, float(drop_p), int(seed) & 0xFFFFFFFFFFFFFFFF, stream())
     return mask
 
 
@@ -405,7 +418,7 @@ def attn_fwd(qkv, out, lse2, B, N, H, scale, drop_p=0.0, seed=0, mask=None):
     with _traced(f"attn_fwd B{B} N{N} H{H}", 4.0 * B * H * N * N * 64):
         if drop_p > 0 and mask is None:
             mask = attn_dropmask(B, N, H, drop_p, seed, qkv.device)
-        lib().call("uva_attn_fwd", ptr(qkv), ptr(out), ptr(lse2), ptr(mask) if drop_p > 0 else None, B, N, H,
+        _call("uva_attn_fwd", ptr(qkv), ptr(out), ptr(lse2), ptr(mask) if drop_p > 0 else None, B, N, H,
                    float(scale), float(drop_p), stream())
     return mask if drop_p > 0 else None
 
@@ -418,7 +431,7 @@ def attn_quant_fp8(qkv, ws, B, N, H):
     """round qkv [B,N,3,H,64] bf16 in place to the fp8 grid; fp8 Q/K, V^T and scales -> ws."""
     assert qkv.dtype == torch.bfloat16 and qkv.is_contiguous() and qkv.numel() == B * N * 3 * H * 64
     assert N % 64 == 0 and ws.dtype == torch.uint8 and ws.numel() >= lib().query("uva_attn_fp8_workspace", B, N, H)
-    lib().call("uva_attn_quant_fp8", ptr(qkv), ptr(ws), B, N, H, stream())
+    _call("uva_attn_quant_fp8", ptr(qkv), ptr(ws), B, N, H, stream())
 
 
 def attn_fwd_fp8(ws, out, lse2, B, N, H, scale, drop_p=0.0, seed=0, mask=None, device=None):
@@ -428,7 +441,7 @@ def attn_fwd_fp8(ws, out, lse2, B, N, H, scale, drop_p=0.0, seed=0, mask=None, d
     with _traced(f"attn_fwd_fp8 B{B} N{N} H{H}", 4.0 * B * H * N * N * 64):
         if drop_p > 0 and mask is None:
             mask = attn_dropmask(B, N, H, drop_p, seed, out.device)
-        lib().call("uva_attn_fwd_fp8", ptr(ws), ptr(out), ptr(lse2), ptr(mask) if drop_p > 0 else None, B, N, H,
+        _call("uva_attn_fwd_fp8", ptr(ws), ptr(out), ptr(lse2), ptr(mask) if drop_p > 0 else None, B, N, H,
                    float(scale), float(drop_p), stream())
     return mask if drop_p > 0 else None
 
@@ -441,7 +454,7 @@ def attn_bwd(qkv, out, dout, lse2, dvec, dqkv, B, N, H, scale, drop_p=0.0, seed=
             mask = attn_dropmask(B, N, H, drop_p, seed, qkv.device)
         nb = lib().query("uva_attn_bwd_workspace", B, N, H, float(drop_p))
         ws = torch.empty(nb, dtype=torch.uint8, device=qkv.device) if nb else None
-        lib().call("uva_attn_bwd", ptr(qkv), ptr(out), ptr(dout), ptr(lse2), ptr(mask) if drop_p > 0 else None,
+        _call("uva_attn_bwd", ptr(qkv), ptr(out), ptr(dout), ptr(lse2), ptr(mask) if drop_p > 0 else None,
                    ptr(dvec), ptr(dqkv), ptr(ws), B, N, H, float(scale), float(drop_p), stream())
 
 
@@ -460,7 +473,7 @@ def conv2d(x, w, out, Nimg, Hin, Win, Ci, Co, ks, stride, pad_t, pad_l, Hout, Wo
 
 def _conv_call(x, w, out, Nimg, Hin, Win, Ci, Co, ks, stride, pad_t, pad_l, Hout, Wout, bias, residual, gn_scale,
                gn_shift, gn_silu, act, force_generic, gn_part):
-    lib().call("uva_conv2d", dt(x), ptr(x), ptr(w), ptr(out), ptr(bias), ptr(residual), Nimg, Hin, Win, Ci, Co, ks,
+    _call("uva_conv2d", dt(x), ptr(x), ptr(w), ptr(out), ptr(bias), ptr(residual), Nimg, Hin, Win, Ci, Co, ks,
                stride, pad_t, pad_l, Hout, Wout, ptr(gn_scale), ptr(gn_shift), int(gn_silu), ACT[act], ptr(gn_part),
                int(force_generic), stream())
 
@@ -476,26 +489,26 @@ def pool4x4_cwh(x, out, n, C):
     """AdaptiveAvgPool2d((4,4)) of NHWC [n,16,16,C] flattened (c w h) -> out [n, 16 C]"""
     assert x.is_contiguous() and out.is_contiguous() and x.dtype == out.dtype
     assert x.numel() == n * 256 * C and out.numel() == n * 16 * C
-    lib().call("uva_pool4x4_cwh", dt(x), ptr(x), ptr(out), n, C, stream())
+    _call("uva_pool4x4_cwh", dt(x), ptr(x), ptr(out), n, C, stream())
 
 
 def pool4x4_relu_bwd(post, gpool, dpre, n, C):
     assert post.is_contiguous() and gpool.is_contiguous() and dpre.is_contiguous() and post.dtype == dpre.dtype
     assert post.numel() == dpre.numel() == n * 256 * C and gpool.numel() == n * 16 * C
-    lib().call("uva_pool4x4_relu_bwd", dt(post), ptr(post), dt(gpool), ptr(gpool), ptr(dpre), n, C, stream())
+    _call("uva_pool4x4_relu_bwd", dt(post), ptr(post), dt(gpool), ptr(gpool), ptr(dpre), n, C, stream())
 
 
 def im2col3x3(x, cols, n, H, W, Ci):
     assert x.is_contiguous() and cols.is_contiguous() and x.dtype == cols.dtype
     assert x.numel() == n * H * W * Ci and cols.numel() == n * H * W * Ci * 9
-    lib().call("uva_im2col3x3", dt(x), ptr(x), ptr(cols), n, H, W, Ci, stream())
+    _call("uva_im2col3x3", dt(x), ptr(x), ptr(cols), n, H, W, Ci, stream())
 
 
 def im2col3x3_tc(x, cols, n, H, W, Ci):
     """tap-major im2col: cols[p][tap*Ci + ci] (uva_im2col3x3_tc)."""
     assert x.is_contiguous() and cols.is_contiguous() and x.dtype == cols.dtype
     assert x.numel() == n * H * W * Ci and cols.numel() == n * H * W * Ci * 9
-    lib().call("uva_im2col3x3_tc", dt(x), ptr(x), ptr(cols), n, H, W, Ci, stream())
+    _call("uva_im2col3x3_tc", dt(x), ptr(x), ptr(cols), n, H, W, Ci, stream())
 
 
 def conv3x3_dw_scatter_add(part, grad):
@@ -503,39 +516,39 @@ def conv3x3_dw_scatter_add(part, grad):
     Co, Ci = grad.shape[0], grad.shape[1]
     assert part.dtype == grad.dtype == torch.float32 and part.is_contiguous() and grad.is_contiguous()
     assert part.numel() == grad.numel() == Co * Ci * 9
-    lib().call("uva_conv3x3_dw_scatter_add", ptr(part), ptr(grad), Co, Ci, stream())
+    _call("uva_conv3x3_dw_scatter_add", ptr(part), ptr(grad), Co, Ci, stream())
 
 
 def conv3x3_weight_layout(w, out, mode):
     """fp32 nn.Conv2d weight [Co,Ci,3,3] -> mode 0 [Co,3,3,Ci] / mode 1 flipped [Ci,3,3,Co]"""
     Co, Ci = w.shape[0], w.shape[1]
     assert w.dtype == torch.float32 and w.is_contiguous() and out.is_contiguous() and out.numel() == w.numel()
-    lib().call("uva_conv3x3_weight_layout", ptr(w), dt(out), ptr(out), Co, Ci, int(mode), stream())
+    _call("uva_conv3x3_weight_layout", ptr(w), dt(out), ptr(out), Co, Ci, int(mode), stream())
 
 
 def groupnorm_finalize_tiles(part, Nimg, HW, C, gamma, beta, scale, shift, eps=1e-6, tile_rows=128):
-    lib().call("uva_groupnorm_finalize_tiles", ptr(part), Nimg, HW, C, tile_rows, ptr(gamma), ptr(beta), float(eps),
+    _call("uva_groupnorm_finalize_tiles", ptr(part), Nimg, HW, C, tile_rows, ptr(gamma), ptr(beta), float(eps),
                ptr(scale), ptr(shift), stream())
 
 
 def groupnorm_apply(x, scale, shift, y, Nimg, HW, C, silu=True):
-    lib().call("uva_groupnorm_apply", ptr(x), ptr(scale), ptr(shift), ptr(y), Nimg, HW, C, int(silu), stream())
+    _call("uva_groupnorm_apply", ptr(x), ptr(scale), ptr(shift), ptr(y), Nimg, HW, C, int(silu), stream())
 
 
 def groupnorm_stats(x, Nimg, HW, C, gamma, beta, scale, shift, eps=1e-6):
     ws = workspace(lib().query("uva_groupnorm_workspace", Nimg, HW), x.device)
-    lib().call("uva_groupnorm_stats", dt(x), ptr(x), Nimg, HW, C, ptr(gamma), ptr(beta), float(eps), ptr(scale),
+    _call("uva_groupnorm_stats", dt(x), ptr(x), Nimg, HW, C, ptr(gamma), ptr(beta), float(eps), ptr(scale),
                ptr(shift), ptr(ws), stream())
 
 
 def resize_select(img, sel, out, Cpad):
     B, T, C, H, W = img.shape
     assert C == 3 and img.dtype == torch.float32 and img.is_contiguous()
-    lib().call("uva_resize_select", ptr(img), B, T, H, W, ptr(sel), sel.numel(), dt(out), ptr(out), Cpad, stream())
+    _call("uva_resize_select", ptr(img), B, T, H, W, ptr(sel), sel.numel(), dt(out), ptr(out), Cpad, stream())
 
 
 def posterior_sample(moments, eps, z, Nimg, scale=0.2325):
-    lib().call("uva_posterior_sample", dt(moments), ptr(moments), ptr(eps), ptr(z), Nimg, float(scale), stream())
+    _call("uva_posterior_sample", dt(moments), ptr(moments), ptr(eps), ptr(z), Nimg, float(scale), stream())
 
 
 def upsample_nearest2x(x, y):
@@ -543,4 +556,4 @@ def upsample_nearest2x(x, y):
     n, H, W, C = x.shape
     if not (x.is_contiguous() and y.is_contiguous() and y.shape == (n, 2 * H, 2 * W, C) and y.dtype == x.dtype):
         raise ValueError(f"upsample_nearest2x: {tuple(x.shape)} -> {tuple(y.shape)}")
-    lib().call("uva_upsample_nearest2x", dt(x), ptr(x), ptr(y), n, H, W, C, stream())
+    _call("uva_upsample_nearest2x", dt(x), ptr(x), ptr(y), n, H, W, C, stream())

@@ -170,9 +170,11 @@ class TrainUnifiedVideoActionWorkspace(BaseWorkspace):
         self.ema_model = copy.deepcopy(self.model) if cfg.training.use_ema else None
         self.optimizer = self.model.get_optimizer(**cfg.model.policy.optimizer)
         # train_step calls optimizer.step() right after backward (no gradient reader between): the
-        # DP tail all-reduce may overlap the AdamW of the already-reduced buckets
+        # DP tail all-reduce may overlap the AdamW of the already-reduced buckets.  Only with one
+        # backward per step: under gradient accumulation the next micro-step's backward would write
+        # the encoder-input gradients while their deferred all-reduce is still in flight
         if hasattr(self.optimizer, "overlap_tail"):
-            self.optimizer.overlap_tail = True
+            self.optimizer.overlap_tail = int(cfg.training.get("gradient_accumulate_every", 1) or 1) == 1
         self.global_step = 0
         self.epoch = 0
 
