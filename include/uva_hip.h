@@ -72,17 +72,24 @@ long long uva_gemm_plan(int in_dtype, int ta, int tb, int M, int N, int K, int b
  * dropout products: 1 on, 0 off (default: measured 1-4 % slower than gemm_8ph),
  * -1 query.  Returns the previous setting. */
 int uva_gemm_set_persist(int on);
-/* Persistent 4-wave GEMM (gemm4.hip: one workgroup of 4 waves per CU, 256 x 256 / 256 x 192 block tiles,
- * 128 x 128 / 128 x 96 per wave with AGPR accumulators, 4-slot LDS-DMA ring of 32-deep K substeps,
- * register epilogue) for the K-contiguous (ta = tb = 0) products with a bias-only epilogue, batch 1,
- * K % 128 == 0: uva_gemm routes them here (timm Block qkv / fc1 / fc2 forwards and the dX products
- * through transposed weight copies, mar_con_unified.py:201-249).
+/* Persistent 4-wave GEMM (gemm4.hip: one workgroup of 4 waves per CU, 256 x 192 block tiles, 128 x 96
+ * per wave with AGPR accumulators, a 2-region LDS-DMA ring of 64-deep K-tiles read as two 32-deep
+ * substeps, register epilogue through buffer stores).  uva_gemm routes to it
+ *   - the K-contiguous (ta = tb = 0) products with a bias-only epilogue, batch 1, K % 128 == 0: the timm
+ *     Block qkv / fc1 / fc2 forwards and the dX products through transposed weight copies
+ *     (mar_con_unified.py:201-249);
+ *   - the fp32 dW products (ta = tb = 1, plain epilogue incl. beta, K = tokens % 128 == 0): (tile,
+ *     K-slice) work items writing fp32 partial slabs into the split-K workspace, reduced in slice order
+ *     (deterministic) by the same reduce as the other split-K paths.
  * uva_gemm4_set(on, force): measurement switch (tests / tools): on = 0 sends those products back to the
- * 8-phase kernel; force = tile configuration (0: 256x256, 1: 256x192; -1 automatic); -2 leaves a value
- * unchanged; returns the previous (on | (force + 1) << 1).
- * uva_gemm4_plan: cfg | grid << 8 the dispatcher would launch, -1 = not eligible (no device work). */
+ * 8-phase kernel; force = tile configuration (1: 256x192; -1 automatic); -2 leaves a value unchanged;
+ * returns the previous (on | (force + 1) << 1).
+ * uva_gemm4_plan: cfg | grid << 8 the dispatcher would launch for a K-contiguous product, -1 = not
+ * eligible; uva_gemm4_plan_tt: splits | grid << 8 for a dW product with ws_floats of workspace, -1 = not
+ * eligible (no device work). */
 int uva_gemm4_set(int on, int force);
 long long uva_gemm4_plan(int M, int N, int K);
+long long uva_gemm4_plan_tt(int M, int N, int K, long long ws_floats);
 int uva_conv2d(int dtype, const void* in, const void* w, void* out, const float* bias, const void* residual, int Nimg,
                int Hin, int Win, int Ci, int Co, int ks, int stride, int pad_t, int pad_l, int Hout, int Wout,
                const float* gn_scale, const float* gn_shift, int gn_silu, int act, float* gn_part,
@@ -259,7 +266,8 @@ int uva_ema_update(float* ema, const float* p, long long n, float decay, hipStre
  *      qkv [B,N,3,H,64] IN PLACE to the fp8 grid (the backward then runs uva_attn_bwd on it:
  *      straight-through rounding) and fills `workspace` (uva_attn_fp8_workspace bytes, 256-B
  *      aligned) with the fp8 Q/K rows, the key-permuted fp8 V^T and the scales.
- * uva_attn_fwd_fp8: Q.K^T and P.V on v_mfma_f32_16x16x32_fp8_fp8, fp32 online softmax; out / lse2
+ * uva_attn_fwd_fp8: Q.K^T and P.V on the block-scaled v_mfma_scale_f32_32x32x64_f8f6f4 (e4m3
+ *      operands, per-tile E8M0 scales as MFMA operands), fp32 online softmax; out / lse2
  *      / mask as uva_attn_fwd.  N % 64 == 0. */
 long long uva_attn_fp8_workspace(int B, int N, int H);
 int uva_attn_quant_fp8(void* qkv, void* workspace, int B, int N, int H, hipStream_t stream);

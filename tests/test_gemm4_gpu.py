@@ -106,3 +106,61 @@ def test_gemm4_ineligible_shapes_fall_back():
         out = torch.empty(M, N, device=DEV)
         ops.linear(a, w, out)
         assert rel_err(out, a.float() @ w.float().t()) < 5e-3
+
+
+# dW products (ta = tb = 1: A = dY [tokens][out], B = X [tokens][in], fp32 gradient C[out][in]) routed
+# to the 4-wave kernel (<= 16 tiles): the Block's proj at B = 32 (mar_con_unified.py:201-215), ragged
+# edges, a K that does not split evenly, a single-slice case
+TT_CASES = [(768, 768, 32768), (1000, 584, 4096), (300, 200, 512), (768, 768, 33280), (1024, 768, 256),
+            (768, 960, 8192)]
+
+
+@pytest.mark.parametrize("beta", [0.0, 1.0])
+@pytest.mark.parametrize("M,N,K", TT_CASES)
+def test_gemm4_dw_vs_fp32(M, N, K, beta):
+    from unified_video_action_amd.native import ops
+    plan = ops.gemm4_plan_tt(M, N, K)
+    assert plan is not None, plan
+    dy = torch.randn(K, M, device=DEV).to(torch.bfloat16)
+    x = torch.randn(K, N, device=DEV).to(torch.bfloat16)
+    dw0 = torch.randn(M, N, device=DEV)
+    dw = dw0.clone() if beta else torch.full((M, N), float("nan"), device=DEV)
+    ops.linear_dw(dy, x, dw, beta=beta)
+    ref = dy.float().t() @ x.float() + (dw0 if beta else 0.0)
+    assert torch.isfinite(dw).all()
+    err = rel_err(dw, ref)
+    assert err < 5e-3, (err, plan)
+
+
+def test_gemm4_dw_matches_8ph_and_repeatable():
+    """the dW product on the 4-wave kernel agrees with the 8-phase route to fp32-accumulation noise and
+    is bit-repeatable (slices reduced in a fixed order)"""
+    from unified_video_action_amd.native import ops
+    M, N, K = 768, 768, 32768
+    dy = torch.randn(K, M, device=DEV).to(torch.bfloat16)
+    x = torch.randn(K, N, device=DEV).to(torch.bfloat16)
+    o1 = torch.zeros(M, N, device=DEV)
+    o2 = torch.zeros(M, N, device=DEV)
+    o8 = torch.zeros(M, N, device=DEV)
+    ops.linear_dw(dy, x, o1)
+    ops.linear_dw(dy, x, o2)
+    assert torch.equal(o1, o2)
+    prev = ops.gemm4_set(0)
+    try:
+        ops.linear_dw(dy, x, o8)
+    finally:
+        ops.gemm4_set(prev[0])
+    assert rel_err(o1, o8) < 1e-5
+
+
+def test_gemm4_dw_strided_operands():
+    """dY / X inside wider rows (the qkv slice of a fused buffer), ldc > N"""
+    from unified_video_action_amd.native import ops
+    M, N, K = 768, 768, 8192
+    A = torch.randn(K, M + 64, device=DEV).to(torch.bfloat16)
+    B = torch.randn(K, N + 128, device=DEV).to(torch.bfloat16)
+    C = torch.zeros(M, N + 256, device=DEV)
+    ops.gemm(A, B, C, M, N, K, M + 64, N + 128, N + 256, 1, 1, alpha=0.5)
+    ref = 0.5 * (A[:, :M].float().t() @ B[:, :N].float())
+    assert rel_err(C[:, :N], ref) < 5e-3
+    assert (C[:, N:] == 0).all()

@@ -117,6 +117,13 @@ def gemm4_plan(M, N, K):
     return None if code < 0 else (code & 255, code >> 8)
 
 
+def gemm4_plan_tt(M, N, K, ws_floats=None):
+    """(splits, grid) of the 4-wave kernel for an eligible dW (ta = tb = 1, fp32 output) product with the
+    default split-K workspace, None otherwise"""
+    code = lib().query("uva_gemm4_plan_tt", M, N, K, SPLITK_WS_FLOATS if ws_floats is None else ws_floats)
+    return None if code < 0 else (code & 255, code >> 8)
+
+
 def linear(x, w, out, bias=None, act="none", aux=None, residual=None, drop_p=0.0, seed=0, beta=0.0, gate=None):
     """out[M,N] = epi(x[M,K] @ w[N,K]^T) -- nn.Linear forward."""
     M, K = x.shape
