@@ -87,14 +87,6 @@ int uva_gemm_set_persist(int on);
  * uva_gemm4_plan: cfg | grid << 8 the dispatcher would launch for a K-contiguous product, -1 = not
  * eligible; uva_gemm4_plan_tt: splits | grid << 8 for a dW product with ws_floats of workspace, -1 = not
  * eligible (no device work). */
-/* Persistent 4-wave halo conv (conv4.hip: 16 x 16-pixel tiles x 128 channels per workgroup, one
- * workgroup per CU, AGPR accumulators, weights by LDS-DMA through a 3-region ring, the next chunk's
- * halo DMA'd raw and GroupNorm + SiLU'd in place under the MFMAs) for the Ci = Co = 128 3x3 / s1 / p1
- * convs (KL-VAE ResnetBlocks, vaekl.py:56-113); uva_conv2d / uva_conv3x3_halo route eligible shapes
- * here.  uva_conv4_ok: 1 if the shape is routed; uva_conv4_set(on): measurement switch (tests / tools;
- * -1 queries), returns the previous setting. */
-int uva_conv4_ok(int Nimg, int H, int W, int Ci, int Co);
-int uva_conv4_set(int on);
 int uva_gemm4_set(int on, int force);
 long long uva_gemm4_plan(int M, int N, int K);
 long long uva_gemm4_plan_tt(int M, int N, int K, long long ws_floats);

@@ -1585,21 +1585,10 @@ static int halo_bn(int Nimg, int H, int W, int Ci, int Co) {
 
 extern "C" int uva_conv3x3_halo_bn(int Nimg, int H, int W, int Ci, int Co) { return halo_bn(Nimg, H, W, Ci, Co); }
 
-extern "C" int uva_conv4_try(const void* in, const void* w, void* out, const float* bias, const void* residual,
-                             int Nimg, int H, int W, int Ci, int Co, const float* gn_scale, const float* gn_shift,
-                             int gn_silu, float* gn_part, hipStream_t s);
-
 extern "C" int uva_conv3x3_halo(const void* in, const void* w, void* out, const float* bias, const void* residual,
                                 int Nimg, int H, int W, int Ci, int Co, const float* gn_scale, const float* gn_shift,
                                 int gn_silu, float* gn_part, hipStream_t stream) {
   if (Nimg <= 0) return 0;
-  {
-    // Ci = Co = 128: the persistent 4-wave kernel (conv4.hip)
-    const int r = uva_conv4_try(in, w, out, bias, residual, Nimg, H, W, Ci, Co, gn_scale, gn_shift, gn_silu, gn_part,
-                                stream);
-    if (r < 0) return -r;
-    if (r > 0) return 0;
-  }
   const int bn = halo_bn(Nimg, H, W, Ci, Co);
   if (!bn || (((uintptr_t)in | (uintptr_t)w | (uintptr_t)out | (uintptr_t)residual) % 16)) return (int)hipErrorInvalidValue;
   if ((gn_scale == nullptr) != (gn_shift == nullptr)) return (int)hipErrorInvalidValue;

@@ -428,7 +428,7 @@ static int g4_cus() {
   return n;
 }
 
-// -1 = automatic; otherwise the configuration index of g4_cfgs (measurement / tests)
+// -1 = automatic; otherwise the configuration index (1: 256 x 192)
 static int g_gemm4_force = -1;
 static int g_gemm4_on = 1;
 
@@ -498,10 +498,11 @@ extern "C" int uva_gemm4_try(int out_dtype, const void* A, const void* B, void* 
   const G4Choice c = g4_plan(M, N, K);
   if (c.cfg < 0) return 0;
   int r;
-  if (out_dtype == UVA_DT_BF16)
+  if (out_dtype == UVA_DT_BF16) {
     r = g4_launch<8, 6, 0, 0, bf16>(A, B, C, M, N, K, lda, ldb, ldc, bias, alpha, c.grid, 1, K, 0, s);
-  else
+  } else {
     r = g4_launch<8, 6, 0, 0, float>(A, B, C, M, N, K, lda, ldb, ldc, bias, alpha, c.grid, 1, K, 0, s);
+  }
   return r ? -r : 1;
 }
 

@@ -485,16 +485,6 @@ def _conv_call(x, w, out, Nimg, Hin, Win, Ci, Co, ks, stride, pad_t, pad_l, Hout
                int(force_generic), stream())
 
 
-def conv4_set(on=-1):
-    """measurement switch of the persistent 4-wave halo conv (tests / tools): 0 routes its shapes back to
-    the two-workgroup halo kernels, -1 queries; returns the previous setting"""
-    return lib().query("uva_conv4_set", int(on))
-
-
-def conv4_ok(Nimg, H, W, Ci, Co):
-    return lib().query("uva_conv4_ok", Nimg, H, W, Ci, Co) == 1
-
-
 def conv_fuses_gn(Nimg, H, W, Ci, Co, ks, stride, dtype=torch.bfloat16):
     """True when uva_conv2d runs this conv on the halo kernel, which applies a GroupNorm(+SiLU)
     prologue while staging its input tile (no separate GN-apply pass needed)."""
