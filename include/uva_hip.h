@@ -113,6 +113,10 @@ int uva_pool4x4_relu_bwd(int dtype, const void* post, int gdtype, const void* gp
                          hipStream_t stream);
 int uva_im2col3x3(int dtype, const void* in, void* cols, int n, int H, int W, int Ci, hipStream_t stream);
 int uva_im2col3x3_tc(int dtype, const void* in, void* cols, int n, int H, int W, int Ci, hipStream_t stream);
+/* uva_pad_nhwc: [n][H][W][C] -> [G + n (H+2) (W+2) + G][C], zero 1-pixel border and G zero guard rows
+ *      at each end: with dY and X both padded, the weight gradient of a 3x3 / p1 conv is 9 plain GEMMs
+ *      dW[:, tap, :] = dYp^T Xp(shifted by (kh-1)(W+2) + (kw-1) rows), G >= W + 3 (no im2col). */
+int uva_pad_nhwc(int dtype, const void* in, void* out, int n, int H, int W, int C, int G, hipStream_t stream);
 int uva_conv3x3_dw_scatter_add(const float* part, float* grad, int Co, int Ci, hipStream_t stream);
 int uva_conv3x3_weight_layout(const float* w, int out_dtype, void* out, int Co, int Ci, int mode, hipStream_t stream);
 int uva_conv3x3_halo_bn(int Nimg, int H, int W, int Ci, int Co);

@@ -1,7 +1,7 @@
 """conv_fc action trunk kernels (diffusion_action_loss.py:42-61) vs plain PyTorch fp32:
 Conv2d(D, D, 3, p=1) + ReLU + AdaptiveAvgPool2d((4, 4)) + flatten (c w h) forward and backward
-through ConvReluPoolFn (HIP conv, pool-(c w h), fused pool/ReLU backward, tap-major im2col + dW scatter-add,
-weight layouts), fp32 (1e-5 of scale) and bf16 (2e-2); and the generic GEMM's split-K path for
+through ConvReluPoolFn (HIP conv, pool-(c w h), fused pool/ReLU backward, implicit-GEMM dW over padded
+operands + dW scatter-add, weight layouts), fp32 (1e-5 of scale) and bf16 (2e-2); and the generic GEMM's split-K path for
 tiny-output, long-K products (the Linear(4 -> 16) frame-interpolation dW)."""
 import pytest
 import torch
@@ -17,7 +17,7 @@ def rel_err(a, b):
 
 
 @pytest.mark.parametrize("prec,tol", [("fp32", 1e-5), ("bf16", 2e-2)])
-@pytest.mark.parametrize("n,D", [(8, 64), (12, 768)])
+@pytest.mark.parametrize("n,D", [(8, 64), (12, 768), (64, 768)])
 def test_conv_relu_pool_fwd_bwd_vs_torch(prec, tol, n, D):
     from unified_video_action_amd.model.autoregressive.diffusion_action_loss import ConvReluPoolFn
     from unified_video_action_amd.runtime import RT, cdt
@@ -122,6 +122,40 @@ def test_im2col_tap_major_and_dw_scatter_add(dtype):
     want = grad + part.reshape(Co, 3, 3, Ci).permute(0, 3, 1, 2)
     ops.conv3x3_dw_scatter_add(part, grad)
     assert torch.equal(grad, want)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_pad_nhwc_zero_border_and_guards(dtype):
+    """uva_pad_nhwc: out rows [G, G + n(H+2)(W+2)) hold x with a zero 1-pixel border, the G guard
+    rows on either side are zero (bit-exact)."""
+    from unified_video_action_amd.native import ops
+    n, H, W, C = 3, 5, 7, 16
+    G = W + 3
+    x = (torch.randn(n, H, W, C, device=DEV) * 4).to(dtype)
+    out = torch.full((2 * G + n * (H + 2) * (W + 2), C), float("nan"), device=DEV, dtype=dtype)
+    ops.pad_nhwc(x, out, n, H, W, C, G)
+    ref = F.pad(x.float(), (0, 0, 1, 1, 1, 1)).reshape(-1, C)
+    ref = torch.cat([torch.zeros(G, C, device=DEV), ref, torch.zeros(G, C, device=DEV)])
+    assert torch.equal(out.float(), ref)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("n,Co,Ci", [(2, 24, 16), (12, 768, 768), (64, 768, 768), (5, 64, 128)])
+def test_conv3x3_dw_implicit_vs_torch(dtype, n, Co, Ci):
+    """The action trunk's dW as 9 shifted-row GEMMs over padded dY / X (no im2col):
+    part[co][tap*Ci + ci] == conv2d_weight's dW[co][ci][kh][kw] (fp32 reference on the same operands).
+    n = 64 gives K = n*18*18 = 20736 (a multiple of 128): the persistent split-K dW route."""
+    from unified_video_action_amd.native import ops
+    H = W = 16
+    torch.manual_seed(n + Co)
+    dy = torch.randn(n, H, W, Co, device=DEV).to(dtype)
+    x = torch.randn(n, H, W, Ci, device=DEV).to(dtype)
+    part = torch.full((Co, 9 * Ci), float("nan"), device=DEV)
+    ops.conv3x3_dw_implicit(dy, x, part, n, H, W, Co, Ci)
+    ref = torch.nn.grad.conv2d_weight(x.double().permute(0, 3, 1, 2), (Co, Ci, 3, 3),
+                                      dy.double().permute(0, 3, 1, 2), padding=1)
+    got = part.reshape(Co, 3, 3, Ci).permute(0, 3, 1, 2)
+    assert rel_err(got, ref) < (1e-5 if dtype == torch.float32 else 2e-3)
 
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])

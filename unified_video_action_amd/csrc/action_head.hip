@@ -2,8 +2,8 @@
 // ReLU + AdaptiveAvgPool2d((4, 4)) + flatten (c w h)), so that its forward and backward run without
 // ATen copies: the pooled features come out already flattened in (c, w, h) order, the pool's
 // backward is fused with the ReLU mask, the conv weight changes layout in one pass, and the
-// weight gradient's im2col operand is built with its columns in the nn.Conv2d (ci, kh, kw) order,
-// so dW = dpre^T cols accumulates straight into the [Co][Ci][3][3] gradient.
+// weight gradient is an implicit GEMM per tap over spatially padded dY / X (uva_pad_nhwc; the im2col
+// builders below remain for tests and external callers).
 // Tensors: activations NHWC [n][16][16][C] (first spatial axis = the reference's w).
 #include "common.h"
 
@@ -188,6 +188,45 @@ extern "C" int uva_im2col3x3_tc(int dtype, const void* in, void* cols, int n, in
     im2col3x3_tc_kernel<bf16><<<nblocks(work), 256, 0, s>>>((const bf16*)in, (bf16*)cols, n, H, W, Ci);
   else
     im2col3x3_tc_kernel<float><<<nblocks(work), 256, 0, s>>>((const float*)in, (float*)cols, n, H, W, Ci);
+  UVA_LAUNCH_CHECK();
+  return 0;
+}
+
+// out[G + (img (H+2) + y) (W+2) + x][c] = in[img][y - 1][x - 1][c] inside, 0 on the 1-pixel border and in
+// the G guard rows before / after (the padded operands of the implicit-GEMM weight gradient: with both
+// dY and X padded, tap (kh, kw) is the constant row shift (kh - 1)(W + 2) + (kw - 1)); 16 B per thread
+template <typename T>
+__global__ __launch_bounds__(256) void pad_nhwc_kernel(const T* __restrict__ in, T* __restrict__ out, int n, int H,
+                                                       int W, int C, int G) {
+  constexpr int V = 16 / sizeof(T);
+  const int cv = C / V;
+  const long long rows = 2LL * G + (long long)n * (H + 2) * (W + 2);
+  const long long t = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (t >= rows * cv) return;
+  const long long r = t / cv;
+  const int c = (int)(t - r * cv) * V;
+  uint4 v = make_uint4(0u, 0u, 0u, 0u);
+  const long long q = r - G;
+  if (q >= 0 && q < (long long)n * (H + 2) * (W + 2)) {
+    const int x = (int)(q % (W + 2));
+    const long long q2 = q / (W + 2);
+    const int y = (int)(q2 % (H + 2));
+    const long long img = q2 / (H + 2);
+    if (y >= 1 && y <= H && x >= 1 && x <= W)
+      v = *(const uint4*)(in + ((img * H + (y - 1)) * W + (x - 1)) * C + c);
+  }
+  *(uint4*)(out + r * C + c) = v;
+}
+
+extern "C" int uva_pad_nhwc(int dtype, const void* in, void* out, int n, int H, int W, int C, int G, hipStream_t s) {
+  if (n <= 0) return 0;
+  const int V = dtype == UVA_DT_BF16 ? 8 : 4;
+  if (C % V || G < 0 || (((uintptr_t)in | (uintptr_t)out) % 16)) return (int)hipErrorInvalidValue;
+  const long long work = (2LL * G + (long long)n * (H + 2) * (W + 2)) * (C / V);
+  if (dtype == UVA_DT_BF16)
+    pad_nhwc_kernel<bf16><<<nblocks(work), 256, 0, s>>>((const bf16*)in, (bf16*)out, n, H, W, C, G);
+  else
+    pad_nhwc_kernel<float><<<nblocks(work), 256, 0, s>>>((const float*)in, (float*)out, n, H, W, C, G);
   UVA_LAUNCH_CHECK();
   return 0;
 }

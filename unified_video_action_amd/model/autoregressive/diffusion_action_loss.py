@@ -20,8 +20,9 @@ class ConvReluPoolFn(torch.autograd.Function):
     """Conv2d(D, D, 3, p=1) + bias + ReLU + AdaptiveAvgPool2d((4, 4)) + flatten (c w h) of NHWC
     [n, 16, 16, D] (diffusion_action_loss.py:42-47, 113-124); weight in nn.Conv2d layout [Co, Ci, 3, 3].
     No ATen kernels: the weight changes layout in one HIP pass, the pool writes (c w h) directly,
-    the backward fuses the pool's broadcast with the ReLU mask, and dW = dpre^T im2col(x) over tap-major
-    im2col columns (16-B vector gather) is added into the Conv2d-layout gradient by a scatter-add pass."""
+    the backward fuses the pool's broadcast with the ReLU mask, and dW is 9 GEMMs over zero-padded
+    copies of dpre / x (a tap = a constant row shift: no im2col), added into the Conv2d-layout gradient
+    by a scatter-add pass."""
 
     @staticmethod
     def forward(ctx, x, weight, bias):
@@ -52,13 +53,11 @@ class ConvReluPoolFn(torch.autograd.Function):
         ops.conv3x3_weight_layout(weight.detach(), wt, 1)
         dx = torch.empty(n, H, W, Ci, dtype=cd, device=g.device)
         ops.conv2d(dpre, wt, dx, n, H, W, Co, Ci, 3, 1, 1, 1, H, W)
-        # dW[co][(kh, kw, ci)] = dpre^T im2col(x) over tap-major columns (16-B vector gather), then
-        # added into the nn.Conv2d-layout gradient [co][ci][kh][kw]
-        cols = torch.empty(n * H * W, 9 * Ci, dtype=cd, device=g.device)
-        ops.im2col3x3_tc(xc, cols, n, H, W, Ci)
+        # dW[co][(kh, kw, ci)] as an implicit GEMM: dpre and x zero-padded to 18 x 18 (plus guard rows),
+        # so tap (kh, kw) is a constant row shift of x -- 9 GEMMs over the padded pixels, no im2col --
+        # then added into the nn.Conv2d-layout gradient [co][ci][kh][kw]
         part = torch.empty(Co, 9 * Ci, dtype=F32, device=g.device)
-        ops.linear_dw(dpre.reshape(-1, Co), cols, part, beta=0.0)
-        del cols
+        ops.conv3x3_dw_implicit(dpre, xc, part, n, H, W, Co, Ci)
         ops.conv3x3_dw_scatter_add(part, grad_buf(weight))
         ops.colsum(dpre.reshape(-1, Co), grad_buf(bias))
         return as_dtype(dx, ctx.xdt), None, None

@@ -518,6 +518,29 @@ def im2col3x3_tc(x, cols, n, H, W, Ci):
     _call("uva_im2col3x3_tc", dt(x), ptr(x), ptr(cols), n, H, W, Ci, stream())
 
 
+def pad_nhwc(x, out, n, H, W, C, G):
+    """out[G + (img (H+2) + y) (W+2) + x] = x[img][y-1][x-1] (zero border and G zero guard rows)."""
+    assert x.is_contiguous() and out.is_contiguous() and x.dtype == out.dtype
+    assert out.numel() == (2 * G + n * (H + 2) * (W + 2)) * C
+    _call("uva_pad_nhwc", dt(x), ptr(x), ptr(out), n, H, W, C, G, stream())
+
+
+def conv3x3_dw_implicit(dy, x, part, n, H, W, Co, Ci):
+    """part[co][kh*3 + kw][ci] = sum_p dy[p][co] x[p + tap shift][ci] (fp32, overwritten): the weight
+    gradient of a 3x3 / p1 conv over NHWC dy [n,H,W,Co] / x [n,H,W,Ci] as 9 GEMMs on padded copies."""
+    G = W + 3
+    K = n * (H + 2) * (W + 2)
+    dyp = torch.empty(2 * G + K, Co, dtype=dy.dtype, device=dy.device)
+    xp = torch.empty(2 * G + K, Ci, dtype=x.dtype, device=x.device)
+    pad_nhwc(dy, dyp, n, H, W, Co, G)
+    pad_nhwc(x, xp, n, H, W, Ci, G)
+    for kh in range(3):
+        for kw in range(3):
+            tap = kh * 3 + kw
+            d = (kh - 1) * (W + 2) + (kw - 1)
+            gemm(dyp[G:], xp[G + d:], part[:, tap * Ci:], Co, Ci, K, Co, Ci, 9 * Ci, 1, 1, beta=0.0)
+
+
 def conv3x3_dw_scatter_add(part, grad):
     """grad[co][ci][kh][kw] += part[co][kh*3 + kw][ci] (fp32)."""
     Co, Ci = grad.shape[0], grad.shape[1]
