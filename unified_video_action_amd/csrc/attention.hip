@@ -152,46 +152,61 @@ __device__ __forceinline__ float quad_max(float v) {
 __host__ __device__ constexpr int mask_pos(int k) { return ((k >> 2) & 3) * 16 + (k >> 4) * 4 + (k & 3); }
 
 // =====================================================================================
-// dropout bit planes: one wave per (bh, query tile qb, key tile kv)
+// dropout bit planes: one wave per (bh, query tile qb, MASK_TPW consecutive key tiles)
 // =====================================================================================
+// Lane L hashes the 32 pairs of (query q, 64 keys of tile kv) and shifts each element's DROP bit
+// (the sign of u16 - th) into its plane word by v_alignbit, visiting positions 63..0 in descending
+// order (pair j holds positions mask_pos(2j), even, and +1): two ops per element instead of the
+// and / sub / shift / or sequence (hash-only floor 65 us, kernel 81 vs 108 us at B32 N1024 H12,
+// bit-identical planes; tools/probe/mask_probe.hip).  Several key tiles per wave amortise the
+// (wave-uniform) index arithmetic.
+constexpr int MASK_TPW = 4;
+__device__ __forceinline__ uint32_t shift_in_sign(uint32_t acc, uint32_t t) {
+  return __builtin_amdgcn_alignbit(acc, t, 31);  // (acc << 1) | (t >> 31)
+}
 __global__ __launch_bounds__(256) void attn_mask_kernel(uint64_t* __restrict__ MQ, uint64_t* __restrict__ MK, int N,
-                                                        int nt, long long tasks, uint32_t th, uint64_t seed) {
-  const long long task = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (task >= tasks) return;  // wave-uniform
+                                                        int nt, long long waves, uint32_t th, uint64_t seed) {
+  // wave index in an SGPR (the host bounds waves < 2^31), so the index divisions are scalar
+  const long long wv = __builtin_amdgcn_readfirstlane((int)(blockIdx.x * 4u + (threadIdx.x >> 6)));
+  if (wv >= waves) return;  // wave-uniform
   const int L = threadIdx.x & 63;
-  const int kv = (int)(task % nt);
-  const long long t2 = task / nt;
+  const int per_row = (nt + MASK_TPW - 1) / MASK_TPW;
+  const int kv0 = (int)(wv % per_row) * MASK_TPW;
+  const long long t2 = wv / per_row;
   const int qb = (int)(t2 % nt);
   const long long bh = t2 / nt;
   const int q = qb * 64 + mask_pos(L);  // lane L holds the query whose MK bit is L
   const uint32_t key = drop_key(seed);
-  const uint64_t pair0 = (((uint64_t)bh * N + q) * (uint64_t)N + (uint64_t)kv * 64) >> 1;
-  // pair0 is a multiple of 32 (N % 64 == 0), so pair0 + j (j < 32) changes only its low 5 bits:
-  // drop_hash's first word for pair j is x0 ^ j (no 64-bit arithmetic in the loop)
-  const uint32_t x0 = drop_first(key, pair0);
-  uint32_t lo = 0, hi = 0;  // DROP bits of this lane's query (bit mask_pos(k) <-> key kv*64 + k)
+  const uint64_t rowpair = (((uint64_t)bh * N + q) * (uint64_t)N) >> 1;
+#pragma unroll 1
+  for (int kv = kv0; kv < kv0 + MASK_TPW && kv < nt; ++kv) {
+    // pair0 = rowpair + 32 kv is a multiple of 32 (N % 64 == 0), so pair0 + j (j < 32) changes only
+    // its low 5 bits: drop_hash's first word for pair j is x0 ^ j
+    const uint32_t x0 = drop_first(key, rowpair + (uint64_t)kv * 32);
+    uint32_t lo = 0, hi = 0;  // DROP bits of this lane's query (bit mask_pos(k) <-> key kv*64 + k)
 #pragma unroll
-  for (int j = 0; j < 32; ++j) {
-    const uint32_t hv = drop_mix(x0 ^ (uint32_t)j);
-    // element dropped iff its 16-bit draw < th: the sign of draw - th
-    const uint32_t d0 = ((hv & 0xFFFFu) - th) >> 31, d1 = ((hv >> 16) - th) >> 31;
-    const int p0 = mask_pos(2 * j), p1 = mask_pos(2 * j + 1);
-    if (p0 < 32) lo |= d0 << p0; else hi |= d0 << (p0 - 32);
-    if (p1 < 32) lo |= d1 << p1; else hi |= d1 << (p1 - 32);
-  }
-  lo = ~lo;
-  hi = ~hi;
-  MQ[((long long)bh * nt + kv) * N + q] = ((uint64_t)hi << 32) | lo;
-  // 64x64 bit transpose across the wave (rows = lanes): afterwards lane L' holds, at bit L, the
-  // bit mask_pos(L') of lane L, i.e. keep(query with MK position L, key kv*64 + mask_pos(L')).
-  // Branch-free: per stage the lane's shift amounts and keep mask are selects, the exchange a
-  // ds_swizzle (xor within 32 lanes) or v_permlane32_swap (the 32-lane stage).
-  {
-    const bool up = L & 32;
-    const auto r = __builtin_amdgcn_permlane32_swap(up ? lo : hi, up ? lo : hi, false, false);
-    const uint32_t o = up ? r[0] : r[1];  // the other half's word
-    if (up) lo = o; else hi = o;
-  }
+    for (int P = 31; P >= 0; --P) {
+      const uint32_t x = drop_mix(x0 ^ (uint32_t)(mask_pos(2 * P) >> 1));
+      const uint32_t t0 = (x & 0xFFFFu) - th, t1 = (x >> 16) - th;  // dropped iff negative
+      if (P >= 16) {
+        hi = shift_in_sign(shift_in_sign(hi, t1), t0);
+      } else {
+        lo = shift_in_sign(shift_in_sign(lo, t1), t0);
+      }
+    }
+    lo = ~lo;
+    hi = ~hi;
+    MQ[((long long)bh * nt + kv) * N + q] = ((uint64_t)hi << 32) | lo;
+    // 64x64 bit transpose across the wave (rows = lanes): afterwards lane L' holds, at bit L, the
+    // bit mask_pos(L') of lane L, i.e. keep(query with MK position L, key kv*64 + mask_pos(L')).
+    // Branch-free: per stage the lane's shift amounts and keep mask are selects, the exchange a
+    // ds_swizzle (xor within 32 lanes) or v_permlane32_swap (the 32-lane stage).
+    {
+      const bool up = L & 32;
+      const auto r = __builtin_amdgcn_permlane32_swap(up ? lo : hi, up ? lo : hi, false, false);
+      const uint32_t o = up ? r[0] : r[1];  // the other half's word
+      if (up) lo = o; else hi = o;
+    }
 #define UVA_TSTAGE(J, M)                                                                    \
   {                                                                                         \
     const bool up = L & (J);                                                                \
@@ -202,13 +217,14 @@ __global__ __launch_bounds__(256) void attn_mask_kernel(uint64_t* __restrict__ M
     lo = (lo & km) | (rl << sr);                                                            \
     hi = (hi & km) | (rh << sr);                                                            \
   }
-  UVA_TSTAGE(16, 0x0000FFFFu)
-  UVA_TSTAGE(8, 0x00FF00FFu)
-  UVA_TSTAGE(4, 0x0F0F0F0Fu)
-  UVA_TSTAGE(2, 0x33333333u)
-  UVA_TSTAGE(1, 0x55555555u)
+    UVA_TSTAGE(16, 0x0000FFFFu)
+    UVA_TSTAGE(8, 0x00FF00FFu)
+    UVA_TSTAGE(4, 0x0F0F0F0Fu)
+    UVA_TSTAGE(2, 0x33333333u)
+    UVA_TSTAGE(1, 0x55555555u)
 #undef UVA_TSTAGE
-  MK[((long long)bh * nt + qb) * N + (long long)kv * 64 + mask_pos(L)] = ((uint64_t)hi << 32) | lo;
+    MK[((long long)bh * nt + qb) * N + (long long)kv * 64 + mask_pos(L)] = ((uint64_t)hi << 32) | lo;
+  }
 }
 
 // =====================================================================================
@@ -896,8 +912,9 @@ extern "C" int uva_attn_dropmask(void* mask, int B, int N, int H, float drop_p, 
   const int nt = N / 64;
   uint64_t* MQ = (uint64_t*)mask;
   uint64_t* MK = MQ + (long long)B * H * N * nt;
-  const long long tasks = (long long)B * H * nt * nt;
-  attn_mask_kernel<<<dim3((unsigned)((tasks + 3) / 4)), 256, 0, s>>>(MQ, MK, N, nt, tasks, th, seed);
+  const long long waves = (long long)B * H * nt * ((nt + MASK_TPW - 1) / MASK_TPW);
+  if (waves > 0x7FFFFFFFLL) return (int)hipErrorInvalidValue;
+  attn_mask_kernel<<<dim3((unsigned)((waves + 3) / 4)), 256, 0, s>>>(MQ, MK, N, nt, waves, th, seed);
   UVA_LAUNCH_CHECK();
   return 0;
 }
