@@ -64,6 +64,29 @@ def test_conv_halo_matches_torch(n, H, W, Ci, Co, gn, residual):
     assert rel_err(gsh, sh_ref) < 1e-4
 
 
+@pytest.mark.parametrize("n,H,W,Ci,Co", [(3, 16, 16, 128, 128), (2, 32, 32, 256, 256)])
+@pytest.mark.parametrize("residual", [False, True])
+def test_conv_halo_gn_without_silu(n, H, W, Ci, Co, residual):
+    """GroupNorm prologue with gn_silu = 0 (the compile-time no-SiLU instantiations of the persistent and
+    single-tile GN kernels): out = bias + residual + conv3x3(x * scale + shift)."""
+    from unified_video_action_amd.native import ops
+    torch.manual_seed(n + H + Ci + int(residual))
+    x = torch.randn(n, H, W, Ci, device=DEV).to(torch.bfloat16)
+    w = (torch.randn(Co, 3, 3, Ci, device=DEV) * 0.05).to(torch.bfloat16)
+    bias = torch.randn(Co, device=DEV) * 0.1
+    sc = torch.rand(n, Ci, device=DEV) + 0.5
+    sh = torch.randn(n, Ci, device=DEV) * 0.3
+    res = torch.randn(n, H, W, Co, device=DEV).to(torch.bfloat16) if residual else None
+    out = torch.empty(n, H, W, Co, device=DEV, dtype=torch.bfloat16)
+    ops.conv2d(x, w, out, n, H, W, Ci, Co, 3, 1, 1, 1, H, W, bias=bias, residual=res, gn_scale=sc, gn_shift=sh,
+               gn_silu=False)
+    a = (x.float() * sc[:, None, None, :] + sh[:, None, None, :]).to(torch.bfloat16).float()
+    ref = F.conv2d(a.permute(0, 3, 1, 2), w.float().permute(0, 3, 1, 2), bias, padding=1).permute(0, 2, 3, 1)
+    if residual:
+        ref = ref + res.float()
+    assert rel_err(out.float(), ref) < 1e-2
+
+
 def test_conv_halo_eligibility():
     from unified_video_action_amd.native import ops
     assert ops.conv_fuses_gn(256, 256, 256, 128, 128, 3, 1)

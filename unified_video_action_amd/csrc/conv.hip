@@ -109,6 +109,48 @@ __device__ __forceinline__ bf16x8 lds_read16(const bf16* p) {
   return v;
 }
 
+typedef __attribute__((ext_vector_type(4))) unsigned ch_u32x4;
+
+// Halo geometry in 32-bit lane arithmetic: thread chunk p of a halo with CH_W = 18 columns sits at
+// (p / 18, p % 18); p < 2^15, so p / 18 = (p * 3641) >> 16 on the full-rate 24-bit multiplier (hipcc
+// lowers the plain division to a quarter-rate v_mul_hi_u32)
+__device__ __forceinline__ int ch_div18(int p) { return (int)(__umul24((unsigned)p, 3641u) >> 16); }
+// buffer descriptor over one image [H][W][C] bf16 (byte offsets < 2^31): per-lane offsets stay 32-bit
+// and the per-image base is scalar (no 64-bit address VALU per load)
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t ch_img_rsrc(const bf16* base, long long img, int img_elems) {
+  return __builtin_amdgcn_make_buffer_rsrc((void*)(base + img * img_elems), 0,
+                                           __builtin_amdgcn_readfirstlane(img_elems * 2), 0x00020000);
+}
+// byte offset of halo round i's pixel (clamped into the image) for the lane's 16-B channel chunk hc
+// of a 64-channel chunk (the chunk's offset goes into soffset)
+__device__ __forceinline__ unsigned ch_halo_off(int p, int oh0, int ow0, int H, int W, int Ci, int hc) {
+  const int hy = ch_div18(p), hx = p - hy * CH_W;
+  const int ih = min(max(oh0 - 1 + hy, 0), H - 1), iw = min(max(ow0 - 1 + hx, 0), W - 1);
+  return (__umul24(__umul24((unsigned)ih, (unsigned)W) + (unsigned)iw, (unsigned)Ci) + (unsigned)hc * 8u) * 2u;
+}
+// GroupNorm-apply (+ SiLU) of one staged 16-B chunk, zeroed for a pixel outside the image (F.conv2d
+// pads the ACTIVATED tensor): packed-f32 math, the select on the four packed words
+template <bool SILU>
+__device__ __forceinline__ bf16x8 ch_gn_act(bf16x8 v, const float (&gsc)[8], const float (&gsh)[8], bool inb) {
+  bf16x8 o;
+#pragma unroll
+  for (int j = 0; j < 8; j += 2) {
+    const f32x2 x = {(float)v[j], (float)v[j + 1]};
+    f32x2 u = x * (f32x2){gsc[j], gsc[j + 1]} + (f32x2){gsh[j], gsh[j + 1]};
+    if constexpr (SILU) {
+      const f32x2 t = u * (f32x2){-1.4426950408889634f, -1.4426950408889634f};
+      const f32x2 d = (f32x2){__builtin_amdgcn_exp2f(t.x), __builtin_amdgcn_exp2f(t.y)} + (f32x2){1.f, 1.f};
+      u = u * (f32x2){__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y)};
+    }
+    o[j] = (bf16)u.x;
+    o[j + 1] = (bf16)u.y;
+  }
+  ch_u32x4 w = __builtin_bit_cast(ch_u32x4, o);
+#pragma unroll
+  for (int k = 0; k < 4; ++k) w[k] = inb ? w[k] : 0u;
+  return __builtin_bit_cast(bf16x8, w);
+}
+
 // s_waitcnt vmcnt(n) for the few counts the 3-slot ring can need (the immediate is compile-time);
 // an unlisted count falls back to vmcnt(0) (over-waiting is always safe)
 template <int NI, int NR, int NP>
@@ -135,7 +177,7 @@ __device__ __forceinline__ void conv_vm_wait(int n) {
 #ifndef UVA_CONV_ILV_RATIO
 #define UVA_CONV_ILV_RATIO 2   // ILV: staging VALU instructions placed after each MFMA
 #endif
-template <int BN, bool GN, int VAR, int TR>
+template <int BN, bool GN, int VAR, int TR, bool SILU = true>
 __global__ __launch_bounds__(TR * 32, 16 / TR) void conv3x3_halo(const bf16* __restrict__ in, const bf16* __restrict__ wt,
                                                        bf16* __restrict__ out, const float* __restrict__ bias,
                                                        const bf16* __restrict__ residual,
@@ -200,13 +242,13 @@ __global__ __launch_bounds__(TR * 32, 16 / TR) void conv3x3_halo(const bf16* __r
   const int hc = tid & 7;
   bf16x8 hreg[G::ROUNDS];
   float gsc[8], gsh[8];
+  const __amdgpu_buffer_rsrc_t rs_in = ch_img_rsrc(in, n, H * W * Ci);
   auto halo_load = [&](int cc) {
 #pragma unroll
     for (int i = 0; i < G::ROUNDS; ++i) {
-      const int p = min((tid + i * G::NTH) >> 3, G::HPIX - 1);
-      const int hy = p / CH_W, hx = p - hy * CH_W;
-      const int ih = min(max(oh0 - 1 + hy, 0), H - 1), iw = min(max(ow0 - 1 + hx, 0), W - 1);  // clamped: always in bounds
-      hreg[i] = *(const bf16x8*)(in + (((long long)n * H + ih) * W + iw) * Ci + cc * 64 + hc * 8);
+      const int p = min((tid + i * G::NTH) >> 3, G::HPIX - 1);  // clamped pixel: always in bounds
+      hreg[i] = __builtin_bit_cast(
+          bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rs_in, ch_halo_off(p, oh0, ow0, H, W, Ci, hc), cc * 128, 0));
     }
     if constexpr (GN) {
       const float* sc = gn_scale + (long long)n * Ci + cc * 64 + hc * 8;
@@ -233,7 +275,7 @@ __global__ __launch_bounds__(TR * 32, 16 / TR) void conv3x3_halo(const bf16* __r
           for (int j = 0; j < 8; j += 2) {
             const f32x2 x = {(float)v[j], (float)v[j + 1]};
             f32x2 u = x * (f32x2){gsc[j], gsc[j + 1]} + (f32x2){gsh[j], gsh[j + 1]};
-            if (gn_silu) {
+            if constexpr (SILU) {
               const f32x2 t = u * (f32x2){-1.4426950408889634f, -1.4426950408889634f};
               const f32x2 d = (f32x2){__builtin_amdgcn_exp2f(t.x), __builtin_amdgcn_exp2f(t.y)} + (f32x2){1.f, 1.f};
               u = u * (f32x2){__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y)};
@@ -252,27 +294,15 @@ __global__ __launch_bounds__(TR * 32, 16 / TR) void conv3x3_halo(const bf16* __r
     for (int i = 0; i < G::ROUNDS; ++i) halo_store_round(hb, i);
   };
   // ILV: the same round without branches (one basic block with the MFMAs it is interleaved with):
-  // out-of-image pixels by select, the pixel index clamped (a clamped thread rewrites pixel HPIX-1
-  // with the value its owner stores), SiLU by a uniform select
+  // out-of-image pixels by select on the packed words, the pixel index clamped (a clamped thread
+  // rewrites pixel HPIX-1 with the value its owner stores)
   auto halo_store_round_bf = [&](int hb, int i) __attribute__((always_inline)) {
     bf16* img = halo + hb * G::HALO_ELEMS;
     const int p = min((tid + i * G::NTH) >> 3, G::HPIX - 1);
-    const int hy = p / CH_W, hx = p - hy * CH_W;
+    const int hy = ch_div18(p), hx = p - hy * CH_W;
     const int ih = oh0 - 1 + hy, iw = ow0 - 1 + hx;
-    const bool inb = ih >= 0 && ih < H && iw >= 0 && iw < W;
-    bf16x8 v = hreg[i];
-#pragma unroll
-    for (int j = 0; j < 8; j += 2) {
-      const f32x2 x = {(float)v[j], (float)v[j + 1]};
-      const f32x2 u = x * (f32x2){gsc[j], gsc[j + 1]} + (f32x2){gsh[j], gsh[j + 1]};
-      const f32x2 t = u * (f32x2){-1.4426950408889634f, -1.4426950408889634f};
-      const f32x2 d = (f32x2){__builtin_amdgcn_exp2f(t.x), __builtin_amdgcn_exp2f(t.y)} + (f32x2){1.f, 1.f};
-      const f32x2 us = u * (f32x2){__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y)};
-      const float a = gn_silu ? us.x : u.x, b = gn_silu ? us.y : u.y;
-      v[j] = inb ? (bf16)a : (bf16)0.f;
-      v[j + 1] = inb ? (bf16)b : (bf16)0.f;
-    }
-    *(bf16x8*)(img + p * G::PP + hc * 8) = v;
+    const bool inb = (unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)W;
+    *(bf16x8*)(img + p * G::PP + hc * 8) = ch_gn_act<SILU>(hreg[i], gsc, gsh, inb);
   };
 
   // ---- HD: halo by LDS-DMA through a per-image buffer descriptor. LDS pixel block b (8 pixels)
@@ -280,10 +310,7 @@ __global__ __launch_bounds__(TR * 32, 16 / TR) void conv3x3_halo(const bf16* __r
   //      (l%8) ^ (p & 7) (the swizzle goes on the source). Pixels outside the image (and the
   //      padding past HPIX) get an offset beyond the descriptor's range: the DMA writes zeros.
   unsigned hoff[HD ? G::HD_I : 1];
-  __amdgpu_buffer_rsrc_t rs_in;
   if constexpr (HD) {
-    const int img_bytes = __builtin_amdgcn_readfirstlane(H * W * Ci * 2);
-    rs_in = __builtin_amdgcn_make_buffer_rsrc((void*)(in + (long long)n * H * W * Ci), 0, img_bytes, 0x00020000);
 #pragma unroll
     for (int i = 0; i < G::HD_I; ++i) {
       const int p = (wid * G::HD_I + i) * 8 + (lane >> 3);
@@ -381,8 +408,17 @@ __global__ __launch_bounds__(TR * 32, 16 / TR) void conv3x3_halo(const bf16* __r
     // (rows >= RQ_PRE at the epilogue's start: all 8 rows up front spilled)
     constexpr int RQ_PRE = G::ROUNDS < G::FM ? G::ROUNDS : G::FM;
     static_assert(G::FN == 2, "the permlane16 pairing joins the wave's two 16-channel fragments");
-    const long long pix0 = ((long long)n * H + oh0) * W + ow0 + frow;  // pixel (row 0, column frow)
     const int c0 = n0 + wn * (G::FN * 16) + fk * 4;
+    // residual loads / output stores through per-image descriptors: 32-bit lane offset of (row 0, column
+    // frow, the lane's 8-channel run), the row in soffset
+    const int cs_ = n0 + wn * (G::FN * 16) + (fk & 1) * 16 + (fk >> 1) * 8;
+    const unsigned pbase = (unsigned)(((oh0 * W + ow0 + frow) * Co + cs_) * 2);
+    const __amdgpu_buffer_rsrc_t rs_res = ch_img_rsrc(residual, n, H * W * Co);
+    const __amdgpu_buffer_rsrc_t rs_out = ch_img_rsrc(out, n, H * W * Co);
+    auto res_row = [&](int f) __attribute__((always_inline)) {
+      return __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(
+                                            rs_res, pbase, __builtin_amdgcn_readfirstlane(f * W * Co * 2), 0));
+    };
     auto chunk_ilv = [&](int cc, auto stc) __attribute__((always_inline)) {
       constexpr bool STG = decltype(stc)::value;  // a next chunk exists: stage it under these taps
       const bf16* hcur = halo + (cc & 1) * G::HALO_ELEMS + abase;
@@ -397,14 +433,13 @@ __global__ __launch_bounds__(TR * 32, 16 / TR) void conv3x3_halo(const bf16* __r
           if (tap == 0) halo_load(cc + 1);
         } else {
           if (tap == 0 && residual) {
-            const int csr = n0 + wn * (G::FN * 16) + (fk & 1) * 16 + (fk >> 1) * 8;
 #pragma unroll
-            for (int f = 0; f < RQ_PRE; ++f) hreg[f] = *(const bf16x8*)(residual + (pix0 + (long long)f * W) * Co + csr);
+            for (int f = 0; f < RQ_PRE; ++f) hreg[f] = res_row(f);
             if constexpr ((VAR & 256) != 0) {
               // rows RQ_PRE.. into the GroupNorm scale registers (no staging in the last chunk)
 #pragma unroll
               for (int f = RQ_PRE; f < G::FM; ++f) {
-                const f32x4 v = __builtin_bit_cast(f32x4, *(const bf16x8*)(residual + (pix0 + (long long)f * W) * Co + csr));
+                const f32x4 v = __builtin_bit_cast(f32x4, res_row(f));
 #pragma unroll
                 for (int j = 0; j < 4; ++j) gsc[(f - RQ_PRE) * 4 + j] = v[j];
               }
@@ -472,9 +507,8 @@ __global__ __launch_bounds__(TR * 32, 16 / TR) void conv3x3_halo(const bf16* __r
         if (tap == 0 && more) halo_load(cc + 1);
         if (tap == 0 && !more && residual) {
           // rows 0..RQ_PRE-1 into the (now free) halo staging registers (the epilogue's 16-B runs)
-          const int csr = n0 + wn * (G::FN * 16) + (fk & 1) * 16 + (fk >> 1) * 8;
 #pragma unroll
-          for (int f = 0; f < RQ_PRE; ++f) hreg[f] = *(const bf16x8*)(residual + (pix0 + (long long)f * W) * Co + csr);
+          for (int f = 0; f < RQ_PRE; ++f) hreg[f] = res_row(f);
           if constexpr ((VAR & 256) != 0) {
             // the remaining rows too, into the GroupNorm scale registers (dead in the last chunk; the
             // same variables, so the allocator needs no new ones): no residual load is left for the
@@ -482,7 +516,7 @@ __global__ __launch_bounds__(TR * 32, 16 / TR) void conv3x3_halo(const bf16* __r
             static_assert(G::FM - RQ_PRE <= 2, "two late rows fit gsc");
 #pragma unroll
             for (int f = RQ_PRE; f < G::FM; ++f) {
-              const f32x4 v = __builtin_bit_cast(f32x4, *(const bf16x8*)(residual + (pix0 + (long long)f * W) * Co + csr));
+              const f32x4 v = __builtin_bit_cast(f32x4, res_row(f));
 #pragma unroll
               for (int j = 0; j < 4; ++j) gsc[(f - RQ_PRE) * 4 + j] = v[j];
             }
@@ -552,7 +586,7 @@ __global__ __launch_bounds__(TR * 32, 16 / TR) void conv3x3_halo(const bf16* __r
           const int o = ((f - RQ_PRE) & 1) * 4;
           rq[f] = __builtin_bit_cast(bf16x8, (f32x4){gsc[o], gsc[o + 1], gsc[o + 2], gsc[o + 3]});
         } else {
-          rq[f] = *(const bf16x8*)(residual + (pix0 + (long long)f * W) * Co + cs);
+          rq[f] = res_row(f);
         }
     }
     float sa = 0.f, sb = 0.f, qa = 0.f, qb = 0.f;
@@ -573,7 +607,8 @@ __global__ __launch_bounds__(TR * 32, 16 / TR) void conv3x3_halo(const bf16* __r
       bf16x8 o;
 #pragma unroll
       for (int e = 0; e < 8; ++e) o[e] = (bf16)v[e];
-      *(bf16x8*)(out + (pix0 + (long long)f * W) * Co + cs) = o;
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(ch_u32x4, o), rs_out, pbase,
+                                             __builtin_amdgcn_readfirstlane(f * W * Co * 2), 0);
       if (gn_part) {
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
@@ -1119,6 +1154,7 @@ __global__ __launch_bounds__(256, 2) void conv3x3_gn_strip(const bf16* __restric
 // registers as they free up (row r at tap 3 + r; rows 6, 7 in the GroupNorm scale registers at tap
 // 8).  After the grid's last tile the current tile is restaged (harmless: nothing reads it).
 // =====================================================================================
+template <bool SILU>
 __global__ __launch_bounds__(256, 2) void conv3x3_gn_pt(const bf16* __restrict__ in, const bf16* __restrict__ wt,
                                                         bf16* __restrict__ out, const float* __restrict__ bias,
                                                         const bf16* __restrict__ residual,
@@ -1156,12 +1192,12 @@ __global__ __launch_bounds__(256, 2) void conv3x3_gn_pt(const bf16* __restrict__
   float gsc[8], gsh[8];
   auto halo_load = [&](const Tile& t, int cc) __attribute__((always_inline)) {
     const int tid = opaque(threadIdx.x), hc = tid & 7;
+    const __amdgpu_buffer_rsrc_t rs_in = ch_img_rsrc(in, t.n, H * W * Ci);
 #pragma unroll
     for (int i = 0; i < G::ROUNDS; ++i) {
       const int p = min((tid + i * G::NTH) >> 3, G::HPIX - 1);
-      const int hy = p / CH_W, hx = p - hy * CH_W;
-      const int ih = min(max(t.oh0 - 1 + hy, 0), H - 1), iw = min(max(t.ow0 - 1 + hx, 0), W - 1);
-      hreg[i] = *(const bf16x8*)(in + (((long long)t.n * H + ih) * W + iw) * Ci + cc * 64 + hc * 8);
+      hreg[i] = __builtin_bit_cast(
+          bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rs_in, ch_halo_off(p, t.oh0, t.ow0, H, W, Ci, hc), cc * 128, 0));
     }
     const float* sc = gn_scale + (long long)t.n * Ci + cc * 64 + hc * 8;
     const float* sh = gn_shift + (long long)t.n * Ci + cc * 64 + hc * 8;
@@ -1175,22 +1211,10 @@ __global__ __launch_bounds__(256, 2) void conv3x3_gn_pt(const bf16* __restrict__
     const int tid = opaque(threadIdx.x), hc = tid & 7;
     bf16* img = halo + hb * G::HALO_ELEMS;
     const int p = min((tid + i * G::NTH) >> 3, G::HPIX - 1);
-    const int hy = p / CH_W, hx = p - hy * CH_W;
+    const int hy = ch_div18(p), hx = p - hy * CH_W;
     const int ih = t.oh0 - 1 + hy, iw = t.ow0 - 1 + hx;
-    const bool inb = ih >= 0 && ih < H && iw >= 0 && iw < W;
-    bf16x8 v = hreg[i];
-#pragma unroll
-    for (int j = 0; j < 8; j += 2) {
-      const f32x2 x = {(float)v[j], (float)v[j + 1]};
-      const f32x2 u = x * (f32x2){gsc[j], gsc[j + 1]} + (f32x2){gsh[j], gsh[j + 1]};
-      const f32x2 tt = u * (f32x2){-1.4426950408889634f, -1.4426950408889634f};
-      const f32x2 d = (f32x2){__builtin_amdgcn_exp2f(tt.x), __builtin_amdgcn_exp2f(tt.y)} + (f32x2){1.f, 1.f};
-      const f32x2 us = u * (f32x2){__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y)};
-      const float a = gn_silu ? us.x : u.x, b = gn_silu ? us.y : u.y;
-      v[j] = inb ? (bf16)a : (bf16)0.f;
-      v[j + 1] = inb ? (bf16)b : (bf16)0.f;
-    }
-    *(bf16x8*)(img + p * G::PP + hc * 8) = v;
+    const bool inb = (unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)W;
+    *(bf16x8*)(img + p * G::PP + hc * 8) = ch_gn_act<SILU>(hreg[i], gsc, gsh, inb);
   };
   const __amdgpu_buffer_rsrc_t rs_w =
       __builtin_amdgcn_make_buffer_rsrc((void*)wt, 0, __builtin_amdgcn_readfirstlane(Co * K * 2), 0x00020000);
@@ -1305,6 +1329,8 @@ __global__ __launch_bounds__(256, 2) void conv3x3_gn_pt(const bf16* __restrict__
     chunk(std::integral_constant<int, 1>{});
 
     // ---- register epilogue (as conv3x3_halo's register-B form, Co = 128: two groups per lane)
+    const __amdgpu_buffer_rsrc_t rs_out = ch_img_rsrc(out, cur.n, H * W * Co);
+    const unsigned obase = (unsigned)(((cur.oh0 * W + cur.ow0 + frow) * Co + cs) * 2);
     float sa = 0.f, sb = 0.f, qa = 0.f, qb = 0.f;
 #pragma unroll
     for (int f = 0; f < G::FM; ++f) {
@@ -1326,7 +1352,10 @@ __global__ __launch_bounds__(256, 2) void conv3x3_gn_pt(const bf16* __restrict__
       bf16x8 o;
 #pragma unroll
       for (int e = 0; e < 8; ++e) o[e] = (bf16)v[e];
-      *(bf16x8*)(out + (pix0 + (long long)f * W) * Co + cs) = o;
+      // per-image descriptor, 32-bit lane offset, the row in soffset (no 64-bit address registers
+      // live across the tile loop: they spilled)
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(ch_u32x4, o), rs_out, obase,
+                                             __builtin_amdgcn_readfirstlane(f * W * Co * 2), 0);
       if (gn_part) {
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
@@ -1597,17 +1626,17 @@ extern "C" int uva_conv3x3_halo(const void* in, const void* w, void* out, const 
   constexpr int tr = 8;
   const long long nblk = (long long)Nimg * (H / tr) * (W / CH_T) * (Co / bn);
   if (nblk >= (1ll << 31)) return (int)hipErrorInvalidValue;
-#define CH_LAUNCH(BNV, GNV, VARV, TRV)                                                                         \
+#define CH_LAUNCH(BNV, GNV, VARV, TRV, SILUV)                                                                  \
   do {                                                                                                         \
     static bool attr = false;                                                                                  \
     const int lb = ConvHCfg<BNV, TRV, ((VARV) & 2) != 0, ((VARV) & 8) != 0 && !(GNV) && !((VARV) & 2),          \
                             ((VARV) & 64) != 0 && (GNV) && !((VARV) & 2) && !((VARV) & 16)>::LDS_BYTES;          \
     if (!attr) {                                                                                               \
-      (void)hipFuncSetAttribute((const void*)conv3x3_halo<BNV, GNV, VARV, TRV>,                               \
+      (void)hipFuncSetAttribute((const void*)conv3x3_halo<BNV, GNV, VARV, TRV, SILUV>,                        \
                                 hipFuncAttributeMaxDynamicSharedMemorySize, lb);                               \
       attr = true;                                                                                             \
     }                                                                                                          \
-    conv3x3_halo<BNV, GNV, VARV, TRV><<<dim3((unsigned)nblk), TRV * 32, lb, stream>>>(                         \
+    conv3x3_halo<BNV, GNV, VARV, TRV, SILUV><<<dim3((unsigned)nblk), TRV * 32, lb, stream>>>(                  \
         (const bf16*)in, (const bf16*)w, (bf16*)out, bias, (const bf16*)residual, gn_scale, gn_shift, gn_silu, \
         gn_part, Nimg, H, W, Ci, Co);                                                                          \
   } while (0)
@@ -1632,16 +1661,24 @@ extern "C" int uva_conv3x3_halo(const void* in, const void* w, void* out, const 
     static bool attr_p = false;
     static int cus = 0;
     if (!attr_p) {
-      (void)hipFuncSetAttribute((const void*)conv3x3_gn_pt, hipFuncAttributeMaxDynamicSharedMemorySize, GS::LDS_BYTES);
+      (void)hipFuncSetAttribute((const void*)conv3x3_gn_pt<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                GS::LDS_BYTES);
+      (void)hipFuncSetAttribute((const void*)conv3x3_gn_pt<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                GS::LDS_BYTES);
       int dev = 0;
       (void)hipGetDevice(&dev);
       if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
       attr_p = true;
     }
     const long long grid = std::min<long long>(nblk, 2LL * cus);
-    conv3x3_gn_pt<<<dim3((unsigned)grid), 256, GS::LDS_BYTES, stream>>>(
-        (const bf16*)in, (const bf16*)w, (bf16*)out, bias, (const bf16*)residual, gn_scale, gn_shift, gn_silu, gn_part,
-        Nimg, H, W);
+    if (gn_silu)
+      conv3x3_gn_pt<true><<<dim3((unsigned)grid), 256, GS::LDS_BYTES, stream>>>(
+          (const bf16*)in, (const bf16*)w, (bf16*)out, bias, (const bf16*)residual, gn_scale, gn_shift, gn_silu,
+          gn_part, Nimg, H, W);
+    else
+      conv3x3_gn_pt<false><<<dim3((unsigned)grid), 256, GS::LDS_BYTES, stream>>>(
+          (const bf16*)in, (const bf16*)w, (bf16*)out, bias, (const bf16*)residual, gn_scale, gn_shift, gn_silu,
+          gn_part, Nimg, H, W);
     UVA_LAUNCH_CHECK();
     return 0;
   }
@@ -1660,8 +1697,9 @@ extern "C" int uva_conv3x3_halo(const void* in, const void* w, void* out, const 
     UVA_LAUNCH_CHECK();
     return 0;
   }
-  if (gn_scale) CH_LAUNCH(128, true, UVA_CONV_GN_VAR, 8);
-  else CH_LAUNCH(128, false, 12, 8);
+  if (gn_scale && gn_silu) CH_LAUNCH(128, true, UVA_CONV_GN_VAR, 8, true);
+  else if (gn_scale) CH_LAUNCH(128, true, UVA_CONV_GN_VAR, 8, false);
+  else CH_LAUNCH(128, false, 12, 8, true);
 #undef CH_LAUNCH
   UVA_LAUNCH_CHECK();
   return 0;
