@@ -1249,7 +1249,14 @@ __global__ __launch_bounds__(256, 2) void conv3x3_gn_pt(const bf16* __restrict__
     const int npid = pid + G_;
     const bool more = npid < ntiles;
     const Tile nxt = tile_of(more ? npid : pid);
-    const long long pix0 = ((long long)cur.n * H + cur.oh0) * W + cur.ow0 + frow;
+    // residual loads / output stores through per-image descriptors: 32-bit lane offset of (row 0,
+    // column frow, the lane's 8-channel run), the row in soffset
+    const unsigned obase = (unsigned)(((cur.oh0 * W + cur.ow0 + frow) * Co + cs) * 2);
+    const __amdgpu_buffer_rsrc_t rs_res = ch_img_rsrc(residual, cur.n, H * W * Co);
+    auto res_row = [&](int f) __attribute__((always_inline)) {
+      return __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(
+                                            rs_res, obase, __builtin_amdgcn_readfirstlane(f * W * Co * 2), 0));
+    };
     f32x4 acc[G::FM][G::FN];
 #pragma unroll
     for (int j = 0; j < G::FN; ++j) {
@@ -1278,12 +1285,11 @@ __global__ __launch_bounds__(256, 2) void conv3x3_gn_pt(const bf16* __restrict__
           if (tap == 0) halo_load(cur, 1);
           if (tap == 8) halo_load(nxt, 0);
         } else {
-          if (tap >= 2 && tap < 8 && residual)
-            hreg[tap - 2] = *(const bf16x8*)(residual + (pix0 + (long long)(tap - 2) * W) * Co + opaque(cs));
+          if (tap >= 2 && tap < 8 && residual) hreg[tap - 2] = res_row(tap - 2);
           if (tap == 7 && residual) {
 #pragma unroll
             for (int f = 6; f < 8; ++f) {
-              const f32x4 v = __builtin_bit_cast(f32x4, *(const bf16x8*)(residual + (pix0 + (long long)f * W) * Co + cs));
+              const f32x4 v = __builtin_bit_cast(f32x4, res_row(f));
 #pragma unroll
               for (int j = 0; j < 4; ++j) gsc[(f - 6) * 4 + j] = v[j];
             }
@@ -1330,7 +1336,6 @@ __global__ __launch_bounds__(256, 2) void conv3x3_gn_pt(const bf16* __restrict__
 
     // ---- register epilogue (as conv3x3_halo's register-B form, Co = 128: two groups per lane)
     const __amdgpu_buffer_rsrc_t rs_out = ch_img_rsrc(out, cur.n, H * W * Co);
-    const unsigned obase = (unsigned)(((cur.oh0 * W + cur.ow0 + frow) * Co + cs) * 2);
     float sa = 0.f, sb = 0.f, qa = 0.f, qb = 0.f;
 #pragma unroll
     for (int f = 0; f < G::FM; ++f) {
@@ -1653,7 +1658,10 @@ extern "C" int uva_conv3x3_halo(const void* in, const void* w, void* out, const 
 #ifndef UVA_CONV_GN_PT
 #define UVA_CONV_GN_PT 1
 #endif
-  if (gn_scale && Ci == 128 && Co == 128 && residual == nullptr && (UVA_CONV_GN_PT)) {
+#ifndef UVA_CONV_GN_PT_RES
+#define UVA_CONV_GN_PT_RES 0
+#endif
+  if (gn_scale && Ci == 128 && Co == 128 && (residual == nullptr || (UVA_CONV_GN_PT_RES)) && (UVA_CONV_GN_PT)) {
     // persistent form (above): two workgroups per CU.  Without a residual only: with one, its late
     // rows cost what the next tile's early halo saves (level 0 6.61 vs 6.64 ms; without: 6.25 ->
     // 6.15-6.19 ms, level 1 1.575 -> 1.55 ms; profiles/r04/ab_gnconv_persistent.txt)
