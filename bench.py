@@ -78,7 +78,7 @@ def parse(argv=None):
     ap.add_argument("--no-cpu-batch-gpu", action="store_true",
                     help="skip the CPU baseline step at the config's per-GPU batch")
     ap.add_argument("--trace-out", default="", help="write every traced kernel row (tag, launches, avg ms) here")
-    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r04_end.json"))
+    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r05_end.json"))
     return ap.parse_args(argv)
 
 
