@@ -104,8 +104,10 @@ int uva_conv2d(int dtype, const void* in, const void* w, void* out, const float*
  *      of ReLU -> mean-pool; post = the forward's post-ReLU conv output, gpool any of bf16 / fp32).
  * uva_im2col3x3: cols[n H W][9 Ci] with column ci*9 + kh*3 + kw (nn.Conv2d weight order), zero pad 1.
  * uva_im2col3x3_tc: the same columns in tap-major order, tap*Ci + ci (16-B vector moves; Ci % 8 for
- *      bf16, % 4 for fp32; 16-B aligned); the dW product over them is [Co][9][Ci], added into the
- *      nn.Conv2d-layout fp32 gradient [Co][Ci][3][3] by uva_conv3x3_dw_scatter_add.
+ *      bf16, % 4 for fp32; 16-B aligned).  Both im2col forms stay exported for hosts that want the
+ *      materialised columns; the training step's trunk dW uses uva_pad_nhwc below (no 9x tensor).
+ *      The tap-major dW partial [Co][9][Ci] is added into the nn.Conv2d-layout fp32 gradient
+ *      [Co][Ci][3][3] by uva_conv3x3_dw_scatter_add.
  * uva_conv3x3_weight_layout: fp32 [Co][Ci][3][3] -> mode 0 [Co][3][3][Ci] (forward conv operand),
  *      mode 1 [Ci][3][3][Co] flipped (the dX conv), out_dtype bf16 / fp32. */
 int uva_pool4x4_cwh(int dtype, const void* in, void* out, int n, int C, hipStream_t stream);
