@@ -8,4 +8,4 @@ tail -1 $O/t.log
 timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || { echo SMOKE_FAIL; tail -5 $O/smoke.log; exit 1; }
 tail -2 $O/smoke.log
 timeout -k 10 600 python -u bench.py --steps 20 --warmup 5 --other-configs "${2-}" --no-cpu-baseline --h2d-steps 0 > $O/bench.json 2> $O/bench.err || { echo BENCH_FAIL; tail -5 $O/bench.err; exit 1; }
-python3 -c "import json; d=json.load(open('$O/bench.json')); print('bench', d['value'], d['ms_per_step'], d.get('roofline',{}).get('frac')); [print(k, v.get('value') if isinstance(v, dict) else v) for k, v in d.get('other_configs', {}).items()]"
+python3 -c "import json; d=json.load(open('$O/bench.json')); print('bench', d['value'], d['ms_per_step'], d.get('roofline',{}).get('frac')); [print(v['config'], v['global_batch'], v['value'], v.get('precision')) for v in d.get('other_configs', [])]"
