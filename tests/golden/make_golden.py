@@ -253,6 +253,36 @@ def gen_mlp():
     print("mlp done")
 
 
+ACT_TRUNKS = ("conv_ori", "conv2", "fc2")
+
+
+def gen_act_trunks():
+    """g3_act_trunks.npz: the reference DiffActLoss with each off-config action trunk (act_model_type
+    conv_ori / conv2 / fc2, diffusion_action_loss.py:63-89, 125-141) on hash weights, z [2, 1024, 64],
+    target [2, 16, 2], injected t / noise: loss, dL/dz rows and every parameter gradient."""
+    from unified_video_action.model.autoregressive.diffusion_action_loss import DiffActLoss
+    d = {}
+    for kind in ACT_TRUNKS:
+        m = DiffActLoss(2, 64, 2, 64, "100", n_frames=4, act_model_type=kind, language_emb_model=None,
+                        language_emb_model_type=1)
+        hash_init_(m, f"act_{kind}.")
+        m.train()
+        z = torch.from_numpy(hash_normal(f"act_{kind}/z", (2, 1024, 64))).requires_grad_(True)
+        target = torch.from_numpy(hash_normal(f"act_{kind}/target", (2, 16, 2)))
+        rng = {"randint": [cases.t_steps(f"act_{kind}", 32)],
+               "randn_like": [hash_normal(f"act_{kind}/noise", (32, 2))]}
+        with injected(rng):
+            loss = m(target, z)
+        loss.backward()
+        names, sums, heads = grad_table(m)
+        d[f"{kind}_loss"] = np.array([loss.item()], np.float64)
+        d[f"{kind}_gz_rows"] = z.grad[:, ::64].detach().numpy()
+        d[f"{kind}_gz_sum"] = checksum(z.grad)
+        d[f"{kind}_gnames"], d[f"{kind}_gsums"], d[f"{kind}_gheads"] = names, sums, heads
+        print(f"act trunk {kind}: loss={loss.item():.6f} ngrads={len(names)}")
+    np.savez(os.path.join(OUT, "g3_act_trunks.npz"), **d)
+
+
 def gen_diffusion_math():
     d = {}
     for tag, C in (("video", 16), ("act", 2), ("act10", 10)):

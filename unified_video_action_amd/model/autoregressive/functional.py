@@ -92,12 +92,15 @@ def _seed():
 
 # --------------------------------------------------------------------------------------
 class LinearFn(torch.autograd.Function):
-    """out = residual + drop(act(x @ W^T + b))  (nn.Linear + fused epilogue)."""
+    """out = residual + drop(act(x @ W^T + b))  (nn.Linear + fused epilogue).  A weight with more than two
+    dims (a Conv1d [out, in, k] over im2col columns) is the [out, in*k] matrix of its contiguous layout."""
 
     @staticmethod
     def forward(ctx, x, weight, bias, act, drop_p, out_dtype, residual):
         xc = as_dtype(x, cdt())
         w = compute_weight(weight)
+        if w.dim() != 2:
+            w = w.reshape(w.shape[0], -1)
         M, N = xc.shape[0], weight.shape[0]
         out = torch.empty(M, N, dtype=out_dtype, device=x.device)
         aux = torch.empty(M, N, dtype=out_dtype, device=x.device) if act != "none" else None
@@ -125,10 +128,10 @@ class LinearFn(torch.autograd.Function):
             dpre = as_dtype(g, cdt())
         gx = None
         if ctx.needs_input_grad[0]:
-            gx = torch.empty(M, weight.shape[1], dtype=F32, device=g.device)
-            ops.linear_dx(dpre, compute_weight(weight), gx)
+            gx = torch.empty(M, xc.shape[1], dtype=F32, device=g.device)
+            ops.linear_dx(dpre, compute_weight(weight).reshape(N, -1), gx)
             gx = as_dtype(gx, xdt)
-        ops.linear_dw(dpre, xc, grad_buf(weight))
+        ops.linear_dw(dpre, xc, grad_buf(weight).view(N, -1))
         if bias is not None and not fused_bias:
             ops.colsum(dpre, grad_buf(bias), accum=True)
         return gx, None, None, None, None, None, (g if has_res else None)
