@@ -100,7 +100,13 @@ def injected(rng):
         assert tuple(shp) == tuple(v.shape), (shp, v.shape)
         return v
 
+    q_rand = [torch.from_numpy(rng["hist_u"])] if "hist_u" in rng else []
+
     def fake_rand(*shape, **k):
+        if q_rand:  # the history-action drop draws first (:512-518), then the label drop
+            v = q_rand.pop(0)
+            assert tuple(shape) == tuple(v.shape), (shape, v.shape)
+            return v
         return torch.from_numpy(rng["text_drop_u"])
 
     torch.randint, torch.randn_like, torch.randn, torch.rand = (
@@ -113,7 +119,7 @@ def injected(rng):
     finally:
         (torch.randint, torch.randn_like, torch.randn, torch.rand, random.choice,
          ref_mar.MAR.sample_orders) = saved
-    assert not q_int and not q_nrm and not q_eps, "unconsumed injected draws"
+    assert not q_int and not q_nrm and not q_eps and not q_rand, "unconsumed injected draws"
 
 
 def build_mar(variant):
@@ -125,17 +131,22 @@ def build_mar(variant):
 
 
 def mar_call(m, variant, mode, inp):
-    v = cases.VARIANTS[variant]
+    v = cases.variant_def(variant)
     t = {k: torch.from_numpy(x) for k, x in inp.items()}
     prop = {}
     if v["use_proprioception"]:
         prop = {k: t[k] for k in t if k.startswith("robot0_")}
-    return m(t["z"], t["c"], None, t["nactions"], t.get("text_latents"), task_mode=mode,
+    return m(t["z"], t["c"], t.get("history_nactions"), t["nactions"], t.get("text_latents"), task_mode=mode,
              proprioception_input=prop)
 
 
-def gen_mar():
-    for variant, v in cases.VARIANTS.items():
+def gen_mar_extra():
+    """g2_mar_<extra variant>_<mode>.npz for cases.EXTRA_VARIANTS (variants no shipped config selects)."""
+    gen_mar(cases.EXTRA_VARIANTS)
+
+
+def gen_mar(variants=None):
+    for variant, v in (variants or cases.VARIANTS).items():
         inp = cases.mar_inputs(variant)
         for mode in v["modes"]:
             m = build_mar(variant)

@@ -21,7 +21,7 @@ def checksum(t):
 
 
 def mar_ctor_kwargs(variant):
-    v = cases.VARIANTS[variant]
+    v = cases.variant_def(variant)
     m = cases.MAR_GOLDEN
     return dict(
         encoder_embed_dim=m["encoder_embed_dim"], encoder_depth=m["encoder_depth"],

@@ -78,8 +78,8 @@ class MAR(nn.Module):
         self.use_proprioception = kwargs.get("use_proprioception") or False
         self.predict_wrist_img = kwargs.get("predict_wrist_img") or False
         self.predict_proprioception = kwargs.get("predict_proprioception") or False
-        if self.use_history_action or self.predict_wrist_img:
-            raise NotImplementedError("history-action / wrist-image variants are outside the accelerated path")
+        if self.predict_wrist_img:
+            raise NotImplementedError("the wrist-image variant is outside the accelerated path")
         self.n_frames = 4
         self.seq_h = self.seq_w = img_size // vae_stride // patch_size
         self.seq_len = self.seq_h * self.seq_w
@@ -98,6 +98,11 @@ class MAR(nn.Module):
         self.fake_latent_x = nn.Parameter(torch.zeros(1, D))
         self.fake_action_latent = nn.Parameter(torch.zeros(1, D))
         n_streams = 3
+        if self.use_history_action:  # (:115-124, 504-522): one more conditioning stream
+            self.action_mask_ratio = kwargs["action_mask_ratio"]
+            self.fake_latent_history_action = nn.Parameter(torch.zeros(1, D))
+            self.history_action_proj_cond = nn.Linear(act_dim, D)
+            n_streams += 1
         if self.use_proprioception:
             if self.task_name != "umi":
                 raise NotImplementedError("proprioception is accelerated for the UMI path only")
@@ -155,6 +160,8 @@ class MAR(nn.Module):
         if self.clip:
             for p in (self.fake_latent, self.text_pos_embed, self.decoder_text_pos_embed):
                 nn.init.normal_(p, std=0.02)
+        if self.use_history_action:
+            nn.init.normal_(self.fake_latent_history_action, std=0.02)
         for m in self.modules():
             if isinstance(m, nn.Linear):
                 nn.init.xavier_uniform_(m.weight)
@@ -194,7 +201,8 @@ class MAR(nn.Module):
         return (temporal[:, :, None, :] + spatial[:, None, :, :]).reshape(1, -1, temporal.shape[-1])
 
     # ---- encoder (:445-659) -------------------------------------------------------------
-    def forward_mae_encoder(self, x, mask, cond, text_latents, nactions, task_mode, prop, text_drop_u):
+    def forward_mae_encoder(self, x, mask, cond, text_latents, nactions, task_mode, prop, text_drop_u,
+                            history_nactions=None, hist_u=None):
         B, T, S, _ = x.shape
         D = self.fake_latent_x.shape[1]
         c = cdt()
@@ -213,7 +221,21 @@ class MAR(nn.Module):
             act = linear(nactions, self.action_proj_cond, out_dtype=c)
         else:
             act = self.fake_action_latent.to(c)[None].expand(B, 16, D)
-        streams = [x_e, cond_e, act.repeat_interleave(self.buffer_size_action, dim=1)]
+        streams = [x_e, cond_e]
+        if self.use_history_action:
+            # history actions [B, T*4, Da] -> latents, training drops each to the fake latent with
+            # probability 1 - action_mask_ratio (torch.rand(B, T*4) > ratio, :512-518)
+            fh = self.fake_latent_history_action.to(c)
+            if history_nactions is None:
+                ha = fh[None].expand(B, T * self.n_frames, D)
+            else:
+                ha = linear(history_nactions.float(), self.history_action_proj_cond, out_dtype=c)
+                if self.training:
+                    u = hist_u if hist_u is not None else torch.rand(B, T * self.n_frames)
+                    drop = (torch.as_tensor(u).to(ha.device) > self.action_mask_ratio)[..., None]
+                    ha = torch.where(drop, fh[None].expand_as(ha), ha)
+            streams.append(ha.repeat_interleave(self.buffer_size_action, dim=1))
+        streams.append(act.repeat_interleave(self.buffer_size_action, dim=1))
         if self.use_proprioception:
             ps = torch.cat([prop["robot0_eef_pos"], prop["robot0_eef_rot_axis_angle"], prop["robot0_gripper_width"],
                             prop["robot0_eef_rot_axis_angle_wrt_start"]], dim=-1).float()
@@ -290,7 +312,8 @@ class MAR(nn.Module):
         tdu = torch.as_tensor(tdu) if tdu is not None else torch.rand(B)
         draws = {"randint": [torch.as_tensor(a).to(dev) for a in rng.get("randint", [])],
                  "randn_like": [torch.as_tensor(a).to(dev) for a in rng.get("randn_like", [])]}
-        h = self.forward_mae_encoder(x, mask, cnd, text_latents, nactions, task_mode, proprioception_input, tdu)
+        h = self.forward_mae_encoder(x, mask, cnd, text_latents, nactions, task_mode, proprioception_input, tdu,
+                                     history_nactions, rng.get("hist_u"))
         z = self.forward_mae_decoder(h)
         return self.forward_loss(z, gt, mask, nactions, task_mode, proprioception_input, draws)
 
@@ -341,7 +364,7 @@ class MAR(nn.Module):
         for step in range(num_iter if task_mode not in act_modes else 1):
             m_full = torch.from_numpy(np.repeat(mask[:, None, :], T, axis=1).reshape(B, T * L)).to(dev)
             h = self.forward_mae_encoder(tokens, m_full, cnd, text_latents, nactions, task_mode,
-                                         proprioception_input, torch.ones(B))
+                                         proprioception_input, torch.ones(B), history_nactions)
             z = self.forward_mae_decoder(h)
             if self.predict_action:
                 if task_mode in act_modes:

@@ -246,6 +246,13 @@ class UnifiedVideoActionPolicy(nn.Module):
             for k in list(obs):
                 if "image" not in k and k in self.normalizer:
                     obs[k] = self.normalizer[k].normalize(obs[k])
+        T_traj = T
+        if self.use_history_action:
+            # (policy:395-396) every observation drops its first step; the trajectory split keeps the
+            # loaded horizon T (get_trajectory: history = nactions[:, 1:] first half)
+            obs = {k: (v[:, 1:] if torch.is_tensor(v) and v.dim() >= 2 else v) for k, v in obs.items()}
+            img = obs.get("image", obs.get(image_key(self.task_name)))
+            T = img.shape[1]
         opt = self.bound_optimizer()
         if opt is not None and self.training:
             red = opt.maybe_init_reducer(self.model)
@@ -274,10 +281,10 @@ class UnifiedVideoActionPolicy(nn.Module):
         tokens = self.vae_model.encode_tokens(x, eps)
         z = tokens[:n_half].reshape(B, -1, 256, tokens.shape[-1])
         c = tokens[n_half:].reshape(B, -1, 256, tokens.shape[-1])
-        _, trajectory = get_trajectory(nactions, T, self.shift_action, self.use_history_action)
+        history, trajectory = get_trajectory(nactions, T_traj, self.shift_action, self.use_history_action)
         mode = rng.get("task_mode") or random.choice(self.task_modes)
-        loss, video_loss, act_loss = self.model(z, c, None, trajectory, text_latents, task_mode=mode,
-                                                proprioception_input=prop, rng=rng)
+        loss, video_loss, act_loss = self.model(z, c, history if self.use_history_action else None, trajectory,
+                                                text_latents, task_mode=mode, proprioception_input=prop, rng=rng)
         if torch.is_grad_enabled() and _ddp_active():
             loss = loss + 0.0 * self.ddp_anchor  # the one parameter DDP reduces (see module docstring)
         return loss, (video_loss, act_loss)
@@ -296,6 +303,9 @@ class UnifiedVideoActionPolicy(nn.Module):
         "noise", "step_noise"} for parity runs."""
         rng = rng or {}
         obs = dict(obs_dict)
+        history = None
+        if self.use_history_action and "past_action" in obs:  # normalize_past_action (policy:256-264)
+            history = self._normalize("action", obs.pop("past_action").float())
         for task, key in self._EVAL_IMAGE_KEYS:  # resize_image_eval key mapping (data_utils.py:86-104)
             if task in self.task_name and key in obs:
                 obs["image"] = obs.pop(key)
@@ -335,7 +345,8 @@ class UnifiedVideoActionPolicy(nn.Module):
         _, act = self.model.sample_tokens(bsz=B, cond=c, text_latents=text_latents, num_iter=sp["num_iter"],
                                           cfg=sp["cfg"], cfg_schedule=sp["cfg_schedule"],
                                           temperature=sp["temperature"], proprioception_input=prop,
-                                          task_mode="policy_model", vae_model=self.vae_model, rng=rng)
+                                          history_nactions=history, task_mode="policy_model",
+                                          vae_model=self.vae_model, rng=rng)
         action_pred = act[..., :self.action_dim]
         if self.normalizer_type == "all":
             action_pred = self.normalizer["action"].unnormalize(action_pred)
