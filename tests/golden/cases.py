@@ -54,6 +54,14 @@ EXTRA_VARIANTS = {
     "pusht_hist": dict(task_name="pusht", Da=2, clip=False, use_proprioception=False,
                        predict_proprioception=False, different_history_freq=False, use_history_action=True,
                        modes=ALL_MODES, input_tag="mar/pusht_hist/e"),
+    # toolhang (config/task/toolhang.yaml) with the proprioception streams (second camera latents +
+    # eef pos / quat / gripper, :126-147, 545-566) and the proprioception head (9-d, :331-344) ...
+    "toolhang_prop": dict(task_name="toolhang", Da=10, clip=False, use_proprioception=True,
+                          predict_proprioception=True, different_history_freq=False, modes=ALL_MODES),
+    # ... and with the wrist-camera video stream + its video loss (predict_wrist_img, :97-114, 281-294, 738-776)
+    "toolhang_wrist": dict(task_name="toolhang", Da=10, clip=False, use_proprioception=True,
+                           predict_proprioception=True, different_history_freq=False, predict_wrist_img=True,
+                           modes=ALL_MODES),
 }
 B_MAR = 2
 
@@ -67,6 +75,7 @@ def mar_kwargs(variant):
     kw = dict(MAR_KW)
     kw.update(
         use_history_action=v.get("use_history_action", False),
+        predict_wrist_img=v.get("predict_wrist_img", False),
         task_name=v["task_name"], use_proprioception=v["use_proprioception"],
         predict_proprioception=v["predict_proprioception"],
         different_history_freq=v["different_history_freq"],
@@ -114,7 +123,14 @@ def mar_inputs(variant, B=B_MAR):
         d["text_latents"] = hash_normal(f"{tag}/text", (B, 512))
     if v.get("use_history_action"):
         d["history_nactions"] = hash_tensor(f"{tag}/hist", (B, 16, v["Da"]))
-    if v["use_proprioception"]:
+    if v["use_proprioception"] and v["task_name"] != "umi":
+        d["second_image_z"] = hash_normal(f"{tag}/z2", (B, 4, 16, 16, 16))
+        for i, (k, n) in enumerate((("robot0_eef_pos", 3), ("robot0_eef_quat", 4), ("robot0_gripper_qpos", 2))):
+            d[k] = hash_tensor(f"{tag}/s{i}", (B, 16, n))
+            d[k + "_pred"] = hash_tensor(f"{tag}/s{i}p", (B, 16, n))
+    if v.get("predict_wrist_img"):
+        d["pred_second_image_z"] = hash_normal(f"{tag}/z2p", (B, 4, 16, 16, 16))
+    if v["use_proprioception"] and v["task_name"] == "umi":
         d["robot0_eef_pos"] = hash_tensor(f"{tag}/p0", (B, 4, 3))
         d["robot0_eef_rot_axis_angle"] = hash_tensor(f"{tag}/p1", (B, 4, 6))
         d["robot0_gripper_width"] = hash_tensor(f"{tag}/p2", (B, 4, 1))
@@ -136,12 +152,15 @@ def mar_rng(variant, mode, B=B_MAR):
     if uses_video(mode):
         r["randint"].append(t_steps(tag + "/video", B * 1024))
         r["randn_like"].append(hash_normal(tag + "/video/noise", (B * 1024, 16)))
+        if v.get("predict_wrist_img"):
+            r["randint"].append(t_steps(tag + "/wrist", B * 1024))
+            r["randn_like"].append(hash_normal(tag + "/wrist/noise", (B * 1024, 16)))
     if uses_action(mode):
         r["randint"].append(t_steps(tag + "/act", B * 16))
         r["randn_like"].append(hash_normal(tag + "/act/noise", (B * 16, v["Da"])))
     if v["predict_proprioception"]:
         r["randint"].append(t_steps(tag + "/prop", B * 16))
-        r["randn_like"].append(hash_normal(tag + "/prop/noise", (B * 16, 6)))
+        r["randn_like"].append(hash_normal(tag + "/prop/noise", (B * 16, 6 if v["task_name"] == "umi" else 9)))
     return r
 
 

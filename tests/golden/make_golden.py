@@ -135,7 +135,7 @@ def mar_call(m, variant, mode, inp):
     t = {k: torch.from_numpy(x) for k, x in inp.items()}
     prop = {}
     if v["use_proprioception"]:
-        prop = {k: t[k] for k in t if k.startswith("robot0_")}
+        prop = {k: t[k] for k in t if k.startswith(("robot0_", "second_image", "pred_second_image"))}
     return m(t["z"], t["c"], t.get("history_nactions"), t["nactions"], t.get("text_latents"), task_mode=mode,
              proprioception_input=prop)
 
@@ -468,7 +468,7 @@ def gen_sample():
         torch.Tensor.cuda = lambda self, *a, **k: self
         ref_mar.MAR.sample_orders = lambda self, bsz: torch.from_numpy(rng["orders"])
         try:
-            prop = {k: inp[k] for k in inp if k.startswith("robot0_") and not k.endswith("_pred")}
+            prop = {k: inp[k] for k in inp if k.startswith(("robot0_", "second_image", "pred_second_image")) and not k.endswith("_pred")}
             _, act = m.sample_tokens(bsz=cases.B_MAR, cond=inp["c"], text_latents=inp.get("text_latents"),
                                      num_iter=1, cfg=1.0, temperature=cases.SAMPLE_TEMPERATURE,
                                      proprioception_input=prop, task_mode="policy_model")

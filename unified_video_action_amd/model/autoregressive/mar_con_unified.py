@@ -78,8 +78,11 @@ class MAR(nn.Module):
         self.use_proprioception = kwargs.get("use_proprioception") or False
         self.predict_wrist_img = kwargs.get("predict_wrist_img") or False
         self.predict_proprioception = kwargs.get("predict_proprioception") or False
-        if self.predict_wrist_img:
-            raise NotImplementedError("the wrist-image variant is outside the accelerated path")
+        self.umi = self.task_name == "umi"
+        if self.predict_wrist_img and self.umi:
+            # the reference's wrist branch reads proprioception_image_cond, which its UMI branch never
+            # builds (mar_con_unified.py:579-587): unrunnable there too
+            raise NotImplementedError("predict_wrist_img with the UMI proprioception streams")
         self.n_frames = 4
         self.seq_h = self.seq_w = img_size // vae_stride // patch_size
         self.seq_len = self.seq_h * self.seq_w
@@ -98,18 +101,25 @@ class MAR(nn.Module):
         self.fake_latent_x = nn.Parameter(torch.zeros(1, D))
         self.fake_action_latent = nn.Parameter(torch.zeros(1, D))
         n_streams = 3
+        if self.predict_wrist_img:  # (:97-114, 465-498): the wrist camera's latents as one more stream
+            self.z_proj_wrist = nn.Linear(self.token_embed_dim, D)
+            self.fake_latent_wrist_x = nn.Parameter(torch.zeros(1, D))
+            n_streams += 1
         if self.use_history_action:  # (:115-124, 504-522): one more conditioning stream
             self.action_mask_ratio = kwargs["action_mask_ratio"]
             self.fake_latent_history_action = nn.Parameter(torch.zeros(1, D))
             self.history_action_proj_cond = nn.Linear(act_dim, D)
             n_streams += 1
         if self.use_proprioception:
-            if self.task_name != "umi":
-                raise NotImplementedError("proprioception is accelerated for the UMI path only")
+            if not self.umi and ("pusht" in self.task_name or "block_push" in self.task_name):
+                # the reference builds a 2-d state projection there but its encoder reads the
+                # second camera and the robot0_* states (:545-566): unrunnable in the reference
+                raise NotImplementedError("use_proprioception for pusht / block_push")
             self.buffer_size_properception = 64 * 4 if self.different_history_freq else 64
-            self.proprioception_proj_cond = nn.Linear(16, D)
+            # (:126-147) UMI: 16-d state stream; toolhang & co: the second camera's latents + 9-d state
+            self.proprioception_proj_cond = nn.Linear(16 if self.umi else 9, D)
             self.proprioception_image_proj_cond = nn.Linear(self.token_embed_dim, D)
-            n_streams += 1
+            n_streams += 1 if self.umi else 2
         self.language_emb_model = kwargs.get("language_emb_model")
         self.clip = self.language_emb_model == "clip"
         if self.clip:
@@ -139,16 +149,21 @@ class MAR(nn.Module):
         if predict_video:
             self.diffloss = DiffLoss(self.token_embed_dim, Dd, diffloss_d, diffloss_w, num_sampling_steps,
                                      grad_checkpointing, n_frames=self.n_frames)
+            if self.predict_wrist_img:  # (:281-294)
+                self.diffloss_wrist = DiffLoss(self.token_embed_dim, Dd, diffloss_d, diffloss_w, num_sampling_steps,
+                                               grad_checkpointing, n_frames=self.n_frames)
         if self.predict_action:
             self.diffactloss = DiffActLoss(act_dim, Dd, diffloss_act_d, diffloss_act_w, num_sampling_steps,
                                            grad_checkpointing, n_frames=self.n_frames,
                                            act_model_type=action_model_params.get("act_model_type", "conv_fc"),
                                            act_diff_training_steps=act_diff_training_steps)
         if self.predict_proprioception:
-            if self.task_name != "umi":
-                raise NotImplementedError
-            self.diffproploss = DiffActLoss(6, Dd, diffloss_act_d, diffloss_act_w, num_sampling_steps,
-                                            grad_checkpointing, n_frames=self.n_frames,
+            # (:313-344) UMI: 6-d rotation targets; toolhang: eef pos + quat + gripper (9-d)
+            if not (self.umi or self.task_name == "toolhang"):
+                raise NotImplementedError(f"predict_proprioception for task {self.task_name}")
+            self.diffproploss = DiffActLoss(6 if self.umi else 9, Dd, diffloss_act_d, diffloss_act_w,
+                                            num_sampling_steps, grad_checkpointing, n_frames=self.n_frames,
+                                            act_model_type=action_model_params.get("act_model_type", "conv_fc"),
                                             act_diff_training_steps=act_diff_training_steps)
 
     # ---- init (mar_con_unified.py:349-391) ----------------------------------------------
@@ -162,6 +177,8 @@ class MAR(nn.Module):
                 nn.init.normal_(p, std=0.02)
         if self.use_history_action:
             nn.init.normal_(self.fake_latent_history_action, std=0.02)
+        if self.predict_wrist_img:
+            nn.init.normal_(self.fake_latent_wrist_x, std=0.02)
         for m in self.modules():
             if isinstance(m, nn.Linear):
                 nn.init.xavier_uniform_(m.weight)
@@ -207,21 +224,32 @@ class MAR(nn.Module):
         D = self.fake_latent_x.shape[1]
         c = cdt()
         fake = self.fake_latent_x.to(c)
+        wrist = None
+        if self.predict_wrist_img:
+            fw = self.fake_latent_wrist_x.to(c)
         if task_mode == "policy_model":
             cond_e = linear(cond, self.z_proj_cond, out_dtype=c).reshape(B, T * S, D)
             x_e = fake.expand(B, T * S, D)
+            if self.predict_wrist_img:
+                wrist = fw.expand(B, T * S, D)
         elif task_mode == "inverse_model":
             x_e = linear(x, self.z_proj, out_dtype=c).reshape(B, T * S, D)
             cond_e = fake.expand(B, T * S, D)
+            if self.predict_wrist_img:
+                wrist = linear(prop["pred_second_image_z"], self.z_proj_wrist, out_dtype=c).reshape(B, T * S, D)
         else:
             cond_e = linear(cond, self.z_proj_cond, out_dtype=c).reshape(B, T * S, D)
             x_e = linear(x, self.z_proj, out_dtype=c).reshape(B, T * S, D)
             x_e = torch.where(mask[..., None] == 1, fake.expand(B, T * S, D), x_e)
+            if self.predict_wrist_img:
+                wrist = linear(prop["pred_second_image_z"], self.z_proj_wrist, out_dtype=c).reshape(B, T * S, D)
+                wrist = torch.where(mask[..., None] == 1, fw.expand(B, T * S, D), wrist)
         if task_mode == "dynamic_model":
             act = linear(nactions, self.action_proj_cond, out_dtype=c)
         else:
             act = self.fake_action_latent.to(c)[None].expand(B, 16, D)
-        streams = [x_e, cond_e]
+        # stream order of :579-603: x (, wrist), cond (, history), action (, proprioception)
+        streams = [x_e] + ([wrist] if wrist is not None else []) + [cond_e]
         if self.use_history_action:
             # history actions [B, T*4, Da] -> latents, training drops each to the fake latent with
             # probability 1 - action_mask_ratio (torch.rand(B, T*4) > ratio, :512-518)
@@ -237,8 +265,14 @@ class MAR(nn.Module):
             streams.append(ha.repeat_interleave(self.buffer_size_action, dim=1))
         streams.append(act.repeat_interleave(self.buffer_size_action, dim=1))
         if self.use_proprioception:
-            ps = torch.cat([prop["robot0_eef_pos"], prop["robot0_eef_rot_axis_angle"], prop["robot0_gripper_width"],
-                            prop["robot0_eef_rot_axis_angle_wrt_start"]], dim=-1).float()
+            if self.umi:
+                ps = torch.cat([prop["robot0_eef_pos"], prop["robot0_eef_rot_axis_angle"], prop["robot0_gripper_width"],
+                                prop["robot0_eef_rot_axis_angle_wrt_start"]], dim=-1).float()
+            else:  # (:545-566): the second camera's latents, then eef pos + quat + gripper
+                pi = linear(prop["second_image_z"], self.proprioception_image_proj_cond, out_dtype=c)
+                streams.append(pi.reshape(B, -1, D))
+                ps = torch.cat([prop["robot0_eef_pos"], prop["robot0_eef_quat"], prop["robot0_gripper_qpos"]],
+                               dim=-1).float()
             pe = linear(ps, self.proprioception_proj_cond, out_dtype=c)
             streams.append(pe.repeat_interleave(self.buffer_size_properception, dim=1))
         h = linear(torch.cat(streams, dim=-1), self.proj_cond_x_layer, out_dtype=F32)
@@ -269,7 +303,7 @@ class MAR(nn.Module):
         return h + self._pos(self.diffusion_temporal_embed, self.diffusion_spatial_embed)
 
     # ---- losses (:728-787) --------------------------------------------------------------
-    def forward_loss(self, z, target, mask, nactions, task_mode, prop, draws):
+    def forward_loss(self, z, target, mask, nactions, task_mode, prop, draws, gt_wrist=None):
         zero = torch.zeros((), device=z.device)
         video_loss = act_loss = zero
 
@@ -281,6 +315,9 @@ class MAR(nn.Module):
         if task_mode in ("video_model", "dynamic_model", "full_dynamic_model"):
             t, nz = nxt()
             video_loss = self.diffloss(target, z, mask, t=t, noise=nz)
+            if self.predict_wrist_img:  # (:738-776) the wrist video loss is part of the video loss
+                t, nz = nxt()
+                video_loss = video_loss + self.diffloss_wrist(gt_wrist, z, mask, t=t, noise=nz)
         if task_mode in ("policy_model", "inverse_model", "full_dynamic_model"):
             t, nz = nxt()
             act_loss = self.diffactloss(nactions, z, task_mode, t=t, noise=nz)
@@ -292,7 +329,12 @@ class MAR(nn.Module):
             loss = act_loss
         if self.predict_proprioception:
             t, nz = nxt()
-            loss = loss + self.diffproploss(prop["robot0_eef_rot_axis_angle_wrt_start_pred"], z, t=t, noise=nz)
+            if self.umi:
+                gt_prop = prop["robot0_eef_rot_axis_angle_wrt_start_pred"]
+            else:  # toolhang (:891-897)
+                gt_prop = torch.cat([prop["robot0_eef_pos_pred"], prop["robot0_eef_quat_pred"],
+                                     prop["robot0_gripper_qpos_pred"]], dim=-1)
+            loss = loss + self.diffproploss(gt_prop, z, t=t, noise=nz)
         return loss, video_loss, act_loss
 
     def forward(self, imgs, cond, history_nactions=None, nactions=None, text_latents=None, task_mode=None,
@@ -312,10 +354,20 @@ class MAR(nn.Module):
         tdu = torch.as_tensor(tdu) if tdu is not None else torch.rand(B)
         draws = {"randint": [torch.as_tensor(a).to(dev) for a in rng.get("randint", [])],
                  "randn_like": [torch.as_tensor(a).to(dev) for a in rng.get("randn_like", [])]}
-        h = self.forward_mae_encoder(x, mask, cnd, text_latents, nactions, task_mode, proprioception_input, tdu,
+        prop = self._prop_tokens(proprioception_input)
+        h = self.forward_mae_encoder(x, mask, cnd, text_latents, nactions, task_mode, prop, tdu,
                                      history_nactions, rng.get("hist_u"))
         z = self.forward_mae_decoder(h)
-        return self.forward_loss(z, gt, mask, nactions, task_mode, proprioception_input, draws)
+        gt_wrist = prop["pred_second_image_z"].reshape(B, -1, x.shape[-1]) if self.predict_wrist_img else None
+        return self.forward_loss(z, gt, mask, nactions, task_mode, prop, draws, gt_wrist)
+
+    def _prop_tokens(self, prop):
+        """second-camera latents [B, T, C, H, W] (or token-major [B, T, S, C]) -> fp32 tokens (:816-845)"""
+        prop = dict(prop)
+        for k in ("second_image_z", "pred_second_image_z"):
+            if k in prop and prop[k] is not None:
+                prop[k] = self.to_tokens(prop[k]).to(F32)
+        return prop
 
 
     # ---- inference (:945-1151) ----------------------------------------------------------
@@ -341,6 +393,10 @@ class MAR(nn.Module):
         T, L = self.n_frames, self.seq_len
         if text_latents is not None and self.clip:
             text_latents = linear(text_latents.to(dev).float(), self.text_proj_cond, out_dtype=F32)
+        proprioception_input = self._prop_tokens(proprioception_input)
+        if self.predict_wrist_img and task_mode != "inverse_model":
+            # (:1003-1006) the wrist stream starts from zero latents and is never sampled
+            proprioception_input["pred_second_image_z"] = torch.zeros(B, T, L, self.token_embed_dim, device=dev)
         if task_mode == "inverse_model":
             tokens = self.to_tokens(x).to(F32)
             mask = np.zeros((B, L), np.float32)
