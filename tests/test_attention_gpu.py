@@ -43,6 +43,24 @@ def test_flash_fwd_bwd_vs_fp32(B, N, H):
         assert rel_err(d[:, :, i].permute(0, 2, 1, 3), t.grad) < 3e-2, i
 
 
+@pytest.mark.parametrize("B,N,H", [(2, 1024, 12), (1, 1088, 12)])
+def test_flash_lse_fp32_pin_vs_fp64(B, N, H):
+    """fp32 pin of the benched forward's statistics: the per-row log-sum-exp (log2 domain, what the
+    backward recomputes P from) against fp64 math on the same bf16 Q / K -- the only error is fp32
+    accumulation of S and of the row sum (the output O is held to bf16 by the bf16 P of the PV product)."""
+    from unified_video_action_amd.native import ops
+    torch.manual_seed(2)
+    qkv = (torch.randn(B, N, 3 * H * 64, device=DEV) * 2.0).to(torch.bfloat16)
+    out = torch.empty(B, N, H * 64, device=DEV, dtype=torch.bfloat16)
+    lse = torch.empty(B, H, N, device=DEV)
+    ops.attn_fwd(qkv, out, lse, B, N, H, 0.125)
+    q, k, _ = qkv.double().view(B, N, 3, H, 64).permute(2, 0, 3, 1, 4)
+    s2 = (q @ k.transpose(-1, -2)) * (0.125 / torch.log(torch.tensor(2.0, dtype=torch.float64)))
+    ref = torch.logsumexp(s2 * torch.log(torch.tensor(2.0, dtype=torch.float64)), dim=-1) / torch.log(
+        torch.tensor(2.0, dtype=torch.float64))
+    assert (lse.double() - ref).abs().max().item() < 5e-6 * ref.abs().max().item() + 1e-5
+
+
 def test_flash_rescale_branch_forced():
     """Spike one key so the running max jumps mid-sweep (exercises the online rescale)."""
     from unified_video_action_amd.native import ops

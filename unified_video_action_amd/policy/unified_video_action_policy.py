@@ -269,6 +269,8 @@ class UnifiedVideoActionPolicy(nn.Module):
         else:
             sel = select_frame_indices(T, different_history_freq=self.different_history_freq,
                                        rng_choice=rng.get("history_combination"))
+            if self.use_proprioception:
+                prop = self._second_camera_prop(obs, sel, train=True)
         if self.training and dev.type == "cuda":
             RT.prefetch_attn_masks(dev)  # attention dropout planes under the VAE encode (side stream)
         x = vae_images(img, sel, self.vae_model.CIN_PAD)
@@ -291,6 +293,33 @@ class UnifiedVideoActionPolicy(nn.Module):
 
     def forward(self, batch, **kwargs):
         return self.compute_loss(batch, **kwargs)
+
+    def _second_camera_prop(self, obs, sel, train):
+        """process_data's second-camera branch (toolhang, data_utils.py:228-285) + get_vae_latent's
+        second-image encodes (:395-410): the wrist frames at the selected indices through the KL-VAE
+        (history half -> second_image_z, future half -> pred_second_image_z when training), the
+        eef pos / quat / gripper states split into history / future halves (train) or whole (eval)."""
+        wk = "wrist_image" if "wrist_image" in obs else "robot0_eye_in_hand_image"
+        wrist = obs[wk]
+        B = wrist.shape[0]
+        h = len(sel) // 2
+        xw = vae_images(wrist, sel, self.vae_model.CIN_PAD)  # [future half | history half]
+        eps = torch.randn(xw.shape[0], self.vae_model.embed_dim, 16, 16, device=wrist.device)
+        tok = self.vae_model.encode_tokens(xw, eps).reshape(2, B, h, 256, -1)
+        prop = {}
+        keys = ("robot0_eef_pos", "robot0_eef_quat", "robot0_gripper_qpos")
+        if train:
+            prop["second_image_z"], prop["pred_second_image_z"] = tok[1], tok[0]
+            for k in keys:
+                prop[k], prop[k + "_pred"] = torch.chunk(obs[k].float(), 2, dim=1)
+                if self.different_history_freq:
+                    prop[k] = prop[k][:, torch.as_tensor(np.asarray(sel[:h]), device=wrist.device)]
+        else:
+            prop["second_image_z"] = torch.cat([tok[1], tok[0]], dim=1)  # all selected frames, in order
+            for k in keys:
+                v = obs[k].float()
+                prop[k] = v[:, torch.as_tensor(np.asarray(sel), device=wrist.device)] if self.different_history_freq else v
+        return prop
 
     _EVAL_IMAGE_KEYS = (("libero", "agentview_image"), ("toolhang", "sideview_image"), ("umi", "camera0_rgb"))
 
@@ -329,6 +358,8 @@ class UnifiedVideoActionPolicy(nn.Module):
                 prop = umi_proprioception(obs, idx, self.different_history_freq, train=False)
         else:
             sel = select_frame_indices(T, eval=True)
+            if self.use_proprioception:
+                prop = self._second_camera_prop(obs, sel, train=False)
         if len(sel) % 2:
             raise ValueError(f"eval frame selection {sel.tolist()} must hold an even number of frames")
         x = vae_images(img, sel, self.vae_model.CIN_PAD)  # [sel[h:] per sample | sel[:h] per sample]
