@@ -321,26 +321,37 @@ class MAR(nn.Module):
                  vae_embed_dim=16, diffloss_d=6, diffloss_w=1024, diffloss_act_d=6,
                  diffloss_act_w=1024, task_name="pusht", act_dim=2, predict_action=True,
                  use_proprioception=False, predict_proprioception=False,
-                 different_history_freq=False, language_emb_model=None, **unused):
+                 different_history_freq=False, language_emb_model=None, use_history_action=False,
+                 predict_wrist_img=False, action_mask_ratio=0.5, **unused):
         super().__init__()
         D, Dd = encoder_embed_dim, decoder_embed_dim
         self.task_name = task_name
+        self.umi = task_name == "umi"
         self.n_frames, self.seq_len, self.C = 4, 256, vae_embed_dim
         self.use_proprioception = use_proprioception
         self.predict_proprioception = predict_proprioception
+        self.use_history_action = use_history_action
+        self.predict_wrist_img = predict_wrist_img
+        self.action_mask_ratio = action_mask_ratio
         self.clip = language_emb_model == "clip"
         self.z_proj_cond = nn.Linear(self.C, D)
         self.z_proj = nn.Linear(self.C, D)
+        if predict_wrist_img:  # mar_con_unified.py:97-114
+            self.z_proj_wrist = nn.Linear(self.C, D)
+            self.fake_latent_wrist_x = nn.Parameter(torch.zeros(1, D))
         self.action_proj_cond = nn.Linear(act_dim, D)
         self.fake_latent_x = nn.Parameter(torch.zeros(1, D))
         self.fake_action_latent = nn.Parameter(torch.zeros(1, D))
-        n_streams = 3
-        if use_proprioception:
-            assert task_name == "umi", "only the UMI proprio path is in scope"
-            self.prop_repeat = 256 if different_history_freq else 64
-            self.proprioception_proj_cond = nn.Linear(16, D)
-            self.proprioception_image_proj_cond = nn.Linear(self.C, D)  # unused on UMI
+        n_streams = 3 + int(predict_wrist_img)
+        if use_history_action:  # :115-124
+            self.fake_latent_history_action = nn.Parameter(torch.zeros(1, D))
+            self.history_action_proj_cond = nn.Linear(act_dim, D)
             n_streams += 1
+        if use_proprioception:  # :126-147 (umi: 16-d state; toolhang: second camera + 9-d state)
+            self.prop_repeat = 256 if different_history_freq else 64
+            self.proprioception_proj_cond = nn.Linear(16 if self.umi else 9, D)
+            self.proprioception_image_proj_cond = nn.Linear(self.C, D)  # unused on UMI
+            n_streams += 1 if self.umi else 2
         if self.clip:
             self.fake_latent = nn.Parameter(torch.zeros(1, D))
             self.text_proj_cond = nn.Linear(512, D)
@@ -363,11 +374,13 @@ class MAR(nn.Module):
         self.diffusion_temporal_embed = nn.Parameter(torch.zeros(1, 4, Dd))
         self.diffusion_spatial_embed = nn.Parameter(torch.zeros(1, 256, Dd))
         self.diffloss = DiffLoss(self.C, Dd, diffloss_w, diffloss_d)
+        if predict_wrist_img:  # :281-294
+            self.diffloss_wrist = DiffLoss(self.C, Dd, diffloss_w, diffloss_d)
         self.predict_action = predict_action
         if predict_action:
             self.diffactloss = DiffActLoss(act_dim, Dd, diffloss_act_w, diffloss_act_d)
-        if predict_proprioception:
-            self.diffproploss = DiffActLoss(6, Dd, diffloss_act_w, diffloss_act_d)
+        if predict_proprioception:  # :313-344
+            self.diffproploss = DiffActLoss(6 if self.umi else 9, Dd, diffloss_act_w, diffloss_act_d)
 
     @staticmethod
     def patchify(z):
@@ -386,28 +399,53 @@ class MAR(nn.Module):
     def _pos(self, temporal, spatial):
         return (temporal[:, :, None, :] + spatial[:, None, :, :]).reshape(1, -1, temporal.shape[-1])
 
-    def encode(self, x, cond, mask, nactions, text, mode, prop, text_drop_u):
+    def encode(self, x, cond, mask, nactions, text, mode, prop, text_drop_u, hist=None, hist_u=None):
         B = x.shape[0]
+        D = self.fake_latent_x.shape[1]
         m = mask.reshape(B, -1)
+        wrist = None
         if mode == "policy_model":
-            cond = self.z_proj_cond(cond).reshape(B, -1, self.fake_latent_x.shape[1])
+            cond = self.z_proj_cond(cond).reshape(B, -1, D)
             x = self.fake_latent_x.expand(B, cond.shape[1], -1)
+            if self.predict_wrist_img:
+                wrist = self.fake_latent_wrist_x.expand(B, cond.shape[1], -1)
         elif mode == "inverse_model":
-            x = self.z_proj(x).reshape(B, -1, self.fake_latent_x.shape[1])
+            x = self.z_proj(x).reshape(B, -1, D)
             cond = self.fake_latent_x.expand(B, x.shape[1], -1)
+            if self.predict_wrist_img:
+                wrist = self.z_proj_wrist(prop["pred_second_image_z"]).reshape(B, -1, D)
         else:
-            cond = self.z_proj_cond(cond).reshape(B, -1, self.fake_latent_x.shape[1])
-            x = self.z_proj(x).reshape(B, -1, self.fake_latent_x.shape[1])
+            cond = self.z_proj_cond(cond).reshape(B, -1, D)
+            x = self.z_proj(x).reshape(B, -1, D)
             x = torch.where(m[..., None] == 1, self.fake_latent_x.expand_as(x), x)
+            if self.predict_wrist_img:
+                wrist = self.z_proj_wrist(prop["pred_second_image_z"]).reshape(B, -1, D)
+                wrist = torch.where(m[..., None] == 1, self.fake_latent_wrist_x.expand_as(wrist), wrist)
         if mode == "dynamic_model":
             act = self.action_proj_cond(nactions)
         else:
             act = self.fake_action_latent[None].expand(B, 16, -1)
-        streams = [x, cond, act.repeat_interleave(64, dim=1)]
+        # stream order :579-603: x (, wrist), cond (, history), action (, proprioception)
+        streams = [x] + ([wrist] if wrist is not None else []) + [cond]
+        if self.use_history_action:  # :504-522
+            if hist is None:
+                ha = self.fake_latent_history_action[None].expand(B, 16, -1)
+            else:
+                ha = self.history_action_proj_cond(hist)
+                if self.training:
+                    drop = (torch.as_tensor(hist_u) > self.action_mask_ratio)[..., None]
+                    ha = torch.where(drop, self.fake_latent_history_action[None].expand_as(ha), ha)
+            streams.append(ha.repeat_interleave(64, dim=1))
+        streams.append(act.repeat_interleave(64, dim=1))
         if self.use_proprioception:
-            ps = torch.cat([prop["robot0_eef_pos"], prop["robot0_eef_rot_axis_angle"],
-                            prop["robot0_gripper_width"],
-                            prop["robot0_eef_rot_axis_angle_wrt_start"]], dim=-1)
+            if self.umi:
+                ps = torch.cat([prop["robot0_eef_pos"], prop["robot0_eef_rot_axis_angle"],
+                                prop["robot0_gripper_width"],
+                                prop["robot0_eef_rot_axis_angle_wrt_start"]], dim=-1)
+            else:  # :545-566
+                streams.append(self.proprioception_image_proj_cond(prop["second_image_z"]).reshape(B, -1, D))
+                ps = torch.cat([prop["robot0_eef_pos"], prop["robot0_eef_quat"], prop["robot0_gripper_qpos"]],
+                               dim=-1)
             streams.append(self.proprioception_proj_cond(ps.float())
                            .repeat_interleave(self.prop_repeat, dim=1))
         h = self.proj_cond_x_layer(torch.cat(streams, dim=-1))
@@ -488,15 +526,20 @@ class MAR(nn.Module):
         out = tokens.reshape(B * 4, 16, 16, -1).permute(0, 3, 1, 2)
         return out, act
 
-    def forward(self, z, c, nactions, text_latents, mode, rng, prop=None):
+    def forward(self, z, c, nactions, text_latents, mode, rng, prop=None, hist=None):
         """Training forward -> (loss, video_loss, act_loss) with injected draws `rng`."""
         B = z.shape[0]
         x = self.patchify(z.reshape(B * 4, *z.shape[2:])).reshape(B, 4, 256, -1)
         cond = self.patchify(c.reshape(B * 4, *c.shape[2:])).reshape(B, 4, 256, -1)
+        prop = dict(prop or {})
+        for k in ("second_image_z", "pred_second_image_z"):  # :816-845
+            if k in prop:
+                v = prop[k]
+                prop[k] = self.patchify(v.reshape(B * 4, *v.shape[2:])).reshape(B, 4, 256, -1)
         text = self.text_proj_cond(text_latents) if self.clip else None
         mask = self.token_mask(torch.as_tensor(rng["orders"]), rng["mask_rate"])
         h = self.encode(x, cond, mask, nactions, text, mode, prop,
-                        torch.as_tensor(rng.get("text_drop_u", np.ones(B, np.float32))))
+                        torch.as_tensor(rng.get("text_drop_u", np.ones(B, np.float32))), hist, rng.get("hist_u"))
         zdec = self.decode(h)
         gt = x.reshape(B, 1024, -1)
         ti = iter(torch.as_tensor(a) for a in rng["randint"])
@@ -505,12 +548,19 @@ class MAR(nn.Module):
         lv = la = zero
         if mode in ("video_model", "dynamic_model", "full_dynamic_model"):
             lv = self.diffloss(gt, zdec, mask.reshape(B, -1), next(ti), next(ni))
+            if self.predict_wrist_img:  # :738-776
+                lv = lv + self.diffloss_wrist(prop["pred_second_image_z"].reshape(B, 1024, -1), zdec,
+                                              mask.reshape(B, -1), next(ti), next(ni))
         if mode in ("policy_model", "inverse_model", "full_dynamic_model"):
             la = self.diffactloss(nactions, zdec, next(ti), next(ni))
         loss = lv + la if mode == "full_dynamic_model" else (lv if la is zero else la)
         if self.predict_proprioception:
-            loss = loss + self.diffproploss(prop["robot0_eef_rot_axis_angle_wrt_start_pred"],
-                                            zdec, next(ti), next(ni))
+            if self.umi:
+                gt_prop = prop["robot0_eef_rot_axis_angle_wrt_start_pred"]
+            else:  # toolhang :891-897
+                gt_prop = torch.cat([prop["robot0_eef_pos_pred"], prop["robot0_eef_quat_pred"],
+                                     prop["robot0_gripper_qpos_pred"]], dim=-1)
+            loss = loss + self.diffproploss(gt_prop, zdec, next(ti), next(ni))
         return loss, lv, la
 
 

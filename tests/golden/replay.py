@@ -33,6 +33,8 @@ def mar_ctor_kwargs(variant):
         act_dim=v["Da"], predict_action=True, use_proprioception=v["use_proprioception"],
         predict_proprioception=v["predict_proprioception"],
         different_history_freq=v["different_history_freq"],
+        use_history_action=v.get("use_history_action", False), predict_wrist_img=v.get("predict_wrist_img", False),
+        action_mask_ratio=cases.MAR_KW["action_mask_ratio"],
         language_emb_model="clip" if v["clip"] else None)
 
 

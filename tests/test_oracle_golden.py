@@ -57,22 +57,28 @@ def test_diffusion_tables_and_math():
         np.testing.assert_allclose(out.grad.numpy(), g[f"{tag}_gout"], rtol=1e-4, atol=1e-6)
 
 
-@pytest.mark.parametrize("variant,mode", [(v, m) for v in cases.VARIANTS
-                                          for m in cases.VARIANTS[v]["modes"]])
+@pytest.mark.parametrize("variant,mode", [(v, m) for vs in (cases.VARIANTS, cases.EXTRA_VARIANTS) for v in vs
+                                          for m in vs[v]["modes"]])
 def test_mar_loss_and_grads(variant, mode):
     g = replay.load(f"g2_mar_{variant}_{mode}.npz")
     m = O.MAR(**replay.mar_ctor_kwargs(variant))
     hash_init_(m, "mar.")
     inp, rng = replay.mar_case(variant, mode)
-    prop = {k: v for k, v in inp.items() if k.startswith("robot0_")} or None
-    loss, lv, la = m(inp["z"], inp["c"], inp["nactions"], inp.get("text_latents"), mode, rng, prop)
+    prop = {k: v for k, v in inp.items() if k.startswith(("robot0_", "second_image", "pred_second_image"))} or None
+    loss, lv, la = m(inp["z"], inp["c"], inp["nactions"], inp.get("text_latents"), mode, rng, prop,
+                     inp.get("history_nactions"))
     ref = g["loss"]
     for got, want in zip((loss.item(), float(lv), float(la)), ref):
         assert abs(got - want) <= 1e-4 * max(abs(want), 1e-6), (got, want)
     loss.backward()
     errs = replay.grad_rel_errors(m.named_parameters(), g, "grad_names", "grad_sums", "grad_heads")
     worst = max(errs.items(), key=lambda kv: kv[1])
-    assert worst[1] < 3e-3, worst  # fp32 op-order noise; semantic errors are O(1)
+    # fp32 op-order noise; semantic errors are O(1).  The off-config variants (cases.EXTRA_VARIANTS) run
+    # two trunks (action + proprioception) whose ReLU pre-activations come within 1.5e-8 - 3.4e-7 of
+    # their max from zero over every input stream tried (make_golden / tools/hist_dbg2.py margins): a
+    # ReLU that two fp32 summation orders resolve differently moves single gradient rows by O(1), up to
+    # 6.6e-3 on the checksums here -- 1e-2 for them
+    assert worst[1] < (3e-3 if variant in cases.VARIANTS else 1e-2), worst
 
 
 def test_block_full_geometry():
