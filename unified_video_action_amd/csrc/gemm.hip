@@ -1744,18 +1744,34 @@ __global__ __launch_bounds__(256) void splitk_reduce(const float* __restrict__ p
 
 // Plain-epilogue fp32 reduce (the dW products: C = alpha * sum + beta * C), 16-byte lanes: the
 // scalar kernel above spends its time on 4-byte loads and a 64-bit divide per element.
+// The slab loads go out four at a time ahead of their (slice-ordered) adds, so a thread keeps four
+// 16-B reads in flight instead of one; a contiguous C (ldc == N: every gradient buffer) skips the
+// per-element 64-bit row division.
 __global__ __launch_bounds__(256) void splitk_reduce_f32x4(const float4* __restrict__ part, int splits,
                                                            float* __restrict__ C, int N, long long n4, long long ldc,
                                                            float alpha, float beta) {
   for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (long long)gridDim.x * blockDim.x) {
     float4 a = part[i];
-    for (int k = 1; k < splits; ++k) {
+    int k = 1;
+    for (; k + 4 <= splits; k += 4) {
+      const float4 b0 = part[k * n4 + i], b1 = part[(k + 1) * n4 + i];
+      const float4 b2 = part[(k + 2) * n4 + i], b3 = part[(k + 3) * n4 + i];
+      a.x += b0.x; a.y += b0.y; a.z += b0.z; a.w += b0.w;  // slice order kept: bitwise as one at a time
+      a.x += b1.x; a.y += b1.y; a.z += b1.z; a.w += b1.w;
+      a.x += b2.x; a.y += b2.y; a.z += b2.z; a.w += b2.w;
+      a.x += b3.x; a.y += b3.y; a.z += b3.z; a.w += b3.w;
+    }
+    for (; k < splits; ++k) {
       const float4 b = part[k * n4 + i];
       a.x += b.x; a.y += b.y; a.z += b.z; a.w += b.w;
     }
     const long long e = 4 * i;
-    const long long row = e / N;
-    float4* c = (float4*)(C + row * ldc + (e - row * N));
+    long long off = e;
+    if (ldc != N) {
+      const long long row = e / N;
+      off = row * ldc + (e - row * N);
+    }
+    float4* c = (float4*)(C + off);
     float4 v = make_float4(alpha * a.x, alpha * a.y, alpha * a.z, alpha * a.w);
     if (beta != 0.f) {
       const float4 o = *c;
