@@ -440,7 +440,9 @@ __global__ __launch_bounds__(256) void softmax_bwd_kernel(const T* __restrict__ 
 
 #define DISPATCH_LN(KERNEL, TI, TO, ...)                                                    \
   do {                                                                                       \
-    if (D % 256 == 0 && D <= 1024) {                                                         \
+    if (D == 768) { /* the Block width: three 4-wide chunks per lane, no idle fourth chunk */ \
+      KERNEL<TI, TO, 4, 3><<<grid, 256, 0, stream>>>(__VA_ARGS__);                           \
+    } else if (D % 256 == 0 && D <= 1024) {                                                  \
       KERNEL<TI, TO, 4, 4><<<grid, 256, 0, stream>>>(__VA_ARGS__);                           \
     } else if (D <= 1024) {                                                                  \
       KERNEL<TI, TO, 1, 16><<<grid, 256, 0, stream>>>(__VA_ARGS__);                          \
