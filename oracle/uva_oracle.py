@@ -10,6 +10,10 @@ Parameter names follow the reference (timm Block names, MAR/DiffLoss/VAE
 attribute names) so that hash-initialised weights and checkpoints line up.
 Every random draw of the step is taken from an explicit `rng` dict (see
 tests/golden/cases.py) instead of global generators.
+
+The MAR restatement also covers the variants no shipped config turns on (use_history_action,
+the toolhang second camera + 9-d state streams and proprioception head, predict_wrist_img),
+pinned by the reference-run goldens of cases.EXTRA_VARIANTS (test_oracle_golden.py).
 """
 import math
 
