@@ -21,7 +21,7 @@ import sys
 # size (("size", k): the k-th largest quarter... see split_pt)
 MEAN = {"conv3x3/s1 bf16 256x256 Ci128 Co128 n256", "conv3x3/s1 bf16 128x128 Ci128 Co128 n256"}
 TAGS = {
-    "attn_bwd B32 N1024 H12": [("attn_bwd_pre", None), ("attn_bwd_dkdv", None), ("attn_bwd_dq", None),
+    "attn_bwd B32 N1024 H12": [("attn_bwd_dkdv", None), ("attn_bwd_dq", None),
                                ("attn_bwd_fused", None), ("attn_bwd_mask", None)],
     "attn_fwd B32 N1024 H12": [("attn_fwd", None), ("attn_mask", None)],
     "conv3x3/s1 bf16 256x256 Ci128 Co128 n256": [("conv3x3_halo", "33554432"), ("conv3x3_gn_pt", "hi")],

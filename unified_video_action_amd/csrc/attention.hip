@@ -30,7 +30,7 @@
 // gives only 640 FLOP per atomic byte, so the 0.8 GB of dQ adds per layer ran at the chip's
 // atomic rate (+0.28 ms per layer), more than the recomputed S/dP of the dQ kernel costs.
 // The dropout scale dsc = 1 / (1 - p) never enters the loops: they run on the unscaled dO with
-// D' = rowsum(dO * O) / dsc from the pre kernel (dS = dsc P (keep dP - D')), and dsc multiplies dK,
+// D' = rowsum(dO * O) / dsc formed by the dQ kernel, which runs first (dS = dsc P (keep dP - D')), and dsc multiplies dK,
 // dQ and dV once when they are stored.
 #include "common.h"
 
@@ -421,36 +421,6 @@ __global__ __launch_bounds__(256, OCC) void attn_fwd_kernel(const bf16* __restri
 }
 
 // =====================================================================================
-// backward prologue: D'[bh][q] = dmul * sum_d dO*O (dmul = 1 / dsc when dropping: the loops run on the
-// unscaled dO, see uva_attn_bwd).  8 lanes per (b, q, h) row of 64, 16-B loads.
-// =====================================================================================
-__global__ __launch_bounds__(256) void attn_bwd_pre_kernel(const bf16* __restrict__ out, const bf16* __restrict__ dout,
-                                                           float* __restrict__ Dvec, long long rows, int N, int H,
-                                                           float dmul) {
-  const long long t = (long long)blockIdx.x * 256 + threadIdx.x;
-  const long long row = t >> 3;  // (b*N + q)*H + h
-  const int sub = threadIdx.x & 7;
-  const bool ok = row < rows;
-  float v = 0.f;
-  if (ok) {
-    const long long e = row * 64 + sub * 8;
-    const bf16x8 o = *(const bf16x8*)(out + e);
-    const bf16x8 d = *(const bf16x8*)(dout + e);
-#pragma unroll
-    for (int j = 0; j < 8; ++j) v += (float)o[j] * (float)d[j];
-  }
-  v += __shfl_xor(v, 1, 64);
-  v += __shfl_xor(v, 2, 64);
-  v += __shfl_xor(v, 4, 64);
-  if (ok && sub == 0) {
-    const int h = (int)(row % H);
-    const long long bq = row / H;
-    const long long b = bq / N, q = bq % N;
-    Dvec[(b * H + h) * N + q] = v * dmul;
-  }
-}
-
-// =====================================================================================
 // backward dK, dV (block = 4 waves x 32 keys, sweeps all 64-query tiles)
 //   lane view of S / dP / Pd / dS: q = qt*16 + 4g + r, key = k0 + kt*16 + li
 // =====================================================================================
@@ -700,11 +670,16 @@ template <bool DROP>
 #ifndef UVA_ATT_DQ_OCC
 #define UVA_ATT_DQ_OCC 2
 #endif
+// D' = dmul * rowsum(dO * O) is formed here for the block's own queries (the lanes of a query hold
+// its 64 dO / O values in four 16-element runs: two permlane-free shuffles) and written to Dvec for the
+// dK / dV kernel that runs after this one: no separate prologue pass (its 2 x 25 MB per layer of dO / O
+// reads and launch), O read once more here instead.
 __global__ __launch_bounds__(256, UVA_ATT_DQ_OCC) void attn_bwd_dq_kernel(const bf16* __restrict__ qkv, const bf16* __restrict__ dOs,
+                                                             const bf16* __restrict__ Os,
                                                              const float* __restrict__ lse2,
-                                                             const float* __restrict__ Dvec,
+                                                             float* __restrict__ Dvec,
                                                              const uint64_t* __restrict__ MQ, bf16* __restrict__ dqkv,
-                                                             int N, int H, float scale, float c) {
+                                                             int N, int H, float scale, float c, float dmul) {
   __shared__ __attribute__((aligned(16))) bf16 sK[2][AT_TILE];
   __shared__ __attribute__((aligned(16))) bf16 sV[2][AT_TILE];
   int bx, bh;
@@ -715,6 +690,7 @@ __global__ __launch_bounds__(256, UVA_ATT_DQ_OCC) void attn_bwd_dq_kernel(const 
   const bf16* Kg = Qg + H * 64;
   const bf16* Vg = Qg + 2 * H * 64;
   const bf16* dOg = dOs + (long long)b * N * ldo + h * 64;
+  const bf16* Og = Os + (long long)b * N * ldo + h * 64;
   const int w = threadIdx.x >> 6, l = threadIdx.x & 63, g = l >> 4, li = l & 15;
   const int q0 = bx * 128 + w * 32;
   const int nkv = N / 64;
@@ -727,13 +703,20 @@ __global__ __launch_bounds__(256, UVA_ATT_DQ_OCC) void attn_bwd_dq_kernel(const 
   for (int qt = 0; qt < 2; ++qt) {
     const int row = q0 + qt * 16 + li;
     const bool ok = row < N;
+    float dsum = 0.f;
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
       qf[qt][ks] = ok ? *(const bf16x8*)(Qg + (long long)row * ld + ks * 32 + 8 * g) : (bf16x8){};
       of[qt][ks] = ok ? *(const bf16x8*)(dOg + (long long)row * ldo + ks * 32 + 8 * g) : (bf16x8){};
+      const bf16x8 ov = ok ? *(const bf16x8*)(Og + (long long)row * ldo + ks * 32 + 8 * g) : (bf16x8){};
+#pragma unroll
+      for (int j = 0; j < 8; ++j) dsum += (float)ov[j] * (float)of[qt][ks][j];
     }
+    dsum += __shfl_xor(dsum, 16, 64);
+    dsum += __shfl_xor(dsum, 32, 64);
+    Dq[qt] = ok ? dsum * dmul : 0.f;
+    if (ok && g == 0) Dvec[(long long)bh * N + row] = Dq[qt];
     L[qt] = ok ? lse2[(long long)bh * N + row] : 0.f;
-    Dq[qt] = ok ? Dvec[(long long)bh * N + row] : 0.f;
     if (DROP) mw[qt] = ok ? mq[(long long)row * 4 + g] : 0u;
   }
   f32x4 dq[4][2];
@@ -952,8 +935,7 @@ extern "C" int uva_attn_bwd(const void* qkv, const void* out, const void* dout, 
   // i.e. the loops run on the unscaled dO with D' = D / dsc, and dsc goes on dK, dQ, dV once at the
   // end (no scaled dO copy: one [B N H 64] bf16 write + its re-reads per layer saved)
   (void)workspace;
-  attn_bwd_pre_kernel<<<(unsigned)((rows * 8 + 255) / 256), 256, 0, s>>>((const bf16*)out, (const bf16*)dout, Dvec,
-                                                                         rows, N, H, 1.0f / ds);
+  (void)rows;
   const int nt = N / 64;
   const uint64_t* MQ = (const uint64_t*)mask;
   const uint64_t* MK = drop ? MQ + (long long)B * H * N * nt : nullptr;
@@ -961,14 +943,17 @@ extern "C" int uva_attn_bwd(const void* qkv, const void* out, const void* dout, 
   dim3 grid((N + 127) / 128, B * H);
   const float c = scale * 1.4426950408889634f;
   const float sk = scale * ds;
+  // dQ first: it forms D' (= rowsum(dO O) / dsc) for its queries and writes Dvec, which dK / dV reads
+  const bf16* O = (const bf16*)out;
   if (drop) {
+    attn_bwd_dq_kernel<true><<<grid, 256, 0, s>>>((const bf16*)qkv, dO, O, lse2, Dvec, MQ, (bf16*)dqkv, N, H, sk, c,
+                                                  1.0f / ds);
     attn_bwd_dkdv_kernel<true><<<grid, 256, 0, s>>>((const bf16*)qkv, dO, lse2, Dvec, MK, (bf16*)dqkv, N, H, sk, c, ds);
-    attn_bwd_dq_kernel<true><<<grid, 256, 0, s>>>((const bf16*)qkv, dO, lse2, Dvec, MQ, (bf16*)dqkv, N, H, sk, c);
   } else {
+    attn_bwd_dq_kernel<false><<<grid, 256, 0, s>>>((const bf16*)qkv, dO, O, lse2, Dvec, nullptr, (bf16*)dqkv, N, H,
+                                                   sk, c, 1.0f);
     attn_bwd_dkdv_kernel<false><<<grid, 256, 0, s>>>((const bf16*)qkv, dO, lse2, Dvec, nullptr, (bf16*)dqkv, N, H,
                                                      sk, c, ds);
-    attn_bwd_dq_kernel<false><<<grid, 256, 0, s>>>((const bf16*)qkv, dO, lse2, Dvec, nullptr, (bf16*)dqkv, N, H, sk,
-                                                   c);
   }
   UVA_LAUNCH_CHECK();
   return 0;
