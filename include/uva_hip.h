@@ -283,7 +283,8 @@ int uva_attn_fwd_fp8(const void* workspace, void* out, float* lse2, const void* 
 /* ---- fused attention, head_dim 64, bf16 (timm Attention / SDPA with attn dropout,
  *      mar_con_unified.py:201-249 -> timm 0.9.7 Attention.forward, F.scaled_dot_product_attention).
  *      qkv: [B,N,3,H,64] (the qkv GEMM output), out/dout: [B,N,H,64], lse2: [B,H,N] log2-domain
- *      row log-sum-exp, Dvec: [B,H,N] scratch, dqkv: [B,N,3,H,64].  N % 64 == 0.
+ *      row log-sum-exp, Dvec: [B,H,N] scratch (D' = rowsum(dO*O)/(1-p), written by the dQ pass and read
+ *      by the dK/dV pass of uva_attn_bwd), dqkv: [B,N,3,H,64].  N % 64 == 0.
  * uva_attn_dropmask: keep-mask bit planes (uva_attn_mask_bytes bytes) of the counter-hash
  *      dropout (p, seed) -- generated once per step, consumed by fwd and bwd (drop_p > 0).
  * uva_attn_bwd: workspace of uva_attn_bwd_workspace bytes (0 in this build: the loops run on the unscaled dO;
