@@ -69,14 +69,14 @@ def parse(argv=None):
     ap.add_argument("--cpu-batch", type=int, default=2, help="CPU baseline batch (BASELINE configs[0]: 2)")
     ap.add_argument("--cpu-warmup", type=int, default=5, help="CPU warm-up steps (BASELINE.md §4: 5)")
     ap.add_argument("--cpu-steps", type=int, default=10, help="timed CPU steps, median reported (BASELINE.md §4: 10)")
-    ap.add_argument("--cpu-budget-s", type=float, default=90.0,
+    ap.add_argument("--cpu-budget-s", type=float, default=200.0,
                     help="wall budget of the B=2 leg: fewer timed steps (stated in `sample`) when a step is slow")
     ap.add_argument("--no-trace", action="store_true")
     ap.add_argument("--trace-steps", type=int, default=3)
     ap.add_argument("--cpu-threads", type=int, default=0,
                     help="0 = the host's physical cores, capped by this process's cgroup CPU quota")
-    ap.add_argument("--no-cpu-batch-gpu", action="store_true",
-                    help="skip the CPU baseline step at the config's per-GPU batch")
+    ap.add_argument("--cpu-batch-gpu", action="store_true",
+                    help="also time one CPU baseline step at the config's per-GPU batch (~3.5 min at B=32)")
     ap.add_argument("--trace-out", default="", help="write every traced kernel row (tag, launches, avg ms) here")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r05_end.json"))
     return ap.parse_args(argv)
@@ -265,7 +265,7 @@ def cpu_threads(args, info):
 def cpu_baseline(args):
     """oracle (PyTorch-CPU fp32 restatement, pinned to the reference) timed per BASELINE.md §4: all
     physical host cores (cgroup quota permitting), 5 warm-up steps + the median of 10 at BASELINE
-    configs[0]'s batch (2), then one step at the config's per-GPU batch.  The B=2 leg keeps to
+    configs[0]'s batch (2) (--cpu-batch-gpu: then one step at the config's per-GPU batch).  The B=2 leg keeps to
     --cpu-budget-s: if the warm-up shows a step too slow for 15 of them, fewer are timed (stated)."""
     import torch
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
@@ -316,7 +316,7 @@ def cpu_baseline(args):
            "sample": f"oracle/uva_oracle.py full training step (resize->KL-VAE->mar_base fwd/bwd->AdamW), "
                      f"PushT video_model, fp32, dropout 0.1, B={B}, torch.set_num_threads({th}): {proto} "
                      f"({', '.join(f'{t:.2f}' for t in ts)} s; B={B} leg {time.perf_counter() - t_start:.0f} s)"}
-    if not args.no_cpu_batch_gpu and args.batch != B:
+    if args.cpu_batch_gpu and args.batch != B:
         t = one(args.batch)  # the warm-ups above already paged in the weights and kernels
         out["per_gpu_batch"] = {"batch": args.batch, "value": round(args.batch / t, 5), "unit": "samples/s",
                                 "sample": f"one step at B={args.batch} after the B={B} runs ({t:.1f} s)"}
