@@ -196,7 +196,7 @@ def sample_rng(variant, B=B_MAR):
     """Injected draws of one sample_tokens(policy_model) call, in the reference's order:
     orders (:994), x_T (diffusion_action_loss.py:212), then one randn_like per p_sample step
     (gaussian_diffusion.py:431)."""
-    v = VARIANTS[variant]
+    v = variant_def(variant)
     tag = f"sample/{variant}"
     rows = B * 16
     return {
@@ -230,10 +230,13 @@ def video_sample_rng(variant, num_iter=VIDEO_SAMPLE_ITERS, B=B_MAR):
     action head (x_T, 100 steps) then the video head on the tokens predicted in that iteration
     (mar_con_unified.py:1026-1100; counts follow the cosine schedule, mask_by_order)."""
     import math
-    v = VARIANTS[variant]
+    v = variant_def(variant)
     tag = f"vsample/{variant}"
     r = {"orders": sample_rng(variant, B)["orders"], "act_noise": [], "act_step_noise": [],
          "video_noise": [], "video_step_noise": []}
+    wrist = bool(v.get("predict_wrist_img"))
+    if wrist:  # diffloss_wrist.sample after the video head, on the same rows (:1118-1140)
+        r["wrist_noise"], r["wrist_step_noise"] = [], []
     cur = 256
     for step in range(num_iter):
         ml = max(1.0, min(cur - 1.0, float(np.floor(256 * np.cos(math.pi / 2.0 * (step + 1) / num_iter)))))
@@ -244,6 +247,9 @@ def video_sample_rng(variant, num_iter=VIDEO_SAMPLE_ITERS, B=B_MAR):
         r["act_step_noise"].append(hash_normal(f"{tag}/{step}/asteps", (SAMPLE_STEPS, B * 16, v["Da"])))
         r["video_noise"].append(hash_normal(f"{tag}/{step}/vxT", (rows, 16)))
         r["video_step_noise"].append(hash_normal(f"{tag}/{step}/vsteps", (SAMPLE_STEPS, rows, 16)))
+        if wrist:
+            r["wrist_noise"].append(hash_normal(f"{tag}/{step}/wxT", (rows, 16)))
+            r["wrist_step_noise"].append(hash_normal(f"{tag}/{step}/wsteps", (SAMPLE_STEPS, rows, 16)))
     return r
 
 

@@ -528,6 +528,53 @@ def gen_video_sample():
     np.savez(os.path.join(OUT, "g5_video_sample.npz"), **out)
 
 
+def gen_video_sample_wrist():
+    """sample_tokens(video_model) of the reference with the wrist-camera video stream
+    (predict_wrist_img, toolhang_wrist): every MaskGIT iteration samples diffloss_wrist on the same
+    rows as the video head and writes them into pred_second_image_z (:1118-1140); the call returns the
+    unpatchified wrist tokens (:1143-1157).  Draws injected in the reference's order per iteration:
+    action head, video head, wrist head (cases.video_sample_rng)."""
+    variant = "toolhang_wrist"
+    m = build_mar(variant)
+    m.eval()
+    inp = {k: torch.from_numpy(x) for k, x in cases.mar_inputs(variant).items()}
+    rng = cases.video_sample_rng(variant)
+    q_randn, q_like = [], []
+    for i in range(cases.VIDEO_SAMPLE_ITERS):
+        q_randn += [torch.from_numpy(rng["act_noise"][i]), torch.from_numpy(rng["video_noise"][i]),
+                    torch.from_numpy(rng["wrist_noise"][i])]
+        q_like += [torch.from_numpy(a) for a in rng["act_step_noise"][i]]
+        q_like += [torch.from_numpy(a) for a in rng["video_step_noise"][i]]
+        q_like += [torch.from_numpy(a) for a in rng["wrist_step_noise"][i]]
+    saved = (torch.randn, torch.randn_like, torch.Tensor.cuda, ref_mar.MAR.sample_orders)
+
+    def fake_randn(*shape, **k):
+        v = q_randn.pop(0)
+        assert tuple(shape) == tuple(v.shape), (shape, v.shape)
+        return v
+
+    def fake_randn_like(x, *a, **k):
+        v = q_like.pop(0)
+        assert v.shape == x.shape, (v.shape, x.shape)
+        return v.to(x.dtype)
+
+    torch.randn, torch.randn_like = fake_randn, fake_randn_like
+    torch.Tensor.cuda = lambda self, *a, **k: self
+    ref_mar.MAR.sample_orders = lambda self, bsz: torch.from_numpy(rng["orders"])
+    prop = {k: inp[k] for k in inp if k.startswith(("robot0_", "second_image")) and not k.endswith("_pred")}
+    try:
+        tok, act = m.sample_tokens(bsz=cases.B_MAR, cond=inp["c"], text_latents=None,
+                                   num_iter=cases.VIDEO_SAMPLE_ITERS, cfg=1.0,
+                                   temperature=cases.SAMPLE_TEMPERATURE, task_mode="video_model",
+                                   proprioception_input=prop)
+    finally:
+        torch.randn, torch.randn_like, torch.Tensor.cuda, ref_mar.MAR.sample_orders = saved
+    assert not q_randn and not q_like, "unconsumed draws"
+    out = {f"{variant}_wrist_tokens": tok.detach().float().numpy(), f"{variant}_act": act.detach().float().numpy()}
+    print(f"video sample {variant}: wrist tokens {tuple(tok.shape)} sum={tok.sum().item():.5f}")
+    np.savez(os.path.join(OUT, "g5_video_sample_wrist.npz"), **out)
+
+
 def gen_predict():
     """UnifiedVideoActionPolicy.predict_action (policy:221-320) of the reference, eval mode, on the
     golden PushT policy (full KL-VAE, reduced MAR), draws injected (cases.predict_rng)."""

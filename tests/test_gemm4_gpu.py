@@ -194,3 +194,24 @@ def test_gemm4_dw_strided_operands():
     ref = 0.5 * (A[:, :M].float().t() @ B[:, :N].float())
     assert rel_err(C[:, :N], ref) < 5e-3
     assert (C[:, N:] == 0).all()
+
+
+@pytest.mark.parametrize("odt", [torch.float32, torch.bfloat16])
+def test_gemm4_output_past_descriptor_range(odt):
+    """an output just past the 0x7fff0000-byte store-descriptor range (fp32: M = 699136 rows of 768;
+    bf16: 1398272 rows) leaves gemm_4w (its 32-bit store offsets) for gemm_8ph: the rows at the very
+    end are written and correct (they used to be dropped by the range check)"""
+    from unified_video_action_amd.native import ops
+    N, K = 768, 256
+    M = 699136 if odt == torch.float32 else 1398272
+    assert M * N * (4 if odt == torch.float32 else 2) > 0x7FFF0000
+    a = torch.randn(M, K, device=DEV).to(torch.bfloat16)
+    w = torch.randn(N, K, device=DEV).to(torch.bfloat16)
+    out = torch.full((M, N), float("nan"), device=DEV, dtype=odt)
+    ops.linear(a, w, out)
+    for rows in (slice(0, 512), slice(M // 2, M // 2 + 512), slice(M - 512, M)):
+        ref = a[rows].float() @ w.float().t()
+        assert torch.isfinite(out[rows]).all()
+        assert rel_err(out[rows].float(), ref) < (1e-2 if odt == torch.bfloat16 else 5e-3)
+    del a, out
+    torch.cuda.empty_cache()

@@ -493,7 +493,11 @@ extern "C" int uva_gemm4_try(int out_dtype, const void* A, const void* B, void* 
   if (M <= 0 || N <= 0 || K <= 0) return 0;
   if (lda % 8 || ldb % 8 || ldc % 8 || N % 8 || lda < K || ldb < K) return 0;
   if (((uintptr_t)A | (uintptr_t)B | (uintptr_t)C) % 16) return 0;
-  if (2.0 * (double)M * (double)lda >= 4.0e9 || 2.0 * (double)N * (double)ldb >= 4.0e9) return 0;
+  // every byte offset the kernel forms (operand origins, lane offsets, the K-step soffset, the C store
+  // offset) is a 32-bit int and the C descriptor's range is clamped to 0x7fff0000: larger operands or
+  // outputs go to gemm_8ph
+  if (2.0 * (double)M * (double)lda >= 2147483648.0 || 2.0 * (double)N * (double)ldb >= 2147483648.0) return 0;
+  if ((double)M * (double)ldc * (out_dtype == UVA_DT_BF16 ? 2.0 : 4.0) > (double)0x7fff0000) return 0;
   if (bias && ((uintptr_t)bias % 16)) return 0;
   const G4Choice c = g4_plan(M, N, K);
   if (c.cfg < 0) return 0;
@@ -553,9 +557,13 @@ extern "C" int uva_gemm4_tt_try(const void* A, const void* B, float* C, int M, i
   if (M <= 0 || N <= 0 || K <= 0) return 0;
   if (lda % 8 || ldb % 8 || ldc % 8 || M % 8 || N % 8 || lda < M || ldb < N) return 0;
   if (((uintptr_t)A | (uintptr_t)B | (uintptr_t)C | (uintptr_t)ws) % 16) return 0;
-  if (2.0 * (double)K * (double)lda >= 4.0e9 || 2.0 * (double)K * (double)ldb >= 4.0e9) return 0;
+  if (2.0 * (double)K * (double)lda >= 2147483648.0 || 2.0 * (double)K * (double)ldb >= 2147483648.0) return 0;
   const G4Split p = g4_plan_tt(M, N, K, ws ? ws_floats : 0, beta != 0.f);
   if (p.splits == 0) return 0;
+  // the C (or slab workspace) byte range must fit the store descriptor (see uva_gemm4_try)
+  if (p.splits == 1 && beta == 0.f ? (double)M * (double)ldc * 4.0 > (double)0x7fff0000
+                                   : (double)p.splits * (double)M * (double)N * 4.0 > (double)0x7fff0000)
+    return 0;
   int r;
   if (p.splits == 1 && beta == 0.f) {
     r = g4_launch<8, 6, 1, 1, float>(A, B, C, M, N, K, lda, ldb, ldc, nullptr, alpha, p.grid, 1, K, 0, s);

@@ -394,8 +394,10 @@ class MAR(nn.Module):
         if text_latents is not None and self.clip:
             text_latents = linear(text_latents.to(dev).float(), self.text_proj_cond, out_dtype=F32)
         proprioception_input = self._prop_tokens(proprioception_input)
-        if self.predict_wrist_img and task_mode != "inverse_model":
-            # (:1003-1006) the wrist stream starts from zero latents and is never sampled
+        wrist = self.predict_wrist_img and task_mode != "inverse_model"
+        if wrist:
+            # (:1003-1006) the wrist stream starts from zero latents; the video modes sample it every
+            # iteration with diffloss_wrist on the rows the video head samples (:1118-1140)
             proprioception_input["pred_second_image_z"] = torch.zeros(B, T, L, self.token_embed_dim, device=dev)
         if task_mode == "inverse_model":
             tokens = self.to_tokens(x).to(F32)
@@ -447,8 +449,17 @@ class MAR(nn.Module):
             flat = tokens.reshape(B * T * L, -1).clone()
             flat.index_copy_(0, sel, lat.to(flat.dtype))
             tokens = flat.reshape(B, T, L, -1)
-        # unpatchify (patch_size 1): [(b t), s, c] -> [(b t), c, h, w]
-        out = tokens.reshape(B * T, self.seq_h, self.seq_w, -1).permute(0, 3, 1, 2).contiguous()
+            if wrist:  # (:1118-1140) the wrist head on the same decoder rows, after the video head
+                wlat = self.diffloss_wrist.sample(zr, temperature, 1.0, text_latents=text_latents,
+                                                  noise=pick("wrist_noise", step),
+                                                  step_noise=pick("wrist_step_noise", step))
+                wflat = proprioception_input["pred_second_image_z"].reshape(B * T * L, -1).clone()
+                wflat.index_copy_(0, sel, wlat.to(wflat.dtype))
+                proprioception_input["pred_second_image_z"] = wflat.reshape(B, T, L, -1)
+        # unpatchify (patch_size 1): [(b t), s, c] -> [(b t), c, h, w]; with the wrist stream the
+        # reference returns the wrist tokens in place of the main ones (:1143-1157)
+        res = proprioception_input["pred_second_image_z"] if wrist else tokens
+        out = res.reshape(B * T, self.seq_h, self.seq_w, -1).permute(0, 3, 1, 2).contiguous()
         return out, act
 
 

@@ -27,13 +27,16 @@ def stream():
 
 
 # ---- live kernel tracing (bench.py roofline / per-step accounting): HIP events around launches ----
-TRACE = None  # dict tag -> list[(start_event, end_event, flops)] when enabled
+TRACE = None  # dict tag -> list[(start_event, end_event, flops, side_stream)] when enabled
+TRACE_ONLY = None  # optional set of tags: only those launches get events (the roofline pass)
 
 
 class _traced:
     """events around one library call on the current stream; only the outermost of nested scopes
     records, so every launch is counted once (the explicitly tagged ops carry shapes and FLOPs, every
-    other entry point is tagged by its C-ABI name through _call)"""
+    other entry point is tagged by its C-ABI name through _call).  Launches on a stream other than the
+    device's default stream (the attention keep-mask planes generated ahead on RT's side stream) are
+    marked, so per-step accounting can keep their overlapped time apart."""
     __slots__ = ("tag", "flops", "ev")
     depth = 0
 
@@ -41,7 +44,7 @@ class _traced:
         self.tag, self.flops, self.ev = tag, flops, None
 
     def __enter__(self):
-        if TRACE is not None and _traced.depth == 0:
+        if TRACE is not None and _traced.depth == 0 and (TRACE_ONLY is None or self.tag in TRACE_ONLY):
             self.ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
             self.ev[0].record()
         _traced.depth += 1
@@ -52,11 +55,15 @@ class _traced:
         if self.ev is not None:
             self.ev[1].record()
             if TRACE is not None:
-                TRACE.setdefault(self.tag, []).append((self.ev[0], self.ev[1], self.flops))
+                side = torch.cuda.current_stream() != torch.cuda.default_stream()
+                TRACE.setdefault(self.tag, []).append((self.ev[0], self.ev[1], self.flops, side))
 
 
 def _call(name, *args):
-    """lib().call under a trace scope tagged by the entry point's name (no FLOP count)"""
+    """lib().call under a trace scope tagged by the entry point's name (no FLOP count); with tracing off
+    the launch goes straight to the library (no scope object on the hot path)"""
+    if TRACE is None:
+        return lib().call(name, *args)
     with _traced(name[4:] if name.startswith("uva_") else name, 0.0):
         return lib().call(name, *args)
 

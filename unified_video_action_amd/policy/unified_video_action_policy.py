@@ -272,7 +272,7 @@ class UnifiedVideoActionPolicy(nn.Module):
             if self.use_proprioception:
                 prop = self._second_camera_prop(obs, sel, train=True)
         if self.training and dev.type == "cuda":
-            RT.prefetch_attn_masks(dev)  # attention dropout planes under the VAE encode (side stream)
+            RT.arm_attn_prefetch(dev)  # attention dropout planes under the VAE encode (side stream)
         x = vae_images(img, sel, self.vae_model.CIN_PAD)
         n_half = B * (len(sel) // 2)
         eps = rng.get("vae_eps_x")
@@ -281,6 +281,7 @@ class UnifiedVideoActionPolicy(nn.Module):
         else:
             eps = torch.randn(2 * n_half, self.vae_model.embed_dim, 16, 16, device=dev)
         tokens = self.vae_model.encode_tokens(x, eps)
+        RT.fire_attn_prefetch()  # (an encode that did not fire it)
         z = tokens[:n_half].reshape(B, -1, 256, tokens.shape[-1])
         c = tokens[n_half:].reshape(B, -1, 256, tokens.shape[-1])
         history, trajectory = get_trajectory(nactions, T_traj, self.shift_action, self.use_history_action)

@@ -32,6 +32,11 @@ class _Runtime:
         # attention dropout masks: per Block the (B, N, H, p) of its last training forward, and the
         # masks generated ahead of time on a side stream (overlapping the VAE encode)
         self.attn_prefetch = True
+        # VAE encoder level at whose start the keep-mask planes are launched on the side stream (0: before
+        # the encode).  The planes' VALU-bound kernels took CU time from the level-0 GN convs (237 us per
+        # launch under them vs 78 us alone); from level 2 on the convs are smaller
+        self.attn_prefetch_level = 2
+        self._prefetch_pending = None
         self._attn_shapes = {}
         self._attn_ready = {}
         self._side = None
@@ -68,6 +73,21 @@ class _Runtime:
     # ---- attention dropout-mask prefetch ------------------------------------------------
     def note_attn_shape(self, key, shape):
         self._attn_shapes[key] = shape
+
+    def arm_attn_prefetch(self, device):
+        """schedule prefetch_attn_masks for the VAE encode that follows: fired by the encoder at the start
+        of level attn_prefetch_level (vae/vaekl.py moments_nhwc), or right away for level 0"""
+        if self.attn_prefetch_level <= 0:
+            self.prefetch_attn_masks(device)
+        else:
+            self._prefetch_pending = device
+
+    def fire_attn_prefetch(self, level=None):
+        """launch an armed prefetch (level None: unconditionally, e.g. after an encode that had fewer levels)"""
+        dev = self._prefetch_pending
+        if dev is not None and (level is None or level >= self.attn_prefetch_level):
+            self._prefetch_pending = None
+            self.prefetch_attn_masks(dev)
 
     def prefetch_attn_masks(self, device):
         """Generate every known Block's attention keep-mask planes for this step on a side stream,

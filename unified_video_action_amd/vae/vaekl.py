@@ -280,12 +280,14 @@ class AutoencoderKL(nn.Module):
         n, H, W, _ = x.shape
         h, H, W, hs = self._conv(P, "encoder.conv_in", x, n, H, W, stats=True)
         for lvl, d in enumerate(e.down):
+            RT.fire_attn_prefetch(lvl)  # the MAR's attention keep-mask planes, armed by the policy
             for j, blk in enumerate(d.block):
                 h, hs = self._resblock(P, f"encoder.down.{lvl}.block.{j}", blk, h, hs, n, H, W)
                 if len(d.attn):
                     h, hs = self._attn(P, f"encoder.down.{lvl}.attn.{j}", d.attn[j], h, hs, n, H, W)
             if hasattr(d, "downsample"):
                 h, H, W, hs = self._conv(P, f"encoder.down.{lvl}.downsample.conv", h, n, H, W, stride=2, stats=True)
+        RT.fire_attn_prefetch()
         h, hs = self._resblock(P, "encoder.mid.block_1", e.mid.block_1, h, hs, n, H, W)
         h, hs = self._attn(P, "encoder.mid.attn_1", e.mid.attn_1, h, hs, n, H, W)
         h, hs = self._resblock(P, "encoder.mid.block_2", e.mid.block_2, h, hs, n, H, W)
