@@ -88,6 +88,33 @@ int uva_gemm_set_persist(int on);
  * eligible; uva_gemm4_plan_tt: splits | grid << 8 for a dW product with ws_floats of workspace, -1 = not
  * eligible (no device work). */
 int uva_gemm4_set(int on, int force);
+/* Persistent 8-wave GEMM (gemm8w.hip: two waves per SIMD, 64 x 96 or 64 x 64 per wave, the gemm_4w ring /
+ * DMA / substep schedule, column-major MFMA order with single-buffered B fragments) whose epilogue can be
+ * DEFERRED into the next tile's first substeps (outputs packed to bf16, one fragment row per even substep,
+ * beside the partner wave's MFMAs).
+ * uva_linear_gelu_drop: the timm Mlp fc1 forward (mar_con_unified.py:236-249, Mlp.fc1 -> GELU -> drop) in
+ *      one launch: pre_out = bf16(X W^T + b) (the GELU input the backward keeps), out = bf16(drop(gelu(pre)))
+ *      -- bit-identical to the bias-only GEMM + uva_act_drop_fwd (same counter-hash mask on the flat index).
+ * uva_linear_drop_res: Mlp.fc2 -> drop (+ the Block's residual add, :247-249): out (fp32) = R +
+ *      drop(bf16(X W^T + b)) -- bit-identical to the bias-only GEMM + uva_act_drop_fwd(residual).
+ *      Both: X [M][K], W [N][K] bf16 (K-contiguous), bias fp32 [N], contiguous outputs; 1 = launched,
+ *      0 = shape not eligible (M >= 256, N >= 192, K % 128 == 0, K >= 256, 16-B aligned), < 0 = -hipError.
+ * uva_gemm8w_try: a plain (bias) product on this kernel when switched on by uva_gemm8w_set(on, mode)
+ *      (measurement: mode bit 0 deferred epilogue, bit 1 64 x 64 wave tiles); uva_gemm routes its plain
+ *      K-contiguous products here first while on.  Returns the previous on | mode << 1; -2 keeps a value. */
+int uva_gemm8w_set(int on, int mode);
+int uva_linear_gelu_drop(const void* X, const void* W, const float* bias, void* pre_out, void* out, int M, int N, int K,
+                         float drop_p, unsigned long long seed, hipStream_t stream);
+int uva_linear_drop_res(const void* X, const void* W, const float* bias, const float* R, float* out, int M, int N,
+                        int K, float drop_p, unsigned long long seed, hipStream_t stream);
+/* uva_linear_dgelu_drop: the timm Mlp backward through fc2 -> dropout -> GELU in fc2's dX product:
+ *      dpre = bf16(gelu'(pre) * drop(bf16(dY Wt^T))) -- bit-identical to the dX GEMM + uva_act_bwd_bias --
+ *      and dbias (+)= the column sums of dpre (fc1's bias gradient: per-64-row partials in `part`,
+ *      ((M + 255) / 256) * 4 * N floats, reduced by a second launch; the sums of the same stored values in
+ *      another order than uva_act_bwd_bias).  dY [M][K], Wt [N][K] (fc2's transposed weight), pre / dpre
+ *      [M][N] bf16 (replaces autograd of mar_con_unified.py:236-249 Mlp fc1 -> GELU -> drop -> fc2). */
+int uva_linear_dgelu_drop(const void* dY, const void* Wt, const void* pre, void* dpre, float* dbias, int accum_bias,
+                          float* part, int M, int N, int K, float drop_p, unsigned long long seed, hipStream_t stream);
 long long uva_gemm4_plan(int M, int N, int K);
 long long uva_gemm4_plan_tt(int M, int N, int K, long long ws_floats);
 int uva_conv2d(int dtype, const void* in, const void* w, void* out, const float* bias, const void* residual, int Nimg,

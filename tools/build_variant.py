@@ -22,7 +22,8 @@ def main():
     out_dir = os.path.join(ROOT, "abx")
     os.makedirs(out_dir, exist_ok=True)
     obj = os.path.join(out_dir, f"{name}_{os.path.basename(src).replace('.hip', '.o')}")
-    r = subprocess.run([bn.HIPCC] + bn.FLAGS + defs + ["-c", src, "-o", obj], capture_output=True, text=True)
+    r = subprocess.run([bn.HIPCC] + bn.FLAGS + bn.EXTRA.get(os.path.basename(src), []) + defs + ["-c", src, "-o", obj],
+                       capture_output=True, text=True)
     if r.returncode:
         raise SystemExit(r.stderr)
     base = os.path.basename(src).replace(".hip", ".o")

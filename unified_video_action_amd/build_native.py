@@ -14,6 +14,12 @@ LIB = os.path.join(HERE, "libuva_hip.so")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 FLAGS = ["--offload-arch=gfx950", "-O3", "-fPIC", "-std=c++17", "-munsafe-fp-atomics",
          "-Wno-unused-result", "-I" + CSRC]
+# per-source extras.  gemm8w.hip: no SLP vectorisation -- its fused epilogues (GELU' / GELU / dropout math
+# beside the MFMA stream) came out of the SLP pass as packed v_pk_*_f32 with op_sel operand swaps, and the
+# GELU-backward form then returned intermittently wrong low halves (one element of a 16-lane row per tile in
+# ~half the launches, tools/dbg_dgelu.py; never with the pass off: 16 / 16 launches bit-exact).  The scalar
+# form is also the cheaper one beside MFMAs (MI355X_MICROARCH.md: packed f32 VALU is an anti-lever there)
+EXTRA = {"gemm8w.hip": ["-fno-slp-vectorize"]}
 
 
 def _compile(src):
@@ -21,7 +27,7 @@ def _compile(src):
     deps = [src] + glob.glob(os.path.join(CSRC, "*.h"))
     if os.path.exists(obj) and os.path.getmtime(obj) >= max(os.path.getmtime(d) for d in deps):
         return obj
-    cmd = [HIPCC] + FLAGS + ["-c", src, "-o", obj]
+    cmd = [HIPCC] + FLAGS + EXTRA.get(os.path.basename(src), []) + ["-c", src, "-o", obj]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"hipcc failed for {src}:\n{r.stderr}")

@@ -144,7 +144,9 @@ __device__ __forceinline__ float gelu_erf_grad(float x) {
   p = fmaf(p, t, 0.254829592f);
   p *= t;
   const float erf_ = copysignf(fmaf(-p, e, 1.0f), x);
-  return fmaf(0.5f, erf_, 0.5f) + x * (0.39894228040143268f * e);
+  // one explicit fma: left to the compiler, the contraction of `a + x * b` depended on the inlining
+  // context, and the fused GEMM epilogue (gemm8w.hip EPI 3) and act_bwd_colsum must give the same bits
+  return fmaf(x, 0.39894228040143268f * e, fmaf(0.5f, erf_, 0.5f));
 }
 // sigmoid as v_exp_f32 + v_rcp_f32 (1 ulp each): a plain `x / (1 + e)` compiles to the IEEE division
 // sequence (2 x v_div_scale, v_div_fmas, v_div_fixup, v_rcp + 4 FMAs) -- 3x the VALU work of the

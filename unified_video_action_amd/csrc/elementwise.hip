@@ -244,6 +244,13 @@ extern "C" int uva_act_bwd_bias(int pdt, const void* pre, int gdt, const void* d
   return 0;
 }
 
+// out[c] (+)= sum_j part[j][c] (C++ linkage, library-internal): the column-partial reduce of the fused
+// GEMM epilogues (gemm8w.hip EPI 3)
+int uva_colsum_final_launch(const float* part, int nrows, int cols, float* out, int accum, hipStream_t s) {
+  colsum_final_kernel<<<dim3((cols + 31) / 32), 256, 0, s>>>(part, nrows, cols, out, accum);
+  return (int)hipGetLastError();
+}
+
 // vectorized tall column sum (uva_colsum fast path): returns 1 if handled
 int uva_colsum_vec(int dtype, const void* in, long long ld, float* out, int rows, int cols, int accum,
                    float* workspace, hipStream_t s) {

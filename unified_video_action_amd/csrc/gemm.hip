@@ -1967,6 +1967,9 @@ static int launch_8ph(int ta, int tb, const void* A, const void* B, void* C, int
 extern "C" int uva_gemm4_try(int out_dtype, const void* A, const void* B, void* C, int M, int N, int K,
                              long long lda, long long ldb, long long ldc, const float* bias, float alpha,
                              hipStream_t s);
+extern "C" int uva_gemm8w_try(int out_dtype, const void* A, const void* B, void* C, int M, int N, int K,
+                              long long lda, long long ldb, long long ldc, const float* bias, float alpha,
+                              hipStream_t s);
 extern "C" int uva_gemm4_tt_try(const void* A, const void* B, float* C, int M, int N, int K, long long lda,
                                 long long ldb, long long ldc, float alpha, float beta, float* ws, long long ws_floats,
                                 int* reduce, hipStream_t s);
@@ -1978,8 +1981,13 @@ static int launch_mfma(int ta, int tb, const void* A, const void* B, void* C, in
   // K-contiguous products with a bias-only epilogue: the persistent 4-wave kernel (gemm4.hip)
   if (ta == 0 && tb == 0 && batch == 1 && !ep.residual && !ep.aux && !ep.gate && ep.act == 0 &&
       ep.drop_thresh == 0 && ep.beta == 0.f && ep.res_grad == 0) {
-    const int r = uva_gemm4_try(sizeof(TC) == 2 ? UVA_DT_BF16 : UVA_DT_F32, A, B, C, M, N, K, lda, ldb, ldc, ep.bias,
-                                ep.alpha, s);
+    // (the 8-wave kernel first when a measurement switch routes plain products to it)
+    int r = uva_gemm8w_try(sizeof(TC) == 2 ? UVA_DT_BF16 : UVA_DT_F32, A, B, C, M, N, K, lda, ldb, ldc, ep.bias,
+                           ep.alpha, s);
+    if (r < 0) return -r;
+    if (r > 0) return 0;
+    r = uva_gemm4_try(sizeof(TC) == 2 ? UVA_DT_BF16 : UVA_DT_F32, A, B, C, M, N, K, lda, ldb, ldc, ep.bias,
+                      ep.alpha, s);
     if (r < 0) return -r;
     if (r > 0) return 0;
   }

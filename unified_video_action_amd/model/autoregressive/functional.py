@@ -285,8 +285,13 @@ class BlockFn(torch.autograd.Function):
             o = as_dtype(o, c)
             lse = None
         x1 = torch.empty(M, D, dtype=F32, device=dev)
-        ops.linear(o, compute_weight(projw), x1, bias=projb.detach(), residual=x, drop_p=p_proj,
-                   seed=seeds[1])
+        # attention proj + proj_drop + the residual add: bf16 (autocast) output rounded before the dropout
+        # and the fp32 add, in the 8-wave GEMM's epilogue; fp32 parity mode (or an ineligible shape): the
+        # fused-epilogue GEMM of gemm.hip
+        if not (c == torch.bfloat16 and RT.proj_8w and
+                ops.linear_drop_res(o, compute_weight(projw), projb.detach(), x, x1, p_proj, seeds[1])):
+            ops.linear(o, compute_weight(projw), x1, bias=projb.detach(), residual=x, drop_p=p_proj,
+                       seed=seeds[1])
         h2 = torch.empty(M, D, dtype=c, device=dev)
         m2 = torch.empty(M, dtype=F32, device=dev)
         r2 = torch.empty(M, dtype=F32, device=dev)
@@ -295,15 +300,21 @@ class BlockFn(torch.autograd.Function):
         a = torch.empty(M, Hd, dtype=c, device=dev)
         pre1 = torch.empty(M, Hd, dtype=c, device=dev)
         x2 = torch.empty(M, D, dtype=F32, device=dev)
-        if c == torch.bfloat16 and RT.mlp_split_epilogue:
-            # bias-only GEMMs (autocast: fc1 / fc2 outputs are bf16 before GELU / dropout / the fp32
-            # residual add) + one elementwise pass each; same dropout masks (flat element index)
-            linear_bias(h2, fc1w, fc1b, pre1)
-            ops.act_drop_fwd(pre1, a, "gelu", drop_p=p_proj, seed=seeds[2])
-            t2 = torch.empty(M, D, dtype=c, device=dev)
-            linear_bias(a, fc2w, fc2b, t2)
-            ops.act_drop_fwd(t2, x2, "none", drop_p=p_proj, seed=seeds[3], residual=x1)
-            del t2
+        if c == torch.bfloat16:
+            # autocast semantics: fc1 / fc2 outputs are bf16 before GELU / dropout / the fp32 residual add.
+            # Fused (RT.mlp_split_epilogue False): the 8-wave GEMM finishes GELU + dropout (fc1) and dropout +
+            # residual (fc2) in its epilogue (csrc/gemm8w.hip); split: bias-only GEMMs + one elementwise pass
+            # each.  Both routes give the same bits (same rounding points, same flat-index dropout masks)
+            fused = not RT.mlp_split_epilogue
+            if not (fused and ops.linear_gelu_drop(h2, compute_weight(fc1w), fc1b.detach(), pre1, a, p_proj,
+                                                   seeds[2])):
+                linear_bias(h2, fc1w, fc1b, pre1)
+                ops.act_drop_fwd(pre1, a, "gelu", drop_p=p_proj, seed=seeds[2])
+            if not (fused and ops.linear_drop_res(a, compute_weight(fc2w), fc2b.detach(), x1, x2, p_proj, seeds[3])):
+                t2 = torch.empty(M, D, dtype=c, device=dev)
+                linear_bias(a, fc2w, fc2b, t2)
+                ops.act_drop_fwd(t2, x2, "none", drop_p=p_proj, seed=seeds[3], residual=x1)
+                del t2
         else:
             ops.linear(h2, compute_weight(fc1w), a, bias=fc1b.detach(), act="gelu", aux=pre1, drop_p=p_proj,
                        seed=seeds[2])
@@ -331,7 +342,12 @@ class BlockFn(torch.autograd.Function):
         Hd = fc1w.shape[0]
         # fc1 (gelu + drop1)
         dpre1 = torch.empty(M, Hd, dtype=c, device=dev)
-        if RT.act_bwd_in_gemm:
+        if c == torch.bfloat16 and RT.act_bwd_in_gemm and ops.linear_dgelu_drop(
+                dpre2, compute_weight_t(fc2w), pre1, dpre1, grad_buf(fc1b), p_proj, seeds[2]):
+            # fc2's dX product finishes dropout + GELU' in its epilogue and the fc1 bias gradient as column
+            # partials (csrc/gemm8w.hip EPI 3): no [M, 3072] round trip of dA
+            pass
+        elif RT.act_bwd_in_gemm:
             ops.linear_dx_act(dpre2, compute_weight(fc2w), dpre1, pre1, "gelu", drop_p=p_proj, seed=seeds[2])
             ops.colsum(dpre1, grad_buf(fc1b))
         else:
@@ -474,7 +490,7 @@ class AdaLNTrunkFn(torch.autograd.Function):
             ops.linear_dw(dhm2, a, grad_buf(w2))
             ops.colsum(dhm2, grad_buf(b2))
             dpre1 = torch.empty(R, W, dtype=c, device=dev)
-            if RT.act_bwd_in_gemm and pre1.dtype == c:
+            if RT.trunk_act_bwd_in_gemm and pre1.dtype == c:
                 ops.linear_dx_act(dhm2, compute_weight(w2), dpre1, pre1, "silu")
                 ops.colsum(dpre1, grad_buf(b1))
             else:

@@ -18,15 +18,21 @@ class _Runtime:
         self.vae_gn_in_conv = True
         # dX of the LayerNorm-fed GEMMs in the compute dtype (autocast semantics) instead of fp32
         self.ln_dy_lowp = True
-        # timm Mlp forward (bf16): fc1 / fc2 as bias-only GEMMs + one elementwise GELU/dropout
-        # (/residual) pass each; the fused-epilogue GEMMs (False) measured equal-to-slower: the fused
-        # fc1 epilogue's stores are not hidden at one workgroup per CU
-        self.mlp_split_epilogue = True
-        # activation (+dropout) backward of the MLPs fused into the following Linear's dX GEMM
-        # epilogue (act'(pre) * dropout(dY W)); bias grad by a column sum of the stored result.
-        # False: dX GEMM -> separate act_bwd + column-sum pass.  Measured slower (128.4 vs 125.8
-        # ms/step, same box): the epilogue is not overlapped with MFMAs; kept off, the mode tested
-        self.act_bwd_in_gemm = False
+        # timm Mlp forward (bf16).  False: fc1 + GELU + dropout and fc2 + dropout + fp32 residual each in ONE
+        # launch of the 8-wave GEMM (csrc/gemm8w.hip: two waves per SIMD, so one wave's epilogue runs beside
+        # its partner's MFMAs).  True: bias-only GEMMs + one elementwise pass each (the route rounds 1-5
+        # kept: at one wave per SIMD the fused epilogue was not hidden).  Same bits either way.
+        self.mlp_split_epilogue = False
+        # attention proj + proj_drop + residual (bf16) on the 8-wave GEMM's epilogue (the bf16 rounding of the
+        # proj output before the dropout and the fp32 residual add, as autocast) instead of gemm_8ph's fused
+        # epilogue (which kept the fp32 accumulator): 59-62 vs 72-75 us at B32 (profiles/r06/g8w_fused.txt)
+        self.proj_8w = True
+        # Mlp backward: dropout + GELU' (+ the fc1 bias gradient) in the epilogue of fc2's dX product (8-wave
+        # GEMM, EPI 3) instead of dX GEMM -> act_bwd_bias (one [M, 3072] bf16 round trip less per Block)
+        self.act_bwd_in_gemm = True
+        # the same for the DiffLoss SimpleMLPAdaLN trunk (SiLU, W = 1024) on gemm_8ph's dX epilogue: measured
+        # slower there (128.4 vs 125.8 ms/step, one wave per SIMD); kept off, the mode tested
+        self.trunk_act_bwd_in_gemm = False
         self._seed_base = 0x5EED
         self._ctr = itertools.count()
         # attention dropout masks: per Block the (B, N, H, p) of its last training forward, and the
