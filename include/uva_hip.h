@@ -104,9 +104,9 @@ int uva_gemm4_set(int on, int force);
  *      K-contiguous products here first while on.  Returns the previous on | mode << 1; -2 keeps a value. */
 int uva_gemm8w_set(int on, int mode);
 int uva_linear_gelu_drop(const void* X, const void* W, const float* bias, void* pre_out, void* out, int M, int N, int K,
-                         float drop_p, unsigned long long seed, hipStream_t stream);
+                         float drop_p, unsigned long long seed, const void* plane, hipStream_t stream);
 int uva_linear_drop_res(const void* X, const void* W, const float* bias, const float* R, float* out, int M, int N,
-                        int K, float drop_p, unsigned long long seed, hipStream_t stream);
+                        int K, float drop_p, unsigned long long seed, const void* plane, hipStream_t stream);
 /* uva_linear_dgelu_drop: the timm Mlp backward through fc2 -> dropout -> GELU in fc2's dX product:
  *      dpre = bf16(gelu'(pre) * drop(bf16(dY Wt^T))) -- bit-identical to the dX GEMM + uva_act_bwd_bias --
  *      and dbias (+)= the column sums of dpre (fc1's bias gradient: per-64-row partials in `part`,
@@ -114,7 +114,15 @@ int uva_linear_drop_res(const void* X, const void* W, const float* bias, const f
  *      another order than uva_act_bwd_bias).  dY [M][K], Wt [N][K] (fc2's transposed weight), pre / dpre
  *      [M][N] bf16 (replaces autograd of mar_con_unified.py:236-249 Mlp fc1 -> GELU -> drop -> fc2). */
 int uva_linear_dgelu_drop(const void* dY, const void* Wt, const void* pre, void* dpre, float* dbias, int accum_bias,
-                          float* part, int M, int N, int K, float drop_p, unsigned long long seed, hipStream_t stream);
+                          float* part, int M, int N, int K, float drop_p, unsigned long long seed, const void* plane,
+                          hipStream_t stream);
+/* Dropout keep-bit planes: bit (i & 31) of u32 word i >> 5 = keep decision of flat element i under (drop_p,
+ * seed) -- the same counter-hash mask every dropout kernel here evaluates (common.h dropout_keep).  The
+ * fused Mlp GEMMs above take one as `plane` (non-null: test a bit instead of hashing per element in the
+ * epilogue; N % 32 == 0, drop_p > 0), so the mask of a Block's fc1 / fc2 / proj dropout is computed once per
+ * step, off the GEMMs (mar_con_unified.py:236-249 Mlp.drop, :201-215 proj_drop).  words = ceil(n / 32). */
+long long uva_dropout_plane_words(long long n);
+int uva_dropout_plane(void* plane, long long n, float drop_p, unsigned long long seed, hipStream_t stream);
 long long uva_gemm4_plan(int M, int N, int K);
 long long uva_gemm4_plan_tt(int M, int N, int K, long long ws_floats);
 int uva_conv2d(int dtype, const void* in, const void* w, void* out, const float* bias, const void* residual, int Nimg,

@@ -162,3 +162,51 @@ def test_block_fused_routes_match_split_routes():
             assert (gf[n] - gs[n]).abs().max().item() <= 1e-5 * gs[n].abs().max().item(), n
         else:
             assert torch.equal(gf[n], gs[n]), n
+
+
+@pytest.mark.parametrize("n", [32 * 1000, 32768 * 768, 70])
+def test_dropout_plane_matches_counter_hash(n):
+    """keep-bit plane (uva_dropout_plane) == the mask act_drop_fwd applies (flat index, same seed)"""
+    from unified_video_action_amd.native import ops
+    p, seed = 0.1, 0xABCDEF12345
+    plane = ops.dropout_plane(n, p, seed, DEV)
+    ones = torch.ones(((n + 7) // 8) * 8, device=DEV, dtype=torch.bfloat16)
+    y = torch.empty_like(ones)
+    ops.act_drop_fwd(ones, y, "none", drop_p=p, seed=seed)
+    keep = (y[:n] != 0)
+    bits = ((plane.view(-1, 1) >> torch.arange(32, device=DEV, dtype=torch.int32).view(1, 32)) & 1).reshape(-1)[:n]
+    assert torch.equal(bits.bool(), keep)
+
+
+@pytest.mark.parametrize("which", ["fc1", "fc2", "dgelu"])
+@pytest.mark.parametrize("M,N,K", [(32768, 3072, 768), (1000, 768, 384)])
+def test_fused_with_plane_bit_exact_vs_hash(which, M, N, K):
+    """the fused epilogues reading a precomputed keep-bit plane give the same bits as evaluating the hash"""
+    from unified_video_action_amd.native import ops
+    p, seed = 0.1, 4242
+    g = torch.Generator(device=DEV).manual_seed(M + N)
+    plane = ops.dropout_plane(M * N, p, seed, DEV)
+    if which == "fc1":
+        x, w = _rand(M, K, g=g), _rand(N, K, 0.1, g=g)
+        b = torch.rand(N, device=DEV, generator=g) * 0.1
+        pa, aa = torch.empty(M, N, device=DEV, dtype=torch.bfloat16), torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+        pb, ab = torch.empty_like(pa), torch.empty_like(aa)
+        assert ops.linear_gelu_drop(x, w, b, pa, aa, drop_p=p, seed=seed)
+        assert ops.linear_gelu_drop(x, w, b, pb, ab, drop_p=p, seed=seed, plane=plane)
+        assert torch.equal(pa, pb) and torch.equal(aa, ab)
+    elif which == "fc2":
+        x, w = _rand(M, K, g=g), _rand(N, K, 0.1, g=g)
+        b = torch.rand(N, device=DEV, generator=g) * 0.1
+        r = torch.randn(M, N, device=DEV, generator=g)
+        oa, ob = torch.empty(M, N, device=DEV), torch.empty(M, N, device=DEV)
+        assert ops.linear_drop_res(x, w, b, r, oa, drop_p=p, seed=seed)
+        assert ops.linear_drop_res(x, w, b, r, ob, drop_p=p, seed=seed, plane=plane)
+        assert torch.equal(oa, ob)
+    else:
+        dy, wt = (torch.randn(M, K, device=DEV, generator=g) * 0.1).to(torch.bfloat16), _rand(N, K, 0.05, g=g)
+        pre = (torch.randn(M, N, device=DEV, generator=g) * 1.5).to(torch.bfloat16)
+        da, db = torch.empty(M, N, device=DEV, dtype=torch.bfloat16), torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+        ga, gb = torch.zeros(N, device=DEV), torch.zeros(N, device=DEV)
+        assert ops.linear_dgelu_drop(dy, wt, pre, da, ga, drop_p=p, seed=seed)
+        assert ops.linear_dgelu_drop(dy, wt, pre, db, gb, drop_p=p, seed=seed, plane=plane)
+        assert torch.equal(da, db) and torch.equal(ga, gb)

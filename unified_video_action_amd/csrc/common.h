@@ -55,7 +55,7 @@ __device__ __forceinline__ float group16_max(float v) {
 // lowbias32 finalizer: 2 x v_mul_lo_u32, no 64-bit multiplies) yields two 16-bit uniforms:
 // low half -> even idx, high half -> odd idx.
 // keep iff u16 >= thresh, thresh = round(p * 65536); kept values scale by 65536 / (65536 - thresh).
-__device__ __forceinline__ uint32_t drop_key(uint64_t seed) {
+__host__ __device__ __forceinline__ uint32_t drop_key(uint64_t seed) {
   uint32_t k = (uint32_t)seed ^ (((uint32_t)(seed >> 32)) * 0x9E3779B1u);
   k ^= k >> 16;
   k *= 0x7feb352du;

@@ -411,6 +411,42 @@ extern "C" int uva_act_drop_fwd(int xdt, const void* x, int ydt, void* y, int rd
   return 0;
 }
 
+// ---- dropout keep-bit planes --------------------------------------------------------------
+// bit (i & 31) of word i >> 5 = the keep decision of flat element i (dropout_keep: the counter hash of pair
+// i >> 1, low half for even i, high half for odd): the mask every dropout kernel of this library derives
+// from (seed, flat index), precomputed once so that the GEMM epilogues that apply it (gemm8w.hip: fc1 GELU +
+// dropout forward, the fused GELU'-backward, fc2 / proj dropout + residual) test a bit instead of hashing.
+// One word per thread: 16 pair hashes whose first words differ only in their low 4 bits (drop_first of a
+// 16-aligned pair base, xor j)
+__global__ __launch_bounds__(256) void drop_plane_kernel(uint32_t* __restrict__ plane, long long nwords, uint32_t key,
+                                                         uint32_t thresh) {
+  GRID_STRIDE(w, nwords) {
+    const uint32_t f0 = drop_first(key, (uint64_t)w * 16);
+    uint32_t bits = 0;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      const uint32_t h = drop_mix(f0 ^ (uint32_t)j);
+      bits |= ((h & 0xFFFFu) >= thresh ? 1u : 0u) << (2 * j);
+      bits |= ((h >> 16) >= thresh ? 1u : 0u) << (2 * j + 1);
+    }
+    plane[w] = bits;
+  }
+}
+
+extern "C" long long uva_dropout_plane_words(long long n) { return (n + 31) / 32; }
+
+extern "C" int uva_dropout_plane(void* plane, long long n, float drop_p, unsigned long long seed, hipStream_t s) {
+  if (n <= 0) return 0;
+  if (!plane || ((uintptr_t)plane % 4)) return (int)hipErrorInvalidValue;
+  uint32_t th;
+  float ds;
+  uva_drop_params(drop_p, &th, &ds);
+  const long long nw = (n + 31) / 32;
+  drop_plane_kernel<<<ew_grid(nw), 256, 0, s>>>((uint32_t*)plane, nw, drop_key(seed), th);
+  UVA_LAUNCH_CHECK();
+  return 0;
+}
+
 extern "C" int uva_act_fwd(int xdt, const void* x, int ydt, void* y, long long n, int act, hipStream_t s) {
   if (n <= 0) return 0;
   act_fwd_kernel<<<ew_grid(n), 256, 0, s>>>(x, xdt, y, ydt, n, act);

@@ -66,6 +66,8 @@ struct G8Epi {
   void* C2;              // EPI 1: the pre-activation (bf16, ldc)
   const float* R;        // EPI 2: fp32 residual (ldc)
   float* part;           // EPI 3: column-sum partials [tm * 4][N]
+  const uint32_t* plane; // dropout keep bits of the [M][N] output (elementwise.hip drop_plane_kernel), or null:
+                         // then the counter hash (key, thresh) is evaluated per element
   uint32_t key;          // dropout: drop_key(seed)
   uint32_t thresh;       // 0 = no dropout
   float dscale;
@@ -179,6 +181,15 @@ __global__ __launch_bounds__(64 * NW, 1) void gemm_8w(const bf16* __restrict__ A
                                                      (int)(unsigned)((EPI == 1 || EPI == 3) ? 2ull * M * ldc : cbytes),
                                                      0x00020000);
   float cs[EPI == 3 ? FN / 2 : 1][8];  // EPI 3: the lane's column sums over its fragment rows
+  const bool use_plane = EPI != 0 && ep.plane != nullptr;
+  const auto rsK = __builtin_amdgcn_make_buffer_rsrc((void*)(use_plane ? ep.plane : (const uint32_t*)C), 0,
+                                                     (int)(unsigned)(use_plane ? (unsigned long long)M * N / 8 : 4ull),
+                                                     0x00020000);
+  // the 8 keep bits of a lane's segment (row, 8 columns from col, col % 8 == 0; N % 32 == 0 with a plane)
+  auto keep8 = [&](bool ok, int row, int col) __attribute__((always_inline)) -> uint32_t {
+    const int koff = ok ? ((row * N + (col & ~31)) >> 5) * 4 : 0x7fff8000;
+    return (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(rsK, koff, 0, 0) >> (col & 31);
+  };
   const auto rsR = __builtin_amdgcn_make_buffer_rsrc(EPI == 2 ? (void*)ep.R : (void*)C, 0, (int)(unsigned)cbytes,
                                                      0x00020000);
   // (acc row f, pair p) -> 8 consecutive fp32 values of one output row: v[e] = alpha * acc + bias
@@ -216,13 +227,17 @@ __global__ __launch_bounds__(64 * NW, 1) void gemm_8w(const bf16* __restrict__ A
     } else if constexpr (EPI == 1) {
       // P stored; GELU + dropout on the bf16 P (autocast: fc1's output is bf16 before the activation)
       const int poff = ok ? (row * ldc + col) * 2 : 0x7fff8000;
+      const uint32_t kb = use_plane ? keep8(ok, row, col) : 0u;
       __builtin_amdgcn_raw_buffer_store_b128((u32x4){pk[0], pk[1], pk[2], pk[3]}, rsP, poff, 0, 0);
       const unsigned long long idx0 = (unsigned long long)row * (unsigned)N + (unsigned)col;  // flat index (even)
       uint32_t o[4];
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         float a0 = gelu_erf(bf_lo(pk[j])), a1 = gelu_erf(bf_hi(pk[j]));
-        if (ep.thresh) {
+        if (use_plane) {
+          a0 = (kb >> (2 * j)) & 1u ? a0 * ep.dscale : 0.f;
+          a1 = (kb >> (2 * j + 1)) & 1u ? a1 * ep.dscale : 0.f;
+        } else if (ep.thresh) {
           const uint32_t h = drop_hash(ep.key, (idx0 >> 1) + j);
           a0 = (h & 0xFFFFu) >= ep.thresh ? a0 * ep.dscale : 0.f;
           a1 = (h >> 16) >= ep.thresh ? a1 * ep.dscale : 0.f;
@@ -234,12 +249,16 @@ __global__ __launch_bounds__(64 * NW, 1) void gemm_8w(const bf16* __restrict__ A
       // dA (bf16) -> dropout -> x GELU'(P) -> bf16; column sums of the stored values
       const int poff = ok ? (row * ldc + col) * 2 : 0x7fff8000;
       const u32x4 pp = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rsP, poff, 0, 0));
+      const uint32_t kb = use_plane ? keep8(ok, row, col) : 0u;
       const unsigned long long idx0 = (unsigned long long)row * (unsigned)N + (unsigned)col;
       uint32_t o[4];
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         float d0 = bf_lo(pk[j]), d1 = bf_hi(pk[j]);
-        if (ep.thresh) {
+        if (use_plane) {
+          d0 = (kb >> (2 * j)) & 1u ? d0 * ep.dscale : 0.f;
+          d1 = (kb >> (2 * j + 1)) & 1u ? d1 * ep.dscale : 0.f;
+        } else if (ep.thresh) {
           const uint32_t h = drop_hash(ep.key, (idx0 >> 1) + j);
           d0 = (h & 0xFFFFu) >= ep.thresh ? d0 * ep.dscale : 0.f;
           d1 = (h >> 16) >= ep.thresh ? d1 * ep.dscale : 0.f;
@@ -253,12 +272,16 @@ __global__ __launch_bounds__(64 * NW, 1) void gemm_8w(const bf16* __restrict__ A
     } else {
       const f32x4 r0 = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rsR, voff, 0, 0));
       const f32x4 r1 = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rsR, voff + 16, 0, 0));
+      const uint32_t kb = use_plane ? keep8(ok, row, col) : 0u;
       const unsigned long long idx0 = (unsigned long long)row * (unsigned)N + (unsigned)col;
       float o[8];
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         float a0 = bf_lo(pk[j]), a1 = bf_hi(pk[j]);
-        if (ep.thresh) {
+        if (use_plane) {
+          a0 = (kb >> (2 * j)) & 1u ? a0 * ep.dscale : 0.f;
+          a1 = (kb >> (2 * j + 1)) & 1u ? a1 * ep.dscale : 0.f;
+        } else if (ep.thresh) {
           const uint32_t h = drop_hash(ep.key, (idx0 >> 1) + j);
           a0 = (h & 0xFFFFu) >= ep.thresh ? a0 * ep.dscale : 0.f;
           a1 = (h >> 16) >= ep.thresh ? a1 * ep.dscale : 0.f;
@@ -546,20 +569,14 @@ static bool g8_ok(const void* A, const void* B, const void* C, int M, int N, int
   return true;
 }
 
-static uint32_t g8_key(unsigned long long seed) {  // drop_key (common.h) on the host
-  uint32_t k = (uint32_t)seed ^ (((uint32_t)(seed >> 32)) * 0x9E3779B1u);
-  k ^= k >> 16;
-  k *= 0x7feb352du;
-  k ^= k >> 15;
-  return k;
-}
+static uint32_t g8_key(unsigned long long seed) { return drop_key(seed); }
 
 // plain product (measurement route): 1 = launched, 0 = not eligible / off, < 0 = -hipError
 extern "C" int uva_gemm8w_try(int out_dtype, const void* A, const void* B, void* C, int M, int N, int K, long long lda,
                               long long ldb, long long ldc, const float* bias, float alpha, hipStream_t s) {
   if (!g_gemm8w_on) return 0;
   if (!g8_ok(A, B, C, M, N, K, lda, ldb, ldc, out_dtype == UVA_DT_BF16 ? 2 : 4, bias)) return 0;
-  G8Epi ep{bias, alpha, nullptr, nullptr, nullptr, 0u, 0u, 1.f};
+  G8Epi ep{bias, alpha, nullptr, nullptr, nullptr, nullptr, 0u, 0u, 1.f};
   const int r = out_dtype == UVA_DT_BF16
                     ? g8_dispatch<0, bf16>(A, B, C, M, N, K, (int)lda, (int)ldb, (int)ldc, ep, s)
                     : g8_dispatch<0, float>(A, B, C, M, N, K, (int)lda, (int)ldb, (int)ldc, ep, s);
@@ -578,12 +595,14 @@ extern "C" int uva_gemm8w_set(int on, int mode) {
 // timm Mlp fc1 forward, fused: pre = bf16(x W^T + b) -> pre_out; out = bf16(drop(gelu(pre))).
 // 1 = launched, 0 = not eligible, < 0 = -hipError
 extern "C" int uva_linear_gelu_drop(const void* X, const void* W, const float* bias, void* pre_out, void* out, int M,
-                                    int N, int K, float drop_p, unsigned long long seed, hipStream_t s) {
+                                    int N, int K, float drop_p, unsigned long long seed, const void* plane,
+                                    hipStream_t s) {
   if (!g8_ok(X, W, out, M, N, K, K, K, N, 2, bias) || ((uintptr_t)pre_out % 16)) return 0;
   uint32_t th;
   float ds;
   uva_drop_params(drop_p, &th, &ds);
-  G8Epi ep{bias, 1.f, pre_out, nullptr, nullptr, th ? g8_key(seed) : 0u, th, ds};
+  if (plane && (N % 32 || !th || ((uintptr_t)plane % 4))) return (int)-hipErrorInvalidValue;
+  G8Epi ep{bias, 1.f, pre_out, nullptr, nullptr, (const uint32_t*)plane, th ? g8_key(seed) : 0u, th, ds};
   const int r = g8_dispatch<1, bf16>(X, W, out, M, N, K, K, K, N, ep, s);
   return r ? -r : 1;
 }
@@ -596,13 +615,14 @@ int uva_colsum_final_launch(const float* part, int nrows, int cols, float* out, 
 // floats of workspace.  1 = launched, 0 = not eligible, < 0 = -hipError
 extern "C" int uva_linear_dgelu_drop(const void* dY, const void* Wt, const void* pre, void* dpre, float* dbias,
                                      int accum_bias, float* part, int M, int N, int K, float drop_p,
-                                     unsigned long long seed, hipStream_t s) {
+                                     unsigned long long seed, const void* plane, hipStream_t s) {
   if (!g8_ok(dY, Wt, dpre, M, N, K, K, K, N, 2, nullptr) || (((uintptr_t)pre | (uintptr_t)part) % 16) || !dbias)
     return 0;
   uint32_t th;
   float ds;
   uva_drop_params(drop_p, &th, &ds);
-  G8Epi ep{nullptr, 1.f, (void*)pre, nullptr, part, th ? g8_key(seed) : 0u, th, ds};
+  if (plane && (N % 32 || !th || ((uintptr_t)plane % 4))) return (int)-hipErrorInvalidValue;
+  G8Epi ep{nullptr, 1.f, (void*)pre, nullptr, part, (const uint32_t*)plane, th ? g8_key(seed) : 0u, th, ds};
   int r = g8_launch<6, 3, 0, bf16>(dY, Wt, dpre, M, N, K, K, K, N, ep, s);
   if (r) return -r;
   r = uva_colsum_final_launch(part, (M + 255) / 256 * 4, N, dbias, accum_bias, s);
@@ -611,12 +631,14 @@ extern "C" int uva_linear_dgelu_drop(const void* dY, const void* Wt, const void*
 
 // timm Mlp fc2 / attention proj forward, fused: out (fp32) = R + drop(bf16(x W^T + b)).
 extern "C" int uva_linear_drop_res(const void* X, const void* W, const float* bias, const float* R, float* out, int M,
-                                   int N, int K, float drop_p, unsigned long long seed, hipStream_t s) {
+                                   int N, int K, float drop_p, unsigned long long seed, const void* plane,
+                                   hipStream_t s) {
   if (!g8_ok(X, W, out, M, N, K, K, K, N, 4, bias) || ((uintptr_t)R % 16)) return 0;
   uint32_t th;
   float ds;
   uva_drop_params(drop_p, &th, &ds);
-  G8Epi ep{bias, 1.f, nullptr, R, nullptr, th ? g8_key(seed) : 0u, th, ds};
+  if (plane && (N % 32 || !th || ((uintptr_t)plane % 4))) return (int)-hipErrorInvalidValue;
+  G8Epi ep{bias, 1.f, nullptr, R, nullptr, (const uint32_t*)plane, th ? g8_key(seed) : 0u, th, ds};
   const int r = g8_dispatch<2, float>(X, W, out, M, N, K, K, K, N, ep, s);
   return r ? -r : 1;
 }

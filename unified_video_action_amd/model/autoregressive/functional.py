@@ -284,19 +284,25 @@ class BlockFn(torch.autograd.Function):
             o, P, Pd = _attn_mat_fwd(qkv, B, N, H, scale, p_attn, seeds[0])
             o = as_dtype(o, c)
             lse = None
+        Hd = fc1w.shape[0]
+        planes = (None, None, None)
+        if c == torch.bfloat16 and RT.drop_planes and p_proj > 0 and D % 32 == 0 and Hd % 32 == 0:
+            # keep-bit planes of the proj / fc1 / fc2 dropouts (seeds 1-3): the fused GEMM epilogues test bits
+            # instead of hashing each element; fc1's plane serves the backward's fused GELU' epilogue too
+            planes = (ops.dropout_plane(M * D, p_proj, seeds[1], dev), ops.dropout_plane(M * Hd, p_proj, seeds[2], dev),
+                      ops.dropout_plane(M * D, p_proj, seeds[3], dev))
         x1 = torch.empty(M, D, dtype=F32, device=dev)
         # attention proj + proj_drop + the residual add: bf16 (autocast) output rounded before the dropout
         # and the fp32 add, in the 8-wave GEMM's epilogue; fp32 parity mode (or an ineligible shape): the
         # fused-epilogue GEMM of gemm.hip
         if not (c == torch.bfloat16 and RT.proj_8w and
-                ops.linear_drop_res(o, compute_weight(projw), projb.detach(), x, x1, p_proj, seeds[1])):
+                ops.linear_drop_res(o, compute_weight(projw), projb.detach(), x, x1, p_proj, seeds[1], planes[0])):
             ops.linear(o, compute_weight(projw), x1, bias=projb.detach(), residual=x, drop_p=p_proj,
                        seed=seeds[1])
         h2 = torch.empty(M, D, dtype=c, device=dev)
         m2 = torch.empty(M, dtype=F32, device=dev)
         r2 = torch.empty(M, dtype=F32, device=dev)
         ops.layernorm_fwd(x1, n2w.detach(), n2b.detach(), h2, m2, r2)
-        Hd = fc1w.shape[0]
         a = torch.empty(M, Hd, dtype=c, device=dev)
         pre1 = torch.empty(M, Hd, dtype=c, device=dev)
         x2 = torch.empty(M, D, dtype=F32, device=dev)
@@ -307,10 +313,11 @@ class BlockFn(torch.autograd.Function):
             # each.  Both routes give the same bits (same rounding points, same flat-index dropout masks)
             fused = not RT.mlp_split_epilogue
             if not (fused and ops.linear_gelu_drop(h2, compute_weight(fc1w), fc1b.detach(), pre1, a, p_proj,
-                                                   seeds[2])):
+                                                   seeds[2], planes[1])):
                 linear_bias(h2, fc1w, fc1b, pre1)
                 ops.act_drop_fwd(pre1, a, "gelu", drop_p=p_proj, seed=seeds[2])
-            if not (fused and ops.linear_drop_res(a, compute_weight(fc2w), fc2b.detach(), x1, x2, p_proj, seeds[3])):
+            if not (fused and ops.linear_drop_res(a, compute_weight(fc2w), fc2b.detach(), x1, x2, p_proj, seeds[3],
+                                                  planes[2])):
                 t2 = torch.empty(M, D, dtype=c, device=dev)
                 linear_bias(a, fc2w, fc2b, t2)
                 ops.act_drop_fwd(t2, x2, "none", drop_p=p_proj, seed=seeds[3], residual=x1)
@@ -322,6 +329,7 @@ class BlockFn(torch.autograd.Function):
         ctx.save_for_backward(x, h1, m1, r1, qkv, o, lse, P, Pd, x1, h2, m2, r2, pre1, a,
                               n1w, n1b, qkvw, qkvb, projw, projb, n2w, n2b, fc1w, fc1b, fc2w, fc2b)
         ctx.cfg = (B, N, H, p_attn, p_proj, seeds, flash)
+        ctx.plane1 = planes[1]
         ctx.hook = hook
         return x2
 
@@ -343,7 +351,7 @@ class BlockFn(torch.autograd.Function):
         # fc1 (gelu + drop1)
         dpre1 = torch.empty(M, Hd, dtype=c, device=dev)
         if c == torch.bfloat16 and RT.act_bwd_in_gemm and ops.linear_dgelu_drop(
-                dpre2, compute_weight_t(fc2w), pre1, dpre1, grad_buf(fc1b), p_proj, seeds[2]):
+                dpre2, compute_weight_t(fc2w), pre1, dpre1, grad_buf(fc1b), p_proj, seeds[2], plane=ctx.plane1):
             # fc2's dX product finishes dropout + GELU' in its epilogue and the fc1 bias gradient as column
             # partials (csrc/gemm8w.hip EPI 3): no [M, 3072] round trip of dA
             pass

@@ -124,7 +124,7 @@ def gemm8w_set(on=-2, mode=-2):
     return prev & 1, prev >> 1
 
 
-def linear_gelu_drop(x, w, bias, pre_out, out, drop_p=0.0, seed=0):
+def linear_gelu_drop(x, w, bias, pre_out, out, drop_p=0.0, seed=0, plane=None):
     """timm Mlp fc1 forward in one launch (uva_linear_gelu_drop): pre_out = bf16(x w^T + b),
     out = bf16(drop(gelu(pre_out))).  -> True if launched, False if the shape is not eligible."""
     M, K = x.shape
@@ -132,13 +132,13 @@ def linear_gelu_drop(x, w, bias, pre_out, out, drop_p=0.0, seed=0):
     assert x.is_contiguous() and w.is_contiguous() and pre_out.is_contiguous() and out.is_contiguous()
     with _traced(f"gemm+gelu+drop bf16 M{M} N{N} K{K}", 2.0 * M * N * K):
         r = lib().query("uva_linear_gelu_drop", ptr(x), ptr(w), ptr(bias), ptr(pre_out), ptr(out), M, N, K,
-                        float(drop_p), int(seed) & 0xFFFFFFFFFFFFFFFF, stream())
+                        float(drop_p), int(seed) & 0xFFFFFFFFFFFFFFFF, ptr(plane), stream())
     if r < 0:
         raise RuntimeError(f"fused Mlp GEMM failed with hipError {-r}")
     return r == 1
 
 
-def linear_drop_res(x, w, bias, residual, out, drop_p=0.0, seed=0):
+def linear_drop_res(x, w, bias, residual, out, drop_p=0.0, seed=0, plane=None):
     """timm Mlp fc2 (or attention proj) forward + dropout + fp32 residual in one launch
     (uva_linear_drop_res): out = residual + drop(bf16(x w^T + b)).  -> True if launched."""
     M, K = x.shape
@@ -146,13 +146,13 @@ def linear_drop_res(x, w, bias, residual, out, drop_p=0.0, seed=0):
     assert x.is_contiguous() and w.is_contiguous() and residual.is_contiguous() and out.is_contiguous()
     with _traced(f"gemm+drop+res bf16 M{M} N{N} K{K}", 2.0 * M * N * K):
         r = lib().query("uva_linear_drop_res", ptr(x), ptr(w), ptr(bias), ptr(residual), ptr(out), M, N, K,
-                        float(drop_p), int(seed) & 0xFFFFFFFFFFFFFFFF, stream())
+                        float(drop_p), int(seed) & 0xFFFFFFFFFFFFFFFF, ptr(plane), stream())
     if r < 0:
         raise RuntimeError(f"fused Mlp GEMM failed with hipError {-r}")
     return r == 1
 
 
-def linear_dgelu_drop(dy, wt, pre, dpre, dbias, drop_p=0.0, seed=0, accum_bias=True):
+def linear_dgelu_drop(dy, wt, pre, dpre, dbias, drop_p=0.0, seed=0, accum_bias=True, plane=None):
     """the timm Mlp backward through fc2 -> dropout -> GELU fused into fc2's dX product
     (uva_linear_dgelu_drop): dpre = bf16(gelu'(pre) * drop(bf16(dy wt^T))), dbias (+)= colsum(dpre).
     wt: fc2's transposed bf16 weight [in, out].  -> True if launched, False if not eligible."""
@@ -162,10 +162,19 @@ def linear_dgelu_drop(dy, wt, pre, dpre, dbias, drop_p=0.0, seed=0, accum_bias=T
     ws = workspace((M + 255) // 256 * 4 * N, dy.device)
     with _traced(f"gemm+dgelu+drop bf16 M{M} N{N} K{K}", 2.0 * M * N * K):
         r = lib().query("uva_linear_dgelu_drop", ptr(dy), ptr(wt), ptr(pre), ptr(dpre), ptr(dbias), int(accum_bias),
-                        ptr(ws), M, N, K, float(drop_p), int(seed) & 0xFFFFFFFFFFFFFFFF, stream())
+                        ptr(ws), M, N, K, float(drop_p), int(seed) & 0xFFFFFFFFFFFFFFFF, ptr(plane), stream())
     if r < 0:
         raise RuntimeError(f"fused Mlp GEMM failed with hipError {-r}")
     return r == 1
+
+
+def dropout_plane(n, drop_p, seed, device, out=None):
+    """keep-bit plane of n flat elements under (drop_p, seed): int32 [ceil(n / 32)] (uva_dropout_plane)"""
+    words = lib().query("uva_dropout_plane_words", int(n))
+    if out is None:
+        out = torch.empty(words, dtype=torch.int32, device=device)
+    _call("uva_dropout_plane", ptr(out), int(n), float(drop_p), int(seed) & 0xFFFFFFFFFFFFFFFF, stream())
+    return out
 
 
 def gemm4_plan(M, N, K):

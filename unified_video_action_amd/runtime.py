@@ -27,6 +27,11 @@ class _Runtime:
         # proj output before the dropout and the fp32 residual add, as autocast) instead of gemm_8ph's fused
         # epilogue (which kept the fp32 accumulator): 59-62 vs 72-75 us at B32 (profiles/r06/g8w_fused.txt)
         self.proj_8w = True
+        # the proj / fc1 / fc2 dropout masks of a Block as keep-bit planes (one launch each per step) read by the
+        # fused epilogues, instead of the counter hash per element inside them (the same bits).  Measured off:
+        # the epilogue's plane-word loads expose their latency where the hash was issue-bound VALU (fc1 285-296
+        # vs 253-271 us, bench 255.2 vs 257.7 samples/s same box, profiles/r06/g8w_planes.txt); kept tested
+        self.drop_planes = False
         # Mlp backward: dropout + GELU' (+ the fc1 bias gradient) in the epilogue of fc2's dX product (8-wave
         # GEMM, EPI 3) instead of dX GEMM -> act_bwd_bias (one [M, 3072] bf16 round trip less per Block)
         self.act_bwd_in_gemm = True
