@@ -121,6 +121,15 @@ int uva_linear_dgelu_drop(const void* dY, const void* Wt, const void* pre, void*
  * fused Mlp GEMMs above take one as `plane` (non-null: test a bit instead of hashing per element in the
  * epilogue; N % 32 == 0, drop_p > 0), so the mask of a Block's fc1 / fc2 / proj dropout is computed once per
  * step, off the GEMMs (mar_con_unified.py:236-249 Mlp.drop, :201-215 proj_drop).  words = ceil(n / 32). */
+/* LayerNorm backward of the timm Block's norm2 (mar_con_unified.py:236-249; fp32 x / dx, bf16 dy, D = 768,
+ * affine, dx = dx_base + LN'(dy)) that also writes drop_out = bf16(drop(dx)) and adds the column sums of those
+ * stored values to dbias: the backward of proj_drop and the attention proj's bias gradient (:201-215) in
+ * the same pass, instead of a second pass (uva_act_bwd_bias, act none) over the fp32 dx.  workspace: 3 *
+ * ceil(rows / 64) * D floats.  Other shapes / forms: hipErrorInvalidValue. */
+int uva_layernorm_bwd_drop(const float* x, const float* w, const void* dy, const float* mean, const float* rstd,
+                           const float* dx_base, float* dx, float* dw, float* db, int accum_wb, void* drop_out,
+                           float drop_p, unsigned long long seed, float* dbias, int accum_dbias, float* workspace,
+                           int rows, int D, hipStream_t stream);
 long long uva_dropout_plane_words(long long n);
 int uva_dropout_plane(void* plane, long long n, float drop_p, unsigned long long seed, hipStream_t stream);
 long long uva_gemm4_plan(int M, int N, int K);

@@ -120,9 +120,11 @@ def test_plain_8w_bit_exact_vs_gemm4(M, N, K, odt, mode):
 
 
 def test_block_fused_routes_match_split_routes():
-    """one timm Block (BlockFn) at the bench geometry slice (B 4, N 1024, D 768, H 12, dropout 0.1) forward +
-    backward with the fused Mlp routes (RT defaults) and with the split routes, same seeds: output and every
-    gradient bit-identical, fc1.bias within 1e-5 (column sums in another order)"""
+    """two chained timm Blocks (BlockFn) at a bench-geometry slice (B 4, N 1024, D 768, H 12, dropout 0.1) forward +
+    backward with the fused routes (RT defaults: Mlp epilogues on the 8-wave GEMM, norm2 backward emitting the
+    proj_drop backward, the second Block's norm1 backward emitting the first Block's fc2 dropout backward) and
+    with the split routes, same seeds: output and every gradient bit-identical, the three bias gradients the
+    fused routes sum in another order (fc1 / proj / fc2 bias) within 1e-5"""
     import copy
     from functools import partial
 
@@ -134,31 +136,36 @@ def test_block_fused_routes_match_split_routes():
 
     RT.set_precision("bf16")
     torch.manual_seed(0)
-    blk = Block(768, 12, 4.0, qkv_bias=True, norm_layer=partial(nn.LayerNorm, eps=1e-6), proj_drop=0.1,
-                attn_drop=0.1).to(DEV).train()
-    with torch.no_grad():
-        for n, p in blk.named_parameters():
-            if n.endswith("bias") or "norm" in n:
-                p.add_(torch.randn_like(p) * 0.05)  # non-trivial biases / LayerNorm affines
+    blocks = []
+    for _ in range(2):
+        blk = Block(768, 12, 4.0, qkv_bias=True, norm_layer=partial(nn.LayerNorm, eps=1e-6), proj_drop=0.1,
+                    attn_drop=0.1).to(DEV).train()
+        with torch.no_grad():
+            for n, p in blk.named_parameters():
+                if n.endswith("bias") or "norm" in n:
+                    p.add_(torch.randn_like(p) * 0.05)  # non-trivial biases / LayerNorm affines
+        blocks.append(blk)
     B, N = 4, 1024
     x0 = torch.randn(B, N, 768, device=DEV)
     gy = torch.randn(B, N, 768, device=DEV)
     out = {}
     for split in (False, True):
-        m = copy.deepcopy(blk)
-        RT.mlp_split_epilogue, RT.act_bwd_in_gemm = split, not split
+        ms = [copy.deepcopy(b) for b in blocks]
+        RT.mlp_split_epilogue, RT.act_bwd_in_gemm, RT.ln_bwd_drop = split, not split, not split
+        RT.begin_forward()
         RT.seed(77)
         x = x0.clone().requires_grad_(True)
-        y = Fn.block_forward(m, x, B, N, 0.1, 0.1)
+        y = Fn.block_forward(ms[1], Fn.block_forward(ms[0], x, B, N, 0.1, 0.1), B, N, 0.1, 0.1)
         y.backward(gy)
         torch.cuda.synchronize()
-        out[split] = (y.detach(), x.grad, {n: p.grad.clone() for n, p in m.named_parameters()})
-    RT.mlp_split_epilogue, RT.act_bwd_in_gemm = False, True
+        out[split] = (y.detach(), x.grad, {f"{i}.{n}": p.grad.clone() for i, m in enumerate(ms)
+                                           for n, p in m.named_parameters()})
+    RT.mlp_split_epilogue, RT.act_bwd_in_gemm, RT.ln_bwd_drop = False, True, True
     (yf, gxf, gf), (ys, gxs, gs) = out[False], out[True]
     assert torch.equal(yf, ys)
     assert torch.equal(gxf, gxs)
     for n in gs:
-        if n == "mlp.fc1.bias":
+        if n.endswith(("mlp.fc1.bias", "attn.proj.bias", "mlp.fc2.bias")):
             assert (gf[n] - gs[n]).abs().max().item() <= 1e-5 * gs[n].abs().max().item(), n
         else:
             assert torch.equal(gf[n], gs[n]), n
@@ -210,3 +217,36 @@ def test_fused_with_plane_bit_exact_vs_hash(which, M, N, K):
         assert ops.linear_dgelu_drop(dy, wt, pre, da, ga, drop_p=p, seed=seed)
         assert ops.linear_dgelu_drop(dy, wt, pre, db, gb, drop_p=p, seed=seed, plane=plane)
         assert torch.equal(da, db) and torch.equal(ga, gb)
+
+
+@pytest.mark.parametrize("p", [0.0, 0.1])
+@pytest.mark.parametrize("rows", [32768, 1000])
+def test_layernorm_bwd_drop_matches_two_pass(rows, p):
+    """norm2 backward with the proj_drop backward + proj bias gradient in the same pass (uva_layernorm_bwd_drop)
+    vs layernorm_bwd then act_bwd_bias(none): dx, dropout output, LN dw / db bit-identical; the proj bias sum
+    within 1e-5 (another summation order)"""
+    from unified_video_action_amd.native import ops
+    D = 768
+    g = torch.Generator(device=DEV).manual_seed(rows)
+    x = torch.randn(rows, D, device=DEV, generator=g)
+    w = torch.rand(D, device=DEV, generator=g) + 0.5
+    dy = (torch.randn(rows, D, device=DEV, generator=g) * 0.1).to(torch.bfloat16)
+    base = torch.randn(rows, D, device=DEV, generator=g) * 0.1
+    mean = x.mean(1)
+    rstd = torch.rsqrt(x.var(1, unbiased=False) + 1e-6)
+    res = []
+    for fused in (True, False):
+        dx = torch.empty(rows, D, device=DEV)
+        dw, db, dbias = torch.full((D,), 0.25, device=DEV), torch.full((D,), 0.5, device=DEV), torch.full((D,), 1.0, device=DEV)
+        out = torch.empty(rows, D, device=DEV, dtype=torch.bfloat16)
+        if fused:
+            assert ops.layernorm_bwd_drop(x, w, dy, mean, rstd, dx, dw, db, base, out, p, 99, dbias)
+        else:
+            ops.layernorm_bwd(x, w, dy, mean, rstd, dx, accum=False, dw=dw, db=db, dx_base=base)
+            ops.act_bwd_bias(None, dx, out, dbias, "none", drop_p=p, seed=99)
+        torch.cuda.synchronize()
+        res.append((dx, out, dw, db, dbias))
+    (a, b) = res
+    for i in range(4):
+        assert torch.equal(a[i], b[i]), i
+    assert (a[4] - b[4]).abs().max().item() <= 1e-5 * b[4].abs().max().item()

@@ -146,7 +146,17 @@ __device__ __forceinline__ RawVec<VEC, T> ldraw(const T* p) {
 // so a wave keeps two rows of loads in flight and each row costs one memory latency, not two (the
 // dx-base read used to wait for the row's reductions).  HBM-bound: per row D * (sizeof(TI) +
 // sizeof(TD) + 4 [+ 4 dx base]) bytes read, D * 4 written.
-template <typename TI, typename TO, int VEC, int NC, typename TD>
+// DROPO: the dx rows also leave as bf16(drop(dx)) (the next op's input: the timm Block's proj_drop backward,
+// mar_con_unified.py:201-215, i.e. what act_bwd_bias(none) computed from dx in a second pass) with the column
+// sums of those stored values (the proj bias gradient) as per-block partials dd_part
+struct LnDrop {
+  bf16* out;
+  float* part;
+  uint32_t key, thresh;
+  float dscale;
+};
+
+template <typename TI, typename TO, int VEC, int NC, typename TD, bool DROPO = false>
 __global__ __launch_bounds__(256) void ln_bwd(const TI* __restrict__ x, const float* __restrict__ w,
                                               const float* __restrict__ b, const TO* __restrict__ scale, long long ldm,
                                               const TD* __restrict__ dy, const float* __restrict__ mean_in,
@@ -154,9 +164,17 @@ __global__ __launch_bounds__(256) void ln_bwd(const TI* __restrict__ x, const fl
                                               float* dx, int accum,
                                               TO* __restrict__ dscale, TO* __restrict__ dshift,
                                               float* __restrict__ dw_part, float* __restrict__ db_part, int rows,
-                                              int D, int rows_per_block) {
+                                              int D, int rows_per_block, LnDrop ldrop = LnDrop{}) {
   __shared__ float red_w[4][1024];
   __shared__ float red_b[4][1024];
+  __shared__ float red_d[DROPO ? 4 : 1][DROPO ? 1024 : 1];
+  float pd[NC][VEC];
+  if constexpr (DROPO) {
+#pragma unroll
+    for (int c = 0; c < NC; ++c)
+#pragma unroll
+      for (int i = 0; i < VEC; ++i) pd[c][i] = 0.f;
+  }
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   float pw[NC][VEC], pb[NC][VEC];
 #pragma unroll
@@ -253,6 +271,30 @@ __global__ __launch_bounds__(256) void ln_bwd(const TI* __restrict__ x, const fl
         o[i] = addsrc ? R.a[c].v[i] + d : d;
       }
       stv<VEC>(dx + (long long)row * D + col0, o);
+      if constexpr (DROPO) {
+        static_assert(VEC % 2 == 0, "pairs");
+        const unsigned long long e0 = (unsigned long long)row * (unsigned)D + (unsigned)col0;  // even
+        float q[VEC];
+#pragma unroll
+        for (int i = 0; i < VEC; i += 2) {
+          const uint32_t h = drop_hash(ldrop.key, (e0 + i) >> 1);
+          q[i] = (h & 0xFFFFu) >= ldrop.thresh ? o[i] * ldrop.dscale : 0.f;
+          q[i + 1] = (h >> 16) >= ldrop.thresh ? o[i + 1] * ldrop.dscale : 0.f;
+        }
+        bf16 qb[VEC];
+#pragma unroll
+        for (int i = 0; i < VEC; ++i) {
+          qb[i] = (bf16)q[i];
+          pd[c][i] += (float)qb[i];
+        }
+        if constexpr (VEC == 4) {
+          bf16x4 v4 = {qb[0], qb[1], qb[2], qb[3]};
+          *(bf16x4*)(ldrop.out + (long long)row * D + col0) = v4;
+        } else {
+#pragma unroll
+          for (int i = 0; i < VEC; ++i) ldrop.out[(long long)row * D + col0 + i] = qb[i];
+        }
+      }
     }
   };
   Row ra, rb;
@@ -288,6 +330,18 @@ __global__ __launch_bounds__(256) void ln_bwd(const TI* __restrict__ x, const fl
       dw_part[(long long)blockIdx.x * D + col] = red_w[0][col] + red_w[1][col] + red_w[2][col] + red_w[3][col];
       db_part[(long long)blockIdx.x * D + col] = red_b[0][col] + red_b[1][col] + red_b[2][col] + red_b[3][col];
     }
+  }
+  if constexpr (DROPO) {
+#pragma unroll
+    for (int c = 0; c < NC; ++c)
+#pragma unroll
+      for (int i = 0; i < VEC; ++i) {
+        const int col = col_of<VEC>(c, lane, i);
+        if (col < D) red_d[wid][col] = pd[c][i];
+      }
+    __syncthreads();
+    for (int col = threadIdx.x; col < D; col += 256)
+      ldrop.part[(long long)blockIdx.x * D + col] = red_d[0][col] + red_d[1][col] + red_d[2][col] + red_d[3][col];
   }
 }
 
@@ -506,6 +560,38 @@ extern "C" int uva_layernorm_bwd(int in_dtype, int out_dtype, const void* x, con
     colsum_partials(pw, db ? pb : nullptr, dw, db, nblk, D, accum_wb, stream);
     UVA_LAUNCH_CHECK();
   }
+  return 0;
+}
+
+// uva_layernorm_bwd for the timm Block's norm2 (fp32 x / dx, bf16 dy, D = 768, affine, dx_base) that also
+// emits bf16(drop(dx)) -> drop_out and adds its column sums to dbias (proj_drop backward + the proj bias
+// gradient, one pass instead of a second read of dx).  workspace: 3 * ceil(rows / 64) * D floats.
+// Other shapes return hipErrorInvalidValue (callers use the two-pass route).
+extern "C" int uva_layernorm_bwd_drop(const float* x, const float* w, const void* dy, const float* mean,
+                                      const float* rstd, const float* dx_base, float* dx, float* dw, float* db,
+                                      int accum_wb, void* drop_out, float drop_p, unsigned long long seed,
+                                      float* dbias, int accum_dbias, float* workspace, int rows, int D,
+                                      hipStream_t stream) {
+  if (rows <= 0) return 0;
+  if (D != 768 || !w || !dw || !db || !drop_out || !dbias || !workspace || ((uintptr_t)drop_out % 8))
+    return (int)hipErrorInvalidValue;
+  const int rpb = 64;
+  const int nblk = (rows + rpb - 1) / rpb;
+  float* pw = workspace;
+  float* pb = workspace + (long long)nblk * D;
+  float* pd = workspace + 2LL * nblk * D;
+  uint32_t th;
+  float ds;
+  uva_drop_params(drop_p, &th, &ds);
+  LnDrop ld{(bf16*)drop_out, pd, drop_key(seed), th, ds};
+  ln_bwd<float, float, 4, 3, bf16, true><<<dim3(nblk), 256, 0, stream>>>(
+      x, w, nullptr, (const float*)nullptr, 0, (const bf16*)dy, mean, rstd, dx_base, dx, 0, (float*)nullptr,
+      (float*)nullptr, pw, pb, rows, D, rpb, ld);
+  UVA_LAUNCH_CHECK();
+  colsum_partials(pw, pb, dw, db, nblk, D, accum_wb, stream);
+  UVA_LAUNCH_CHECK();
+  colsum_partials(pd, nullptr, dbias, nullptr, nblk, D, accum_dbias, stream);
+  UVA_LAUNCH_CHECK();
   return 0;
 }
 

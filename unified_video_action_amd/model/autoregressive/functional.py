@@ -257,6 +257,10 @@ class BlockFn(torch.autograd.Function):
         c = cdt()
         scale = (D // H) ** -0.5
         seeds = [_seed() for _ in range(4)]
+        # is x the previous Block's output (whose fc2 dropout backward this Block's norm1 backward can emit)?
+        up = RT._drop_pending.pop(x.data_ptr(), None)
+        if up is not None and not (up[0].shape == x.shape and up[0].dtype == x.dtype):
+            up = None
         if premask is not None:  # attention keep-mask planes generated ahead on the side stream
             seeds[0] = premask[0]
         h1 = torch.empty(M, D, dtype=c, device=dev)
@@ -330,6 +334,9 @@ class BlockFn(torch.autograd.Function):
                               n1w, n1b, qkvw, qkvb, projw, projb, n2w, n2b, fc1w, fc1b, fc2w, fc2b)
         ctx.cfg = (B, N, H, p_attn, p_proj, seeds, flash)
         ctx.plane1 = planes[1]
+        ctx.up = up[1:] if up is not None else None
+        if c == torch.bfloat16 and RT.ln_bwd_drop and any(ctx.needs_input_grad):
+            RT._drop_pending[x2.data_ptr()] = (x2, p_proj, seeds[3], fc2b)
         ctx.hook = hook
         return x2
 
@@ -343,9 +350,14 @@ class BlockFn(torch.autograd.Function):
         c = cdt()
         scale = (D // H) ** -0.5
         g2 = as_dtype(g2, F32)
-        # fc2 (+drop2, residual)
-        dpre2 = torch.empty(M, D, dtype=c, device=dev)
-        ops.act_bwd_bias(None, g2, dpre2, grad_buf(fc2b), "none", drop_p=p_proj, seed=seeds[3])
+        # fc2 (+drop2, residual): bf16(drop(g2)) and the fc2 bias gradient -- already emitted by the next Block's
+        # norm1 backward when g2 is exactly the gradient it produced (hand-off by seed; verified by pointer)
+        ready = RT._drop_ready.pop(seeds[3], None)
+        if ready is not None and ready[0] == g2.data_ptr() and ready[1].shape == (M, D):
+            dpre2 = ready[1]
+        else:
+            dpre2 = torch.empty(M, D, dtype=c, device=dev)
+            ops.act_bwd_bias(None, g2, dpre2, grad_buf(fc2b), "none", drop_p=p_proj, seed=seeds[3])
         ops.linear_dw(dpre2, a, grad_buf(fc2w))
         Hd = fc1w.shape[0]
         # fc1 (gelu + drop1)
@@ -371,12 +383,17 @@ class BlockFn(torch.autograd.Function):
         linear_dx_w(dpre1, fc1w, dh2)
         del dpre1
         g1 = torch.empty(M, D, dtype=F32, device=dev)
-        ops.layernorm_bwd(x1, n2w.detach(), dh2, m2, r2, g1, accum=False, dw=grad_buf(n2w), db=grad_buf(n2b),
-                          dx_base=g2)
-        del dh2
-        # proj (+proj_drop, residual)
         dprep = torch.empty(M, D, dtype=c, device=dev)
-        ops.act_bwd_bias(None, g1, dprep, grad_buf(projb), "none", drop_p=p_proj, seed=seeds[1])
+        # norm2 backward; with bf16 operands it also emits the proj_drop backward (dprep) and the proj bias
+        # gradient in the same pass (ln_bwd DROPO)
+        if not (c == torch.bfloat16 and RT.ln_bwd_drop and dh2.dtype == c and
+                ops.layernorm_bwd_drop(x1, n2w.detach(), dh2, m2, r2, g1, grad_buf(n2w), grad_buf(n2b), g2, dprep,
+                                       p_proj, seeds[1], grad_buf(projb))):
+            ops.layernorm_bwd(x1, n2w.detach(), dh2, m2, r2, g1, accum=False, dw=grad_buf(n2w), db=grad_buf(n2b),
+                              dx_base=g2)
+            # proj (+proj_drop, residual)
+            ops.act_bwd_bias(None, g1, dprep, grad_buf(projb), "none", drop_p=p_proj, seed=seeds[1])
+        del dh2
         ops.linear_dw(dprep, o, grad_buf(projw))
         do = torch.empty(M, D, dtype=c, device=dev)
         linear_dx_w(dprep, projw, do)
@@ -394,8 +411,19 @@ class BlockFn(torch.autograd.Function):
         linear_dx_w(dqkv, qkvw, dh1)
         del dqkv
         gx = torch.empty(M, D, dtype=F32, device=dev)
-        ops.layernorm_bwd(x, n1w.detach(), dh1, m1, r1, gx, accum=False, dw=grad_buf(n1w), db=grad_buf(n1b),
-                          dx_base=g1)
+        up = ctx.up
+        if up is not None and dh1.dtype == c:
+            # norm1 backward + the previous Block's fc2 dropout backward and fc2 bias gradient in one pass
+            p_up, seed_up, fc2b_up = up
+            d_up = torch.empty(M, D, dtype=c, device=dev)
+            if ops.layernorm_bwd_drop(x, n1w.detach(), dh1, m1, r1, gx, grad_buf(n1w), grad_buf(n1b), g1, d_up,
+                                      p_up, seed_up, grad_buf(fc2b_up)):
+                RT._drop_ready[seed_up] = (gx.data_ptr(), d_up)
+            else:
+                up = None
+        if up is None or dh1.dtype != c:
+            ops.layernorm_bwd(x, n1w.detach(), dh1, m1, r1, gx, accum=False, dw=grad_buf(n1w), db=grad_buf(n1b),
+                              dx_base=g1)
         if ctx.hook is not None:
             ctx.hook()  # every grad of this block is enqueued: launch its DP bucket all-reduce
         return (gx,) + (None,) * 17

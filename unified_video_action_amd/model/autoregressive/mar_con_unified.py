@@ -21,7 +21,7 @@ import scipy.stats as stats
 import torch
 import torch.nn as nn
 
-from ...runtime import cdt
+from ...runtime import RT, cdt
 from .diffusion_action_loss import DiffActLoss
 from .diffusion_loss import DiffLoss
 from .functional import F32, block_forward, layer_norm, linear
@@ -339,6 +339,7 @@ class MAR(nn.Module):
 
     def forward(self, imgs, cond, history_nactions=None, nactions=None, text_latents=None, task_mode=None,
                 proprioception_input={}, rng=None):
+        RT.begin_forward()
         dev = cond.device
         x = self.to_tokens(imgs).to(F32)
         cnd = self.to_tokens(cond).to(F32)

@@ -268,6 +268,21 @@ def layernorm_bwd(x, w, dy, mean, rstd, dx, accum, dw=None, db=None, scale=None,
                stream())
 
 
+def layernorm_bwd_drop(x, w, dy, mean, rstd, dx, dw, db, dx_base, drop_out, drop_p, seed, dbias, accum_wb=True,
+                       accum_dbias=True):
+    """layernorm_bwd (fp32 x / dx, bf16 dy, D 768, affine, dx_base) + drop_out = bf16(drop(dx)) and dbias (+)=
+    colsum(drop_out) in one pass (uva_layernorm_bwd_drop).  -> False when the form is not covered."""
+    rows, D = x.shape
+    if not (D == 768 and x.dtype == torch.float32 and dy.dtype == torch.bfloat16 and dx_base is not None
+            and drop_out.dtype == torch.bfloat16 and drop_out.is_contiguous() and dx_base.is_contiguous()):
+        return False
+    ws = workspace(3 * ((rows + 63) // 64) * D, x.device)
+    _call("uva_layernorm_bwd_drop", ptr(x), ptr(w), ptr(dy), ptr(mean), ptr(rstd), ptr(dx_base), ptr(dx), ptr(dw),
+          ptr(db), int(accum_wb), ptr(drop_out), float(drop_p), int(seed) & 0xFFFFFFFFFFFFFFFF, ptr(dbias),
+          int(accum_dbias), ptr(ws), rows, D, stream())
+    return True
+
+
 def softmax_fwd(S, P, Pd, L, scale, drop_p=0.0, seed=0):
     rows = S.numel() // L
     _call("uva_softmax_fwd", dt(S), ptr(S), ptr(P), ptr(Pd), rows, L, float(scale), float(drop_p),

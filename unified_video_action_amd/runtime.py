@@ -32,6 +32,8 @@ class _Runtime:
         # the epilogue's plane-word loads expose their latency where the hash was issue-bound VALU (fc1 285-296
         # vs 253-271 us, bench 255.2 vs 257.7 samples/s same box, profiles/r06/g8w_planes.txt); kept tested
         self.drop_planes = False
+        # norm2's LayerNorm backward also emits the proj_drop backward + proj bias gradient (one pass over dx)
+        self.ln_bwd_drop = True
         # Mlp backward: dropout + GELU' (+ the fc1 bias gradient) in the epilogue of fc2's dX product (8-wave
         # GEMM, EPI 3) instead of dX GEMM -> act_bwd_bias (one [M, 3072] bf16 round trip less per Block)
         self.act_bwd_in_gemm = True
@@ -51,6 +53,11 @@ class _Runtime:
         self._attn_shapes = {}
         self._attn_ready = {}
         self._side = None
+        # cross-Block fusion of the fc2 dropout backward into the NEXT Block's norm1 backward: a Block's output
+        # (data_ptr) -> (the output itself, p, seed, fc2.bias) while a training forward is in flight; the
+        # consumer Block's backward leaves (dX tensor it produced, bf16(drop(dX))) under the seed
+        self._drop_pending = {}
+        self._drop_ready = {}
         # bumped whenever HIP kernels rewrite parameters in place (optimizer / EMA steps): caches
         # keyed on parameters (non-static compute shadows, the sampler's captured graphs) compare it
         self.param_gen = 0
@@ -69,6 +76,11 @@ class _Runtime:
             self.attn_fp8 = True
         else:
             raise ValueError(f"unknown precision {name}")
+
+    def begin_forward(self):
+        """a new MAR forward: hand-offs of the previous step that found no consumer are dropped"""
+        self._drop_pending.clear()
+        self._drop_ready.clear()
 
     def bump_params(self):
         self.param_gen += 1
