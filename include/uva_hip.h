@@ -340,6 +340,13 @@ int uva_attn_fwd(const void* qkv, void* out, float* lse2, const void* mask, int 
                  float drop_p, hipStream_t stream);
 int uva_attn_bwd(const void* qkv, const void* out, const void* dout, const float* lse2, const void* mask, float* Dvec,
                  void* dqkv, void* workspace, int B, int N, int H, float scale, float drop_p, hipStream_t stream);
+/* uva_attn_bwd + the qkv Linear's bias gradient, dbias[3 H 64] (+)= column sums of dqkv as stored (bf16):
+ * per-(batch, 128-row block) partials from the dQ / dK-dV kernels' epilogues in `part`
+ * (B * ceil(N / 128) * 3 H 64 floats), then one column reduce -- no separate pass over dqkv
+ * (replaces autograd's sum of the qkv output gradient for nn.Linear.bias, mar_con_unified.py:201-215). */
+int uva_attn_bwd_bias(const void* qkv, const void* out, const void* dout, const float* lse2, const void* mask,
+                      float* Dvec, void* dqkv, float* dbias, int accum, float* part, int B, int N, int H, float scale,
+                      float drop_p, hipStream_t stream);
 
 /* ---- KL-VAE encoder plumbing (vae/vaekl.py, utils/data_utils.py) ---------------------
  * uva_resize_select: obs image [B,T,3,Hin,Win] fp32 in [0,1] -> NHWC [B*nsel,256,256,Cpad]

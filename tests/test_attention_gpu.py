@@ -192,3 +192,28 @@ def test_flash_dropout_production_grid_vs_fp32(B, N, H):
             assert rel_err(d[:, :, i].permute(0, 2, 1, 3), t.grad) < 3e-2, (b0, i)
         del refo, qq, kk, vv, keep
     assert abs(sum(kept) / len(kept) - 0.9) < 0.005
+
+
+@pytest.mark.parametrize("p", [0.0, 0.1])
+@pytest.mark.parametrize("B,N,H", [(4, 1024, 12), (2, 1088, 12), (1, 192, 2)])
+def test_attn_bwd_bias_partials(B, N, H, p):
+    """uva_attn_bwd_bias: dqkv bit-identical to uva_attn_bwd, and the qkv bias gradient from the kernels'
+    epilogue partials equal to the column sums of the stored dqkv (fp64) within 1e-5 of scale, accumulating
+    onto the existing gradient; N = 1088 / 192 leave a half-empty 128-row block (its masked rows add zeros)"""
+    from unified_video_action_amd.native import ops
+    torch.manual_seed(1)
+    qkv = torch.randn(B, N, 3 * H * 64, device=DEV).to(torch.bfloat16)
+    out = torch.empty(B, N, H * 64, device=DEV, dtype=torch.bfloat16)
+    lse = torch.empty(B, H, N, device=DEV)
+    seed = 1234
+    ops.attn_fwd(qkv, out, lse, B, N, H, 0.125, drop_p=p, seed=seed)
+    dout = torch.randn(B, N, H * 64, device=DEV).to(torch.bfloat16)
+    dvec = torch.empty(B, H, N, device=DEV)
+    d0 = torch.empty_like(qkv)
+    ops.attn_bwd(qkv, out, dout, lse, dvec, d0, B, N, H, 0.125, drop_p=p, seed=seed)
+    d1 = torch.full_like(qkv, float("nan"))
+    db = torch.full((3 * H * 64,), 0.75, device=DEV)
+    ops.attn_bwd(qkv, out, dout, lse, dvec, d1, B, N, H, 0.125, drop_p=p, seed=seed, dbias=db)
+    assert torch.equal(d1, d0)
+    want = d0.double().reshape(-1, 3 * H * 64).sum(0) + 0.75
+    assert (db.double() - want).abs().max().item() <= 1e-5 * want.abs().max().item()

@@ -438,7 +438,8 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_kernel(const bf16* __res
                                                                const float* __restrict__ lse2,
                                                                const float* __restrict__ Dvec,
                                                                const uint64_t* __restrict__ MK, bf16* __restrict__ dqkv,
-                                                               int N, int H, float scale, float c, float vsc) {
+                                                               int N, int H, float scale, float c, float vsc,
+                                                               float* __restrict__ cpart) {
   __shared__ __attribute__((aligned(16))) bf16 sQ[2][AT_TILE];
   __shared__ __attribute__((aligned(16))) bf16 sO[2][AT_TILE];
   __shared__ __attribute__((aligned(16))) float sL[2][64];
@@ -651,6 +652,36 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_kernel(const bf16* __res
     cur ^= 1;
   }
   // lane holds [d = dt*16+4g+r][key = kt*16+li]
+  if (cpart) {
+    // the qkv bias gradient's K / V columns: sums over this block's 128 keys of the values as stored
+    // (bf16), per wave by DPP row sums over the 16 key lanes, then over the 4 waves through LDS
+    float* red = (float*)&sQ[0][0];  // [4 waves][128] (the loop is over: the last barrier passed)
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float sk = 0.f, sv = 0.f;
+#pragma unroll
+        for (int kt = 0; kt < 2; ++kt) {
+          const bool ok = k0 + kt * 16 + li < N;
+          sk += ok ? (float)(bf16)(dk[dt][kt][r] * scale) : 0.f;
+          sv += ok ? (float)(bf16)(dv[dt][kt][r] * vsc) : 0.f;
+        }
+        sk = row16_sum(sk);
+        sv = row16_sum(sv);
+        if (li == 0) {
+          red[w * 128 + dt * 16 + 4 * g + r] = sk;
+          red[w * 128 + 64 + dt * 16 + 4 * g + r] = sv;
+        }
+      }
+    __syncthreads();
+    if (threadIdx.x < 128) {
+      const int t = threadIdx.x;
+      const float v = (red[t] + red[128 + t]) + (red[256 + t] + red[384 + t]);
+      const long long rowp = (long long)b * gridDim.x + bx;
+      cpart[rowp * (3LL * H * 64) + (t < 64 ? H * 64 : 2 * H * 64) + h * 64 + (t & 63)] = v;
+    }
+  }
 #pragma unroll
   for (int kt = 0; kt < 2; ++kt) {
     const int key = k0 + kt * 16 + li;
@@ -687,7 +718,8 @@ __global__ __launch_bounds__(256, UVA_ATT_DQ_OCC) void attn_bwd_dq_kernel(const 
                                                              const float* __restrict__ lse2,
                                                              float* __restrict__ Dvec,
                                                              const uint64_t* __restrict__ MQ, bf16* __restrict__ dqkv,
-                                                             int N, int H, float scale, float c, float dmul) {
+                                                             int N, int H, float scale, float c, float dmul,
+                                                             float* __restrict__ cpart) {
   __shared__ __attribute__((aligned(16))) bf16 sK[2][AT_TILE];
   __shared__ __attribute__((aligned(16))) bf16 sV[2][AT_TILE];
   int bx, bh;
@@ -868,6 +900,28 @@ __global__ __launch_bounds__(256, UVA_ATT_DQ_OCC) void attn_bwd_dq_kernel(const 
     cur ^= 1;
   }
   // lane holds dQ^T[d = dt*16+4g+r][q = qt*16+li]
+  if (cpart) {
+    // the qkv bias gradient's Q columns: sums over this block's 128 queries of the values as stored
+    float* red = (float*)&sK[0][0];  // [4 waves][64]
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float sq = 0.f;
+#pragma unroll
+        for (int qt = 0; qt < 2; ++qt)
+          sq += q0 + qt * 16 + li < N ? (float)(bf16)(dq[dt][qt][r] * scale) : 0.f;
+        sq = row16_sum(sq);
+        if (li == 0) red[w * 64 + dt * 16 + 4 * g + r] = sq;
+      }
+    __syncthreads();
+    if (threadIdx.x < 64) {
+      const int t = threadIdx.x;
+      const float v = (red[t] + red[64 + t]) + (red[128 + t] + red[192 + t]);
+      const long long rowp = (long long)b * gridDim.x + bx;
+      cpart[rowp * (3LL * H * 64) + h * 64 + t] = v;
+    }
+  }
 #pragma unroll
   for (int qt = 0; qt < 2; ++qt) {
     const int q = q0 + qt * 16 + li;
@@ -929,9 +983,33 @@ extern "C" int uva_attn_fwd(const void* qkv, void* out, float* lse2, const void*
   return 0;
 }
 
+static int attn_bwd_launch(const void* qkv, const void* out, const void* dout, const float* lse2, const void* mask,
+                           float* Dvec, void* dqkv, int B, int N, int H, float scale, float drop_p, float* cpart,
+                           hipStream_t s);
+
 extern "C" int uva_attn_bwd(const void* qkv, const void* out, const void* dout, const float* lse2, const void* mask,
                             float* Dvec, void* dqkv, void* workspace, int B, int N, int H, float scale, float drop_p,
                             hipStream_t s) {
+  (void)workspace;
+  return attn_bwd_launch(qkv, out, dout, lse2, mask, Dvec, dqkv, B, N, H, scale, drop_p, nullptr, s);
+}
+
+int uva_colsum_final_launch(const float* part, int nrows, int cols, float* out, int accum, hipStream_t s);
+
+// + the qkv Linear's bias gradient (the column sums of dqkv as stored): per-(batch, 128-row block) partials
+// written by the two kernels' epilogues into `part` ((B * ceil(N / 128)) * 3 H 64 floats), reduced into dbias
+extern "C" int uva_attn_bwd_bias(const void* qkv, const void* out, const void* dout, const float* lse2,
+                                 const void* mask, float* Dvec, void* dqkv, float* dbias, int accum, float* part, int B,
+                                 int N, int H, float scale, float drop_p, hipStream_t s) {
+  if (!dbias || !part) return (int)hipErrorInvalidValue;
+  int r = attn_bwd_launch(qkv, out, dout, lse2, mask, Dvec, dqkv, B, N, H, scale, drop_p, part, s);
+  if (r) return r;
+  return uva_colsum_final_launch(part, B * ((N + 127) / 128), 3 * H * 64, dbias, accum, s);
+}
+
+static int attn_bwd_launch(const void* qkv, const void* out, const void* dout, const float* lse2, const void* mask,
+                           float* Dvec, void* dqkv, int B, int N, int H, float scale, float drop_p, float* cpart,
+                           hipStream_t s) {
   if (N % 64 != 0) return (int)hipErrorInvalidValue;
   const bool drop = drop_p > 0.f;
   if (drop && mask == nullptr) return (int)hipErrorInvalidValue;
@@ -942,7 +1020,6 @@ extern "C" int uva_attn_bwd(const void* qkv, const void* out, const void* dout, 
   // the dropout scale 1/(1-p) is not applied to dO: dP' = dsc dO V^T, so dS = dsc P (keep dP - D / dsc),
   // i.e. the loops run on the unscaled dO with D' = D / dsc, and dsc goes on dK, dQ, dV once at the
   // end (no scaled dO copy: one [B N H 64] bf16 write + its re-reads per layer saved)
-  (void)workspace;
   (void)rows;
   const int nt = N / 64;
   const uint64_t* MQ = (const uint64_t*)mask;
@@ -955,13 +1032,14 @@ extern "C" int uva_attn_bwd(const void* qkv, const void* out, const void* dout, 
   const bf16* O = (const bf16*)out;
   if (drop) {
     attn_bwd_dq_kernel<true><<<grid, 256, 0, s>>>((const bf16*)qkv, dO, O, lse2, Dvec, MQ, (bf16*)dqkv, N, H, sk, c,
-                                                  1.0f / ds);
-    attn_bwd_dkdv_kernel<true><<<grid, 256, 0, s>>>((const bf16*)qkv, dO, lse2, Dvec, MK, (bf16*)dqkv, N, H, sk, c, ds);
+                                                  1.0f / ds, cpart);
+    attn_bwd_dkdv_kernel<true><<<grid, 256, 0, s>>>((const bf16*)qkv, dO, lse2, Dvec, MK, (bf16*)dqkv, N, H, sk, c, ds,
+                                                    cpart);
   } else {
     attn_bwd_dq_kernel<false><<<grid, 256, 0, s>>>((const bf16*)qkv, dO, O, lse2, Dvec, nullptr, (bf16*)dqkv, N, H,
-                                                   sk, c, 1.0f);
+                                                   sk, c, 1.0f, cpart);
     attn_bwd_dkdv_kernel<false><<<grid, 256, 0, s>>>((const bf16*)qkv, dO, lse2, Dvec, nullptr, (bf16*)dqkv, N, H,
-                                                     sk, c, ds);
+                                                     sk, c, ds, cpart);
   }
   UVA_LAUNCH_CHECK();
   return 0;

@@ -51,7 +51,12 @@ def compute_weight(p):
 def compute_weight_t(p):
     """transposed compute-dtype copy [in, out] of an fp32 [out, in] weight, rebuilt once per
     parameter generation (the optimizer bumps RT.param_gen): the bf16 dX products run on it as
-    forward-layout (K-contiguous) GEMMs"""
+    forward-layout (K-contiguous) GEMMs.  A copy built ahead on RT's side stream (prefetch_weight_t) is
+    waited for on first use."""
+    ev = getattr(p, "_uva_t_event", None)
+    if ev is not None:
+        torch.cuda.current_stream().wait_event(ev)
+        p._uva_t_event = None
     w = compute_weight(p)
     key = (p._version, p.data_ptr(), RT.param_gen)
     t = getattr(p, "_uva_shadow_t", None)
@@ -62,6 +67,33 @@ def compute_weight_t(p):
         p._uva_shadow_t = t
         p._uva_shadow_t_ver = key
     return t
+
+
+def prefetch_weight_t(params, side):
+    """build this step's transposed bf16 weight copies on the side stream `side` (which already waits for the
+    main stream's optimizer step), each with an event its first use waits on: the 4 transposes per Block
+    (~5 us each) run under the VAE encode instead of on the backward's critical path"""
+    if cdt() != torch.bfloat16:
+        return
+    todo = []
+    for p in params:  # compute shadows (a cast only for parameters no ParamStore owns) and targets on main
+        w = compute_weight(p)
+        key = (p._version, p.data_ptr(), RT.param_gen)
+        if getattr(p, "_uva_shadow_t_ver", None) == key and getattr(p, "_uva_t_event", None) is None:
+            continue
+        t = getattr(p, "_uva_shadow_t", None)
+        if t is None or t.shape != (w.shape[1], w.shape[0]):
+            t = torch.empty(w.shape[1], w.shape[0], dtype=w.dtype, device=w.device)  # persistent
+            p._uva_shadow_t = t
+        todo.append((p, w, t, key))
+    side.wait_stream(torch.cuda.current_stream())
+    for p, w, t, key in todo:
+        with torch.cuda.stream(side):
+            ops.transpose_bf16(w, t)
+            ev = torch.cuda.Event()
+            ev.record(side)
+        p._uva_shadow_t_ver = key
+        p._uva_t_event = ev
 
 
 def linear_bias(x, p, b, out):
@@ -401,12 +433,15 @@ class BlockFn(torch.autograd.Function):
         if flash:
             dqkv = torch.empty(M, 3 * D, dtype=c, device=dev)
             dvec = torch.empty(B, H, N, dtype=F32, device=dev)
-            ops.attn_bwd(qkv, o, do, lse, dvec, dqkv, B, N, H, scale, p_attn, seeds[0], mask=Pd)
+            # the qkv bias gradient comes out of the attention backward's epilogues (column partials of dqkv)
+            ops.attn_bwd(qkv, o, do, lse, dvec, dqkv, B, N, H, scale, p_attn, seeds[0], mask=Pd,
+                         dbias=grad_buf(qkvb) if RT.attn_bias_grad else None)
         else:
             dqkv = as_dtype(_attn_mat_bwd(qkv, P, Pd, do, B, N, H, scale, p_attn, seeds[0]), c)
         del do
         ops.linear_dw(dqkv, h1, grad_buf(qkvw))
-        ops.colsum(dqkv, grad_buf(qkvb))
+        if not (flash and RT.attn_bias_grad):
+            ops.colsum(dqkv, grad_buf(qkvb))
         dh1 = torch.empty(M, D, dtype=c if RT.ln_dy_lowp else F32, device=dev)
         linear_dx_w(dqkv, qkvw, dh1)
         del dqkv

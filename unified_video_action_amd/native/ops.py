@@ -534,12 +534,22 @@ def attn_fwd_fp8(ws, out, lse2, B, N, H, scale, drop_p=0.0, seed=0, mask=None, d
     return mask if drop_p > 0 else None
 
 
-def attn_bwd(qkv, out, dout, lse2, dvec, dqkv, B, N, H, scale, drop_p=0.0, seed=0, mask=None):
+def attn_bwd(qkv, out, dout, lse2, dvec, dqkv, B, N, H, scale, drop_p=0.0, seed=0, mask=None, dbias=None,
+             accum_bias=True):
+    """flash attention backward -> dqkv; with `dbias` ([3 H 64] fp32) also the qkv bias gradient (column sums of
+    dqkv as stored) from the kernels' epilogues (uva_attn_bwd_bias)"""
     assert dout.dtype == torch.bfloat16 and dout.is_contiguous() and dqkv.is_contiguous()
     assert dout.numel() == B * N * H * 64 and dqkv.numel() == B * N * 3 * H * 64 and dvec.numel() == B * H * N
     with _traced(f"attn_bwd B{B} N{N} H{H}", 8.0 * B * H * N * N * 64):
         if drop_p > 0 and mask is None:
             mask = attn_dropmask(B, N, H, drop_p, seed, qkv.device)
+        if dbias is not None:
+            assert dbias.dtype == torch.float32 and dbias.numel() == 3 * H * 64 and dbias.is_contiguous()
+            ws = workspace(B * ((N + 127) // 128) * 3 * H * 64, qkv.device)
+            _call("uva_attn_bwd_bias", ptr(qkv), ptr(out), ptr(dout), ptr(lse2), ptr(mask) if drop_p > 0 else None,
+                  ptr(dvec), ptr(dqkv), ptr(dbias), int(accum_bias), ptr(ws), B, N, H, float(scale), float(drop_p),
+                  stream())
+            return
         nb = lib().query("uva_attn_bwd_workspace", B, N, H, float(drop_p))
         ws = torch.empty(nb, dtype=torch.uint8, device=qkv.device) if nb else None
         _call("uva_attn_bwd", ptr(qkv), ptr(out), ptr(dout), ptr(lse2), ptr(mask) if drop_p > 0 else None,

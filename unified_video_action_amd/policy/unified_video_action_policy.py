@@ -272,6 +272,11 @@ class UnifiedVideoActionPolicy(nn.Module):
             if self.use_proprioception:
                 prop = self._second_camera_prop(obs, sel, train=True)
         if self.training and dev.type == "cuda":
+            if getattr(self, "_wt_params", None) is None:
+                from ..model.autoregressive.mar_con_unified import Block
+                self._wt_params = [w for m in self.model.modules() if isinstance(m, Block)
+                                   for w in (m.attn.qkv.weight, m.attn.proj.weight, m.mlp.fc1.weight, m.mlp.fc2.weight)]
+            RT._weight_t_params = self._wt_params  # their transposed bf16 copies are built on the side stream too
             RT.arm_attn_prefetch(dev)  # attention dropout planes under the VAE encode (side stream)
         x = vae_images(img, sel, self.vae_model.CIN_PAD)
         n_half = B * (len(sel) // 2)

@@ -32,6 +32,8 @@ class _Runtime:
         # the epilogue's plane-word loads expose their latency where the hash was issue-bound VALU (fc1 285-296
         # vs 253-271 us, bench 255.2 vs 257.7 samples/s same box, profiles/r06/g8w_planes.txt); kept tested
         self.drop_planes = False
+        # the qkv bias gradient from the attention backward kernels' epilogues (no column-sum pass over dqkv)
+        self.attn_bias_grad = True
         # norm2's LayerNorm backward also emits the proj_drop backward + proj bias gradient (one pass over dx)
         self.ln_bwd_drop = True
         # Mlp backward: dropout + GELU' (+ the fc1 bias gradient) in the epilogue of fc2's dX product (8-wave
@@ -50,6 +52,9 @@ class _Runtime:
         # launch under them vs 78 us alone); from level 2 on the convs are smaller
         self.attn_prefetch_level = 2
         self._prefetch_pending = None
+        # transposed bf16 weights of the Blocks' dX products, built on the side stream with the masks
+        self.weight_t_prefetch = True
+        self._weight_t_params = []
         self._attn_shapes = {}
         self._attn_ready = {}
         self._side = None
@@ -113,6 +118,15 @@ class _Runtime:
             self.prefetch_attn_masks(dev)
 
     def prefetch_attn_masks(self, device):
+        """side-stream work launched under the VAE encode: the attention keep-mask planes of every known Block,
+        then the transposed bf16 weight copies the Blocks' dX products use (registered by the policy)"""
+        self._prefetch_masks(device)
+        if self.weight_t_prefetch and self._weight_t_params and self._side is not None:
+            from .model.autoregressive.functional import prefetch_weight_t
+            self._side.wait_stream(torch.cuda.current_stream(device))
+            prefetch_weight_t(self._weight_t_params, self._side)
+
+    def _prefetch_masks(self, device):
         """Generate every known Block's attention keep-mask planes for this step on a side stream,
         so the VALU-bound mask kernels run under the (MFMA-bound) VAE encode that precedes the MAR.
         Each Block waits on its own event before its attention forward reads the planes."""
