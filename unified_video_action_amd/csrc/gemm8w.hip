@@ -73,7 +73,9 @@ struct G8Epi {
   float dscale;
 };
 
-template <int FM, int FN, int NW, int EPI, int NDEF, typename TC>
+// DM: dropout in the fused epilogues -- 0 none, 1 the counter hash per element, 2 a keep-bit plane (compile-time:
+// runtime branches per segment split the epilogue into small basic blocks the scheduler cannot interleave)
+template <int FM, int FN, int NW, int EPI, int NDEF, typename TC, int DM>
 __global__ __launch_bounds__(64 * NW, 1) void gemm_8w(const bf16* __restrict__ A, const bf16* __restrict__ B,
                                                        TC* __restrict__ C, int M, int N, int K, int lda, int ldb,
                                                        int ldc, G8Epi ep, int w1ok) {
@@ -181,7 +183,7 @@ __global__ __launch_bounds__(64 * NW, 1) void gemm_8w(const bf16* __restrict__ A
                                                      (int)(unsigned)((EPI == 1 || EPI == 3) ? 2ull * M * ldc : cbytes),
                                                      0x00020000);
   float cs[EPI == 3 ? FN / 2 : 1][8];  // EPI 3: the lane's column sums over its fragment rows
-  const bool use_plane = EPI != 0 && ep.plane != nullptr;
+  constexpr bool use_plane = EPI != 0 && DM == 2;
   const auto rsK = __builtin_amdgcn_make_buffer_rsrc((void*)(use_plane ? ep.plane : (const uint32_t*)C), 0,
                                                      (int)(unsigned)(use_plane ? (unsigned long long)M * N / 8 : 4ull),
                                                      0x00020000);
@@ -227,17 +229,18 @@ __global__ __launch_bounds__(64 * NW, 1) void gemm_8w(const bf16* __restrict__ A
     } else if constexpr (EPI == 1) {
       // P stored; GELU + dropout on the bf16 P (autocast: fc1's output is bf16 before the activation)
       const int poff = ok ? (row * ldc + col) * 2 : 0x7fff8000;
-      const uint32_t kb = use_plane ? keep8(ok, row, col) : 0u;
+      uint32_t kb = 0u;
+      if constexpr (use_plane) kb = keep8(ok, row, col);
       __builtin_amdgcn_raw_buffer_store_b128((u32x4){pk[0], pk[1], pk[2], pk[3]}, rsP, poff, 0, 0);
       const unsigned long long idx0 = (unsigned long long)row * (unsigned)N + (unsigned)col;  // flat index (even)
       uint32_t o[4];
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         float a0 = gelu_erf(bf_lo(pk[j])), a1 = gelu_erf(bf_hi(pk[j]));
-        if (use_plane) {
+        if constexpr (DM == 2) {
           a0 = (kb >> (2 * j)) & 1u ? a0 * ep.dscale : 0.f;
           a1 = (kb >> (2 * j + 1)) & 1u ? a1 * ep.dscale : 0.f;
-        } else if (ep.thresh) {
+        } else if constexpr (DM == 1) {
           const uint32_t h = drop_hash(ep.key, (idx0 >> 1) + j);
           a0 = (h & 0xFFFFu) >= ep.thresh ? a0 * ep.dscale : 0.f;
           a1 = (h >> 16) >= ep.thresh ? a1 * ep.dscale : 0.f;
@@ -249,16 +252,17 @@ __global__ __launch_bounds__(64 * NW, 1) void gemm_8w(const bf16* __restrict__ A
       // dA (bf16) -> dropout -> x GELU'(P) -> bf16; column sums of the stored values
       const int poff = ok ? (row * ldc + col) * 2 : 0x7fff8000;
       const u32x4 pp = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rsP, poff, 0, 0));
-      const uint32_t kb = use_plane ? keep8(ok, row, col) : 0u;
+      uint32_t kb = 0u;
+      if constexpr (use_plane) kb = keep8(ok, row, col);
       const unsigned long long idx0 = (unsigned long long)row * (unsigned)N + (unsigned)col;
       uint32_t o[4];
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         float d0 = bf_lo(pk[j]), d1 = bf_hi(pk[j]);
-        if (use_plane) {
+        if constexpr (DM == 2) {
           d0 = (kb >> (2 * j)) & 1u ? d0 * ep.dscale : 0.f;
           d1 = (kb >> (2 * j + 1)) & 1u ? d1 * ep.dscale : 0.f;
-        } else if (ep.thresh) {
+        } else if constexpr (DM == 1) {
           const uint32_t h = drop_hash(ep.key, (idx0 >> 1) + j);
           d0 = (h & 0xFFFFu) >= ep.thresh ? d0 * ep.dscale : 0.f;
           d1 = (h >> 16) >= ep.thresh ? d1 * ep.dscale : 0.f;
@@ -272,16 +276,17 @@ __global__ __launch_bounds__(64 * NW, 1) void gemm_8w(const bf16* __restrict__ A
     } else {
       const f32x4 r0 = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rsR, voff, 0, 0));
       const f32x4 r1 = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rsR, voff + 16, 0, 0));
-      const uint32_t kb = use_plane ? keep8(ok, row, col) : 0u;
+      uint32_t kb = 0u;
+      if constexpr (use_plane) kb = keep8(ok, row, col);
       const unsigned long long idx0 = (unsigned long long)row * (unsigned)N + (unsigned)col;
       float o[8];
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         float a0 = bf_lo(pk[j]), a1 = bf_hi(pk[j]);
-        if (use_plane) {
+        if constexpr (DM == 2) {
           a0 = (kb >> (2 * j)) & 1u ? a0 * ep.dscale : 0.f;
           a1 = (kb >> (2 * j + 1)) & 1u ? a1 * ep.dscale : 0.f;
-        } else if (ep.thresh) {
+        } else if constexpr (DM == 1) {
           const uint32_t h = drop_hash(ep.key, (idx0 >> 1) + j);
           a0 = (h & 0xFFFFu) >= ep.thresh ? a0 * ep.dscale : 0.f;
           a1 = (h >> 16) >= ep.thresh ? a1 * ep.dscale : 0.f;
@@ -518,8 +523,8 @@ static int g8_cus() {
 static int g_gemm8w_on = 0;        // plain products (measurement switch; the fused forms are called directly)
 static int g_gemm8w_mode = 0;     // bit 1: 64 x 64 wave tiles; bits 2..4: deferred rows (64 x 64 only: 4)
 
-template <int FN, int EPI, int NDEF, typename TC>
-static int g8_launch(const void* A, const void* B, void* C, int M, int N, int K, int lda, int ldb, int ldc,
+template <int FN, int EPI, int NDEF, typename TC, int DM>
+static int g8_launch1(const void* A, const void* B, void* C, int M, int N, int K, int lda, int ldb, int ldc,
                      const G8Epi& ep, hipStream_t s) {
   using G = G8Cfg<4, FN, 8>;
   const int tn = (N + G::BN - 1) / G::BN;
@@ -528,15 +533,28 @@ static int g8_launch(const void* A, const void* B, void* C, int M, int N, int K,
   const int lds = G::RING + (ep.bias ? tn * G::BN * 4 : 0);
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute((const void*)gemm_8w<4, FN, 8, EPI, NDEF, TC>,
+    (void)hipFuncSetAttribute((const void*)gemm_8w<4, FN, 8, EPI, NDEF, TC, DM>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
     attr = true;
   }
   const int w1ok = (M % G::BM == 0) && (N % G::BN == 0);
-  gemm_8w<4, FN, 8, EPI, NDEF, TC><<<dim3(grid), 512, lds, s>>>((const bf16*)A, (const bf16*)B, (TC*)C, M, N, K,
+  gemm_8w<4, FN, 8, EPI, NDEF, TC, DM><<<dim3(grid), 512, lds, s>>>((const bf16*)A, (const bf16*)B, (TC*)C, M, N, K,
                                                                  lda, ldb, ldc, ep, w1ok);
   UVA_LAUNCH_CHECK();
   return 0;
+}
+
+// the dropout form is a template parameter (DM): none for plain products / p = 0, else hash or plane
+template <int FN, int EPI, int NDEF, typename TC>
+static int g8_launch(const void* A, const void* B, void* C, int M, int N, int K, int lda, int ldb, int ldc,
+                     const G8Epi& ep, hipStream_t s) {
+  if constexpr (EPI == 0) {
+    return g8_launch1<FN, EPI, NDEF, TC, 0>(A, B, C, M, N, K, lda, ldb, ldc, ep, s);
+  } else {
+    if (!ep.thresh) return g8_launch1<FN, EPI, NDEF, TC, 0>(A, B, C, M, N, K, lda, ldb, ldc, ep, s);
+    if (ep.plane) return g8_launch1<FN, EPI, NDEF, TC, 2>(A, B, C, M, N, K, lda, ldb, ldc, ep, s);
+    return g8_launch1<FN, EPI, NDEF, TC, 1>(A, B, C, M, N, K, lda, ldb, ldc, ep, s);
+  }
 }
 
 // deferred rows ride in the peeled groups 0 (1 .. 2 rows) and 1 (3 .. 4 rows) of the next tile, neither of
@@ -551,6 +569,8 @@ static int g8_dispatch(const void* A, const void* B, void* C, int M, int N, int 
   const int nd = (EPI == 0 && sizeof(TC) == 4) ? 0 : (g_gemm8w_mode >> 2) & 7;
 #define G8L(FN_, ND_) g8_launch<FN_, EPI, ND_, TC>(A, B, C, M, N, K, lda, ldb, ldc, ep, s)
   if (g_gemm8w_mode & 2) return (nd && K / 128 >= 3) ? G8L(4, 4) : G8L(4, 0);
+  // 64 x 96 tiles with 1 or 2 deferred rows spill 7-50 VGPRs and measured no faster on the fused Mlp
+  // epilogues (profiles/r06/g8w_dm.txt): the wide tile always finishes its rows immediately
   return G8L(6, 0);
 #undef G8L
 }
