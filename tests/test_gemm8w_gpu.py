@@ -28,6 +28,19 @@ def _lib():
     ops.gemm8w_set(*prev)
 
 
+# gemm_8w launch forms: 64 one 8-wave workgroup per CU (256 x 192 tiles), 32 two 4-wave workgroups per CU
+# (128 x 192 tiles, bias from L2); the default (0) picks one of them per product
+FORMS = [64, 32]
+
+
+@pytest.fixture(params=FORMS)
+def form(request):
+    from unified_video_action_amd.native import ops
+    prev = ops.gemm8w_set(-2, request.param)
+    yield request.param
+    ops.gemm8w_set(-2, prev[1])
+
+
 def _rand(M, N, scale=1.0, dtype=torch.bfloat16, g=None):
     return ((torch.rand(M, N, device=DEV, generator=g) * 2 - 1) * scale).to(dtype)
 
@@ -37,7 +50,7 @@ SHAPES = [(32768, 3072, 768), (4096, 768, 3072), (1000, 776, 384), (300, 200, 25
 
 @pytest.mark.parametrize("p", [0.0, 0.1])
 @pytest.mark.parametrize("M,N,K", SHAPES)
-def test_fc1_gelu_drop_bit_exact_vs_split(M, N, K, p):
+def test_fc1_gelu_drop_bit_exact_vs_split(M, N, K, p, form):
     from unified_video_action_amd.native import ops
     g = torch.Generator(device=DEV).manual_seed(M + N + K)
     x, w = _rand(M, K, g=g), _rand(N, K, 0.1, g=g)
@@ -57,7 +70,7 @@ def test_fc1_gelu_drop_bit_exact_vs_split(M, N, K, p):
 
 @pytest.mark.parametrize("p", [0.0, 0.1])
 @pytest.mark.parametrize("M,N,K", [(32768, 768, 3072), (32768, 768, 768), (1000, 776, 384), (300, 200, 256)])
-def test_fc2_drop_residual_bit_exact_vs_split(M, N, K, p):
+def test_fc2_drop_residual_bit_exact_vs_split(M, N, K, p, form):
     from unified_video_action_amd.native import ops
     g = torch.Generator(device=DEV).manual_seed(7 * M + N + K)
     h, w = _rand(M, K, g=g), _rand(N, K, 0.05, g=g)
@@ -74,7 +87,7 @@ def test_fc2_drop_residual_bit_exact_vs_split(M, N, K, p):
 
 @pytest.mark.parametrize("p", [0.0, 0.1])
 @pytest.mark.parametrize("M,N,K", [(32768, 3072, 768), (1000, 776, 384), (300, 200, 256)])
-def test_dgelu_drop_bit_exact_vs_split(M, N, K, p):
+def test_dgelu_drop_bit_exact_vs_split(M, N, K, p, form):
     """fc2's dX product with dropout + GELU' in the epilogue and the fc1 bias gradient as column partials"""
     from unified_video_action_amd.native import ops
     g = torch.Generator(device=DEV).manual_seed(3 * M + N + K)
@@ -97,7 +110,7 @@ def test_dgelu_drop_bit_exact_vs_split(M, N, K, p):
     assert (db_f - db_s).abs().max().item() < 1e-5 * scale
 
 
-@pytest.mark.parametrize("mode", [0, 2 | (4 << 2)])
+@pytest.mark.parametrize("mode", [0, 2 | (4 << 2), 32])
 @pytest.mark.parametrize("odt", [torch.bfloat16, torch.float32])
 @pytest.mark.parametrize("M,N,K", SHAPES + [(32768, 768, 768)])
 def test_plain_8w_bit_exact_vs_gemm4(M, N, K, odt, mode):

@@ -11,7 +11,7 @@ from unified_video_action_amd.native import ops  # noqa: E402
 
 SHAPES = [("qkv fwd", 2304, 768), ("fc1 fwd", 3072, 768), ("fc2 fwd", 768, 3072), ("dX N768 K768", 768, 768),
           ("fc1 dX N768 K3072", 768, 3072)]
-MODES = {"6imm": 0, "4def": 2 | (4 << 2)}
+MODES = {"nw8": 64, "nw4": 32}
 
 
 def timeit(fn, iters=20):

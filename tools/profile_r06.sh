@@ -1,14 +1,14 @@
 #!/bin/bash
-# Round-5 end profile (tools only).  All files under profiles/<tag>/ come from THIS run:
+# End-of-round profile (tools only).  All files under profiles/<tag>/ come from THIS run:
 #   kernel_stats.csv / kernel_stats_by_grid.csv / trace_rows.json / bench.json : rocprofv3 --kernel-trace --stats
 #       of the default bench command (headline + the other-config lines), bench's own HIP-event rows beside it
 #   kernel_stats_headline_only.csv / step_gaps.txt : a headline-only traced run (busy / idle per optimizer step)
 #   traffic.json : FETCH_SIZE / WRITE_SIZE passes (separate runs, no tracing domains), per traced tag
 #   mfma_busy.json : SQ_VALU_MFMA_BUSY_CYCLES pass (tools/pmc_step.sh)
-# bash tools/profile_r05.sh <tag>
+# bash tools/profile_r06.sh <tag>
 set -e
 set -o pipefail
-TAG=${1:-r05_end}
+TAG=${1:-r06_end}
 export TMPDIR=/tmp
 OUT=gpurun_out/prof_$TAG
 mkdir -p $OUT

@@ -33,6 +33,11 @@ typedef __attribute__((ext_vector_type(4))) unsigned u32x4;
 #ifndef UVA_G8_DBG
 #define UVA_G8_DBG 0
 #endif
+// 1: EPI 3 row inputs (the saved pre-activation) loaded one fragment row ahead; 0: each segment loads its own just
+// before use.  (EPI 2's residual rows ahead measured no faster: fc2 157 vs 154 us, profiles/r06/g8w_prefetch.txt)
+#ifndef UVA_G8_PREFETCH
+#define UVA_G8_PREFETCH 1
+#endif
 
 namespace {
 
@@ -75,8 +80,11 @@ struct G8Epi {
 
 // DM: dropout in the fused epilogues -- 0 none, 1 the counter hash per element, 2 a keep-bit plane (compile-time:
 // runtime branches per segment split the epilogue into small basic blocks the scheduler cannot interleave)
+// NW = 8: one workgroup per CU (two waves per SIMD in lockstep: both reach the epilogue together), the bias
+// row in LDS.  NW = 4: a 128 x 192 block tile, two independent workgroups per CU (80 KB of ring each: the
+// bias comes from L2 instead), so one workgroup's epilogue can run beside the other's MFMA loop.
 template <int FM, int FN, int NW, int EPI, int NDEF, typename TC, int DM>
-__global__ __launch_bounds__(64 * NW, 1) void gemm_8w(const bf16* __restrict__ A, const bf16* __restrict__ B,
+__global__ __launch_bounds__(64 * NW, 8 / NW) void gemm_8w(const bf16* __restrict__ A, const bf16* __restrict__ B,
                                                        TC* __restrict__ C, int M, int N, int K, int lda, int ldb,
                                                        int ldc, G8Epi ep, int w1ok) {
   using G = G8Cfg<FM, FN, NW>;
@@ -101,7 +109,10 @@ __global__ __launch_bounds__(64 * NW, 1) void gemm_8w(const bf16* __restrict__ A
 
   float* sbias = (float*)(smem + G::RING);
   const bool has_bias = ep.bias != nullptr;
-  if (has_bias) {
+  constexpr bool LDS_BIAS = NW == 8;
+  const auto rsBias = __builtin_amdgcn_make_buffer_rsrc((void*)(has_bias ? ep.bias : (const float*)A), 0,
+                                                        has_bias ? 4 * N : 0, 0x00020000);
+  if (LDS_BIAS && has_bias) {
     for (int i = threadIdx.x; i < tn * G::BN; i += 64 * NW) sbias[i] = i < N ? ep.bias[i] : 0.f;
     __syncthreads();
   }
@@ -204,9 +215,16 @@ __global__ __launch_bounds__(64 * NW, 1) void gemm_8w(const bf16* __restrict__ A
       v[4 + q] = __uint_as_float(x[1]);
     }
     if (has_bias) {
-      const float4 x0 = *(const float4*)(sbias + n0 + wc * (FN * 16) + p * 32 + csub);
-      const float4 x1 = *(const float4*)(sbias + n0 + wc * (FN * 16) + p * 32 + csub + 4);
-      const float bv[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
+      f32x4 x0, x1;
+      if constexpr (LDS_BIAS) {
+        x0 = *(const f32x4*)(sbias + n0 + wc * (FN * 16) + p * 32 + csub);
+        x1 = *(const f32x4*)(sbias + n0 + wc * (FN * 16) + p * 32 + csub + 4);
+      } else {  // columns past N read zeros (buffer range)
+        const int bo = (n0 + wc * (FN * 16) + p * 32 + csub) * 4;
+        x0 = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rsBias, bo, 0, 0));
+        x1 = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rsBias, bo + 16, 0, 0));
+      }
+      const float bv[8] = {x0[0], x0[1], x0[2], x0[3], x1[0], x1[1], x1[2], x1[3]};
 #pragma unroll
       for (int e = 0; e < 8; ++e) v[e] = fmaf(ep.alpha, v[e], bv[e]);
     } else {
@@ -216,7 +234,40 @@ __global__ __launch_bounds__(64 * NW, 1) void gemm_8w(const bf16* __restrict__ A
   };
   // final values of one (row, 8 columns) segment -> stores.  pk: the 8 outputs as bf16 (EPI 0 bf16 / 1 / 2)
   // or the fp32 v (EPI 0 fp32)
-  auto finish = [&](int row, int col, int pi, const uint32_t (&pk)[4], const float (&v)[8]) __attribute__((always_inline)) {
+  // a segment's row inputs -- EPI 3: the saved pre-activation (a); EPI 2: the fp32 residual (a, b) -- loaded one
+  // fragment row ahead of their use (prefetch_in)
+  struct RowIn {
+    u32x4 a, b;
+  };
+  auto load_in = [&](int row, int col) __attribute__((always_inline)) -> RowIn {
+    RowIn r{};
+    const bool ok = row < M && col < N;
+    if constexpr (EPI == 3) {
+      r.a = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rsP, ok ? (row * ldc + col) * 2 : 0x7fff8000, 0, 0));
+    } else if constexpr (EPI == 2) {
+      const int voff = ok ? (row * ldc + col) * (int)sizeof(TC) : 0x7fff8000;
+      r.a = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rsR, voff, 0, 0));
+      r.b = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rsR, voff + 16, 0, 0));
+    }
+    return r;
+  };
+  // the counter hash's first word for the segment's first pair: its flat index row * N + col is a multiple of 8
+  // (col % 8 == 0, N % 8 == 0), so pairs p0 + j (j < 4) differ from p0 in the low two bits only and their first
+  // words are x0 ^ j (common.h drop_first)
+  auto seg_hash0 = [&](int row, int col) __attribute__((always_inline)) -> uint32_t {
+    return drop_first(ep.key, ((unsigned long long)row * (unsigned)N + (unsigned)col) >> 1);
+  };
+  // keep ? v * dscale : +0 without a branch: left to itself hipcc sank the GELU into an exec-masked block per
+  // element (48 s_cbranch_execz per tile row set in the fc1 epilogue); the empty asm pins v as computed
+  auto drop_sel = [&](float v, bool keep) __attribute__((always_inline)) -> float {
+    float x = v * ep.dscale;
+    asm volatile("" : "+v"(x));
+    return keep ? x : 0.f;
+  };
+  // (have_in false: the deferred rows, which load their inputs here)
+  auto finish = [&](int row, int col, int pi, const uint32_t (&pk)[4], const float (&v)[8], const RowIn& in_,
+                    bool have_in) __attribute__((always_inline)) {
+    const RowIn in = have_in ? in_ : load_in(row, col);
     const bool ok = row < M && col < N;
     const int voff = ok ? (row * ldc + col) * (int)sizeof(TC) : 0x7fff8000;
     if constexpr (EPI == 0) {
@@ -232,7 +283,7 @@ __global__ __launch_bounds__(64 * NW, 1) void gemm_8w(const bf16* __restrict__ A
       uint32_t kb = 0u;
       if constexpr (use_plane) kb = keep8(ok, row, col);
       __builtin_amdgcn_raw_buffer_store_b128((u32x4){pk[0], pk[1], pk[2], pk[3]}, rsP, poff, 0, 0);
-      const unsigned long long idx0 = (unsigned long long)row * (unsigned)N + (unsigned)col;  // flat index (even)
+      const uint32_t x0 = seg_hash0(row, col);
       uint32_t o[4];
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
@@ -241,9 +292,9 @@ __global__ __launch_bounds__(64 * NW, 1) void gemm_8w(const bf16* __restrict__ A
           a0 = (kb >> (2 * j)) & 1u ? a0 * ep.dscale : 0.f;
           a1 = (kb >> (2 * j + 1)) & 1u ? a1 * ep.dscale : 0.f;
         } else if constexpr (DM == 1) {
-          const uint32_t h = drop_hash(ep.key, (idx0 >> 1) + j);
-          a0 = (h & 0xFFFFu) >= ep.thresh ? a0 * ep.dscale : 0.f;
-          a1 = (h >> 16) >= ep.thresh ? a1 * ep.dscale : 0.f;
+          const uint32_t h = drop_mix(x0 ^ (uint32_t)j);
+          a0 = drop_sel(a0, (h & 0xFFFFu) >= ep.thresh);
+          a1 = drop_sel(a1, (h >> 16) >= ep.thresh);
         }
         o[j] = pk_bf16(a0, a1);
       }
@@ -251,10 +302,10 @@ __global__ __launch_bounds__(64 * NW, 1) void gemm_8w(const bf16* __restrict__ A
     } else if constexpr (EPI == 3) {
       // dA (bf16) -> dropout -> x GELU'(P) -> bf16; column sums of the stored values
       const int poff = ok ? (row * ldc + col) * 2 : 0x7fff8000;
-      const u32x4 pp = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rsP, poff, 0, 0));
+      const u32x4 pp = in.a;
       uint32_t kb = 0u;
       if constexpr (use_plane) kb = keep8(ok, row, col);
-      const unsigned long long idx0 = (unsigned long long)row * (unsigned)N + (unsigned)col;
+      const uint32_t x0 = seg_hash0(row, col);
       uint32_t o[4];
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
@@ -263,7 +314,7 @@ __global__ __launch_bounds__(64 * NW, 1) void gemm_8w(const bf16* __restrict__ A
           d0 = (kb >> (2 * j)) & 1u ? d0 * ep.dscale : 0.f;
           d1 = (kb >> (2 * j + 1)) & 1u ? d1 * ep.dscale : 0.f;
         } else if constexpr (DM == 1) {
-          const uint32_t h = drop_hash(ep.key, (idx0 >> 1) + j);
+          const uint32_t h = drop_mix(x0 ^ (uint32_t)j);
           d0 = (h & 0xFFFFu) >= ep.thresh ? d0 * ep.dscale : 0.f;
           d1 = (h >> 16) >= ep.thresh ? d1 * ep.dscale : 0.f;
         }
@@ -274,11 +325,10 @@ __global__ __launch_bounds__(64 * NW, 1) void gemm_8w(const bf16* __restrict__ A
       __builtin_amdgcn_raw_buffer_store_b128((u32x4){o[0], o[1], o[2], o[3]}, rsC, poff, 0, 0);
       if (UVA_G8_DBG & 2) asm volatile("s_nop 7\n s_nop 7" ::: "memory");
     } else {
-      const f32x4 r0 = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rsR, voff, 0, 0));
-      const f32x4 r1 = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rsR, voff + 16, 0, 0));
+      const f32x4 r0 = __builtin_bit_cast(f32x4, in.a), r1 = __builtin_bit_cast(f32x4, in.b);
       uint32_t kb = 0u;
       if constexpr (use_plane) kb = keep8(ok, row, col);
-      const unsigned long long idx0 = (unsigned long long)row * (unsigned)N + (unsigned)col;
+      const uint32_t x0 = seg_hash0(row, col);
       float o[8];
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
@@ -287,9 +337,9 @@ __global__ __launch_bounds__(64 * NW, 1) void gemm_8w(const bf16* __restrict__ A
           a0 = (kb >> (2 * j)) & 1u ? a0 * ep.dscale : 0.f;
           a1 = (kb >> (2 * j + 1)) & 1u ? a1 * ep.dscale : 0.f;
         } else if constexpr (DM == 1) {
-          const uint32_t h = drop_hash(ep.key, (idx0 >> 1) + j);
-          a0 = (h & 0xFFFFu) >= ep.thresh ? a0 * ep.dscale : 0.f;
-          a1 = (h >> 16) >= ep.thresh ? a1 * ep.dscale : 0.f;
+          const uint32_t h = drop_mix(x0 ^ (uint32_t)j);
+          a0 = drop_sel(a0, (h & 0xFFFFu) >= ep.thresh);
+          a1 = drop_sel(a1, (h >> 16) >= ep.thresh);
         }
         o[2 * j] = a0;
         o[2 * j + 1] = a1;
@@ -303,7 +353,8 @@ __global__ __launch_bounds__(64 * NW, 1) void gemm_8w(const bf16* __restrict__ A
   auto seg_row = [&](int m0, int f) __attribute__((always_inline)) { return m0 + wr * (FM * 16) + f * 16 + lrow; };
   auto seg_col = [&](int n0, int p) __attribute__((always_inline)) { return n0 + wc * (FN * 16) + p * 32 + csub; };
   // immediate epilogue of one fragment row
-  auto epi_row = [&](int f, int m0, int n0) __attribute__((always_inline)) {
+  constexpr bool PF = EPI == 3 && UVA_G8_PREFETCH;
+  auto epi_row = [&](int f, int m0, int n0, const RowIn (&in_row)[FN / 2]) __attribute__((always_inline)) {
 #pragma unroll
     for (int p = 0; p < FN / 2; ++p) {
       float v[8];
@@ -311,7 +362,16 @@ __global__ __launch_bounds__(64 * NW, 1) void gemm_8w(const bf16* __restrict__ A
       uint32_t pk[4];
 #pragma unroll
       for (int j = 0; j < 4; ++j) pk[j] = pk_bf16(v[2 * j], v[2 * j + 1]);
-      finish(seg_row(m0, f), seg_col(n0, p), p, pk, v);
+      finish(seg_row(m0, f), seg_col(n0, p), p, pk, v, in_row[p], PF);
+    }
+  };
+  // EPI 3 loads row f + 1's inputs before finishing row f (the wave otherwise sits in s_waitcnt for each
+  // segment's load: SQ_WAIT_ANY 0.47 of the kernel's cycles, profiles/r06/g8w_pmc.txt; 234 vs 255 us)
+  RowIn in_buf[2][FN / 2];
+  auto prefetch_in = [&](int f, int m0, int n0) __attribute__((always_inline)) {
+    if constexpr (PF) {
+#pragma unroll
+      for (int p = 0; p < FN / 2; ++p) in_buf[f & 1][p] = load_in(seg_row(m0, f), seg_col(n0, p));
     }
   };
   // deferred epilogue: the last NDEF fragment rows of a tile are packed to bf16 (every EPI form rounds there
@@ -343,7 +403,7 @@ __global__ __launch_bounds__(64 * NW, 1) void gemm_8w(const bf16* __restrict__ A
           v[2 * j] = bf_lo(pend[d][p][j]);
           v[2 * j + 1] = bf_hi(pend[d][p][j]);
         }
-        finish(seg_row(pm0, F0 + d), seg_col(pn0, p), p, pend[d][p], v);
+        finish(seg_row(pm0, F0 + d), seg_col(pn0, p), p, pend[d][p], v, in_buf[0][0], false);
       }
     }
   };
@@ -459,17 +519,19 @@ __global__ __launch_bounds__(64 * NW, 1) void gemm_8w(const bf16* __restrict__ A
 #pragma unroll
         for (int e = 0; e < 8; ++e) cs[p][e] = 0.f;
     }
+    prefetch_in(0, m0, n0);
 #pragma unroll
     for (int f = 0; f < F0; ++f) {
       __builtin_amdgcn_sched_barrier(0);
-      epi_row(f, m0, n0);
+      if (f + 1 < F0) prefetch_in(f + 1, m0, n0);
+      epi_row(f, m0, n0, in_buf[f & 1]);
     }
     if (UVA_G8_DBG & 4) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     if constexpr (EPI == 3 && !(UVA_G8_DBG & 1)) {
       // the wave's 64-row column sums: over the 16 row lanes of each DPP row (lane & 15), stored by lane 0
       // of each row group to part[(m0 + 64 wr) / 64][col] (every wave stores: rows past M contributed zeros)
       const auto rsS = __builtin_amdgcn_make_buffer_rsrc((void*)ep.part, 0,
-                                                         (int)(unsigned)(4ull * (unsigned)(tm * 4) * (unsigned)N), 0x00020000);
+                                                         (int)(unsigned)(4ull * (unsigned)(tm * (G::BM / 64)) * (unsigned)N), 0x00020000);
 #pragma unroll
       for (int p = 0; p < FN / 2; ++p) {
         f32x4 s0, s1;
@@ -521,39 +583,46 @@ static int g8_cus() {
 }
 
 static int g_gemm8w_on = 0;        // plain products (measurement switch; the fused forms are called directly)
-static int g_gemm8w_mode = 0;     // bit 1: 64 x 64 wave tiles; bits 2..4: deferred rows (64 x 64 only: 4)
+static int g_gemm8w_mode = 0;     // bit 1: 64 x 64 wave tiles; bits 2..4: deferred rows (64 x 64 only: 4);
+                                  // bit 5 / 6: every product on two 4-wave workgroups per CU (NW = 4) / on
+                                  // one 8-wave workgroup (NW = 8); neither: EPI 3 on NW = 4, the rest NW = 8
+                                  // (fc2 dX + GELU' 222-232 vs 230-237 us, fc1 + GELU 247-250 vs 235-242,
+                                  // profiles/r06/g8w_nw4_final.txt)
 
-template <int FN, int EPI, int NDEF, typename TC, int DM>
+template <int FN, int EPI, int NDEF, typename TC, int DM, int NW>
 static int g8_launch1(const void* A, const void* B, void* C, int M, int N, int K, int lda, int ldb, int ldc,
                      const G8Epi& ep, hipStream_t s) {
-  using G = G8Cfg<4, FN, 8>;
+  using G = G8Cfg<4, FN, NW>;
   const int tn = (N + G::BN - 1) / G::BN;
   const long long tiles = (long long)((M + G::BM - 1) / G::BM) * tn;
-  const int grid = (int)std::min<long long>(tiles, g8_cus());
-  const int lds = G::RING + (ep.bias ? tn * G::BN * 4 : 0);
+  const int grid = (int)std::min<long long>(tiles, (long long)g8_cus() * (8 / NW));
+  const int lds = G::RING + (NW == 8 && ep.bias ? tn * G::BN * 4 : 0);
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute((const void*)gemm_8w<4, FN, 8, EPI, NDEF, TC, DM>,
-                              hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
+    (void)hipFuncSetAttribute((const void*)gemm_8w<4, FN, NW, EPI, NDEF, TC, DM>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, NW == 8 ? 163840 : G::RING);
     attr = true;
   }
   const int w1ok = (M % G::BM == 0) && (N % G::BN == 0);
-  gemm_8w<4, FN, 8, EPI, NDEF, TC, DM><<<dim3(grid), 512, lds, s>>>((const bf16*)A, (const bf16*)B, (TC*)C, M, N, K,
-                                                                 lda, ldb, ldc, ep, w1ok);
+  gemm_8w<4, FN, NW, EPI, NDEF, TC, DM><<<dim3(grid), 64 * NW, lds, s>>>((const bf16*)A, (const bf16*)B, (TC*)C, M, N,
+                                                                       K, lda, ldb, ldc, ep, w1ok);
   UVA_LAUNCH_CHECK();
   return 0;
 }
+// rows of EPI 3 column-sum partials the launch writes (every wave of every row tile stores its 64 rows)
+static bool g8_nw4(int epi) { return (g_gemm8w_mode & 32) || (!(g_gemm8w_mode & 64) && epi == 3); }
+static int g8_part_rows(int M) { return g8_nw4(3) ? (M + 127) / 128 * 2 : (M + 255) / 256 * 4; }
 
 // the dropout form is a template parameter (DM): none for plain products / p = 0, else hash or plane
-template <int FN, int EPI, int NDEF, typename TC>
+template <int FN, int EPI, int NDEF, typename TC, int NW = 8>
 static int g8_launch(const void* A, const void* B, void* C, int M, int N, int K, int lda, int ldb, int ldc,
                      const G8Epi& ep, hipStream_t s) {
   if constexpr (EPI == 0) {
-    return g8_launch1<FN, EPI, NDEF, TC, 0>(A, B, C, M, N, K, lda, ldb, ldc, ep, s);
+    return g8_launch1<FN, EPI, NDEF, TC, 0, NW>(A, B, C, M, N, K, lda, ldb, ldc, ep, s);
   } else {
-    if (!ep.thresh) return g8_launch1<FN, EPI, NDEF, TC, 0>(A, B, C, M, N, K, lda, ldb, ldc, ep, s);
-    if (ep.plane) return g8_launch1<FN, EPI, NDEF, TC, 2>(A, B, C, M, N, K, lda, ldb, ldc, ep, s);
-    return g8_launch1<FN, EPI, NDEF, TC, 1>(A, B, C, M, N, K, lda, ldb, ldc, ep, s);
+    if (!ep.thresh) return g8_launch1<FN, EPI, NDEF, TC, 0, NW>(A, B, C, M, N, K, lda, ldb, ldc, ep, s);
+    if (ep.plane) return g8_launch1<FN, EPI, NDEF, TC, 2, NW>(A, B, C, M, N, K, lda, ldb, ldc, ep, s);
+    return g8_launch1<FN, EPI, NDEF, TC, 1, NW>(A, B, C, M, N, K, lda, ldb, ldc, ep, s);
   }
 }
 
@@ -568,6 +637,7 @@ static int g8_dispatch(const void* A, const void* B, void* C, int M, int N, int 
   // (deferred rows are held as bf16: a plain fp32-output product finishes every row at once)
   const int nd = (EPI == 0 && sizeof(TC) == 4) ? 0 : (g_gemm8w_mode >> 2) & 7;
 #define G8L(FN_, ND_) g8_launch<FN_, EPI, ND_, TC>(A, B, C, M, N, K, lda, ldb, ldc, ep, s)
+  if (g_gemm8w_mode & 32) return g8_launch<6, EPI, 0, TC, 4>(A, B, C, M, N, K, lda, ldb, ldc, ep, s);
   if (g_gemm8w_mode & 2) return (nd && K / 128 >= 3) ? G8L(4, 4) : G8L(4, 0);
   // 64 x 96 tiles with 1 or 2 deferred rows spill 7-50 VGPRs and measured no faster on the fused Mlp
   // epilogues (profiles/r06/g8w_dm.txt): the wide tile always finishes its rows immediately
@@ -643,9 +713,10 @@ extern "C" int uva_linear_dgelu_drop(const void* dY, const void* Wt, const void*
   uva_drop_params(drop_p, &th, &ds);
   if (plane && (N % 32 || !th || ((uintptr_t)plane % 4))) return (int)-hipErrorInvalidValue;
   G8Epi ep{nullptr, 1.f, (void*)pre, nullptr, part, (const uint32_t*)plane, th ? g8_key(seed) : 0u, th, ds};
-  int r = g8_launch<6, 3, 0, bf16>(dY, Wt, dpre, M, N, K, K, K, N, ep, s);
+  int r = g8_nw4(3) ? g8_launch<6, 3, 0, bf16, 4>(dY, Wt, dpre, M, N, K, K, K, N, ep, s)
+                                : g8_launch<6, 3, 0, bf16>(dY, Wt, dpre, M, N, K, K, K, N, ep, s);
   if (r) return -r;
-  r = uva_colsum_final_launch(part, (M + 255) / 256 * 4, N, dbias, accum_bias, s);
+  r = uva_colsum_final_launch(part, g8_part_rows(M), N, dbias, accum_bias, s);
   return r ? -r : 1;
 }
 
