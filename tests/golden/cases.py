@@ -286,7 +286,10 @@ def trace_rng(step, B=POLICY_B):
 
 # ---- policy-level Libero / UMI cases (config 4 / 5 plumbing through compute_loss) ----------
 POLICY_VARIANT_MODES = {"libero": ["full_dynamic_model", "policy_model"],
-                        "umi": ["full_dynamic_model", "policy_model"]}
+                        "umi": ["full_dynamic_model", "policy_model"],
+                        # toolhang's second camera through the policy: wrist frames VAE-encoded with their own
+                        # posterior draws (vae_eps_wrist), eef / gripper streams split into history / future
+                        "toolhang_prop": ["full_dynamic_model"]}
 
 
 def umi_img_indices(tag, B):
@@ -314,6 +317,13 @@ def ref_language_latents(B, start=0):
 def policy_variant_batch(variant, B=POLICY_B):
     """Libero / UMI batches; the language latents are the reference's own CLIP latents (G6)."""
     tag = f"policy/{variant}"
+    if variant == "toolhang_prop":
+        obs = {"sideview_image": (hash_tensor(tag + "/img", (B, 32, 3, 128, 128)) + 1.0) * 0.5,
+               "robot0_eye_in_hand_image": (hash_tensor(tag + "/wrist", (B, 32, 3, 128, 128)) + 1.0) * 0.5}
+        for k, d in (("robot0_eef_pos", 3), ("robot0_eef_quat", 4), ("robot0_gripper_qpos", 2)):
+            obs[k] = hash_normal(f"{tag}/{k}", (B, 32, d))
+        return {"obs": obs, "action": hash_tensor(tag + "/action", (B, 32, 10)),
+                "language_latents": ref_language_latents(B, 2)}
     if variant == "libero":
         return {"obs": {"agentview_rgb": (hash_tensor(tag + "/img", (B, 32, 3, 128, 128)) + 1.0) * 0.5},
                 "action": hash_tensor(tag + "/action", (B, 32, 10)),
@@ -333,6 +343,10 @@ def policy_variant_rng(variant, mode, B=POLICY_B):
     r["vae_eps_x"] = hash_normal(tag + "/eps_x", (B * 4, 16, 16, 16))
     r["vae_eps_c"] = hash_normal(tag + "/eps_c", (B * 4, 16, 16, 16))
     r["task_mode"] = mode
+    if variant == "toolhang_prop":
+        # the wrist frames' posterior draws, [future half | history half] as the policy encodes them; the
+        # reference draws the history half first (get_vae_latent: second_image, then pred_second_image)
+        r["vae_eps_wrist"] = hash_normal(tag + "/eps_w", (2 * B * 4, 16, 16, 16))
     # keep the text (no label drop): the batch carries the reference's own CLIP latents (G6); the
     # label-drop branch is pinned by the g2_mar goldens, whose sample 0 is dropped
     r["text_drop_u"] = np.full(B, 0.5, dtype=np.float32)
@@ -341,13 +355,13 @@ def policy_variant_rng(variant, mode, B=POLICY_B):
 
 def policy_variant_kwargs(variant):
     """UnifiedVideoActionPolicy kwargs (besides vae / autoregressive params) of the variant."""
-    v = VARIANTS[variant]
+    v = variant_def(variant)
     umi = variant == "umi"
     return dict(action_model_params=dict(predict_action=True, act_model_type="conv_fc"),
                 shape_meta={"action": {"shape": [v["Da"]]}}, n_action_steps=8, shift_action=not umi,
                 language_emb_model="clip", task_name=v["task_name"],
                 task_modes=["policy_model", "full_dynamic_model"] if umi else [],
-                normalizer_type="none" if umi else "all", selected_training_mode=None, use_history_action=False,
+                normalizer_type="none" if umi or "toolhang" in variant else "all", selected_training_mode=None, use_history_action=False,
                 use_proprioception=v["use_proprioception"], action_mask_ratio=0.5,
                 different_history_freq=v["different_history_freq"], predict_wrist_img=False,
                 predict_proprioception=v["predict_proprioception"])

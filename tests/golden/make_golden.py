@@ -81,6 +81,9 @@ def injected(rng):
     q_int = [torch.from_numpy(x) for x in rng.get("randint", [])]
     q_nrm = [torch.from_numpy(x) for x in rng.get("randn_like", [])]
     q_eps = [torch.from_numpy(rng[k]) for k in ("vae_eps_x", "vae_eps_c") if k in rng]
+    if "vae_eps_wrist" in rng:  # second camera: history half (second_image) first, then the future half
+        w = torch.from_numpy(rng["vae_eps_wrist"])
+        q_eps = [w[len(w) // 2:], w[: len(w) // 2]] + q_eps
     saved = (torch.randint, torch.randn_like, torch.randn, torch.rand, random.choice,
              ref_mar.MAR.sample_orders)
 

@@ -130,9 +130,29 @@ __device__ __forceinline__ unsigned ch_halo_off(int p, int oh0, int ow0, int H, 
 }
 // GroupNorm-apply (+ SiLU) of one staged 16-B chunk, zeroed for a pixel outside the image (F.conv2d
 // pads the ACTIVATED tensor): packed-f32 math, the select on the four packed words
+#ifndef UVA_CONV_SCALAR_GN
+#define UVA_CONV_SCALAR_GN 0
+#endif
 template <bool SILU>
 __device__ __forceinline__ bf16x8 ch_gn_act(bf16x8 v, const float (&gsc)[8], const float (&gsh)[8], bool inb) {
   bf16x8 o;
+  if constexpr (UVA_CONV_SCALAR_GN != 0) {
+    // scalar f32 (the same IEEE operations per element as the packed form below, so the same bits): packed
+    // f32 VALU beside MFMAs costs more issue time than two scalar instructions (MI355X_MICROARCH.md)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      float u = fmaf((float)v[j], gsc[j], gsh[j]);
+      if constexpr (SILU) {
+        const float d = __builtin_amdgcn_exp2f(u * -1.4426950408889634f) + 1.f;
+        u = u * __builtin_amdgcn_rcpf(d);
+      }
+      o[j] = (bf16)u;
+    }
+    ch_u32x4 w = __builtin_bit_cast(ch_u32x4, o);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) w[k] = inb ? w[k] : 0u;
+    return __builtin_bit_cast(bf16x8, w);
+  }
 #pragma unroll
   for (int j = 0; j < 8; j += 2) {
     const f32x2 x = {(float)v[j], (float)v[j + 1]};

@@ -270,7 +270,7 @@ class UnifiedVideoActionPolicy(nn.Module):
             sel = select_frame_indices(T, different_history_freq=self.different_history_freq,
                                        rng_choice=rng.get("history_combination"))
             if self.use_proprioception:
-                prop = self._second_camera_prop(obs, sel, train=True)
+                prop = self._second_camera_prop(obs, sel, train=True, eps=rng.get("vae_eps_wrist"))
         if self.training and dev.type == "cuda":
             if getattr(self, "_wt_params", None) is None:
                 from ..model.autoregressive.mar_con_unified import Block
@@ -300,7 +300,7 @@ class UnifiedVideoActionPolicy(nn.Module):
     def forward(self, batch, **kwargs):
         return self.compute_loss(batch, **kwargs)
 
-    def _second_camera_prop(self, obs, sel, train):
+    def _second_camera_prop(self, obs, sel, train, eps=None):
         """process_data's second-camera branch (toolhang, data_utils.py:228-285) + get_vae_latent's
         second-image encodes (:395-410): the wrist frames at the selected indices through the KL-VAE
         (history half -> second_image_z, future half -> pred_second_image_z when training), the
@@ -310,7 +310,12 @@ class UnifiedVideoActionPolicy(nn.Module):
         B = wrist.shape[0]
         h = len(sel) // 2
         xw = vae_images(wrist, sel, self.vae_model.CIN_PAD)  # [future half | history half]
-        eps = torch.randn(xw.shape[0], self.vae_model.embed_dim, 16, 16, device=wrist.device)
+        # eps: the wrist posterior draws [future half | history half] (rng key 'vae_eps_wrist', as vae_eps_x / _c)
+        if eps is None:
+            eps = torch.randn(xw.shape[0], self.vae_model.embed_dim, 16, 16, device=wrist.device)
+        else:
+            eps = torch.as_tensor(eps).to(wrist.device)
+            assert tuple(eps.shape) == (xw.shape[0], self.vae_model.embed_dim, 16, 16), eps.shape
         tok = self.vae_model.encode_tokens(xw, eps).reshape(2, B, h, 256, -1)
         prop = {}
         keys = ("robot0_eef_pos", "robot0_eef_quat", "robot0_gripper_qpos")

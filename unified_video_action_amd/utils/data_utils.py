@@ -35,6 +35,8 @@ def image_key(task_name):
         return "agentview_rgb"
     if "umi" in task_name:
         return "camera0_rgb"
+    if "toolhang" in task_name:
+        return "sideview_image"  # (data_utils.py:47-58: resize_image renames it to "image")
     return "image"
 
 
