@@ -80,7 +80,7 @@ def parse(argv=None):
     ap.add_argument("--wall-budget-s", type=float, default=530.0,
                     help="the per-GPU-batch CPU step runs only if the whole bench is expected to end within this")
     ap.add_argument("--trace-out", default="", help="write every traced kernel row (tag, launches, avg ms) here")
-    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r05_end.json"))
+    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r06_end.json"))
     return ap.parse_args(argv)
 
 
