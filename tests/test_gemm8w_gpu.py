@@ -263,3 +263,31 @@ def test_layernorm_bwd_drop_matches_two_pass(rows, p):
     for i in range(4):
         assert torch.equal(a[i], b[i]), i
     assert (a[4] - b[4]).abs().max().item() <= 1e-5 * b[4].abs().max().item()
+
+
+@pytest.mark.parametrize("beta", [0.0, 1.0])
+@pytest.mark.parametrize("M,N,K", [(768, 768, 32768), (2304, 768, 32768), (3072, 768, 32768), (768, 3072, 8192),
+                                   (1000, 776, 1024), (256, 192, 256)])
+def test_dw_8w_tt_vs_routes(M, N, K, beta):
+    """the dW products (dw[M,N] (+)= dy[K,M]^T x[K,N], k-major operands) on gemm_8w (mode bit 7): bit-identical to
+    gemm_4w's split-K form where that one takes the shape (the same plan, the same per-slice k order, the same
+    slab reduce), and within 2e-6 of an fp64 product everywhere (fp32 accumulation over K)"""
+    from unified_video_action_amd.native import ops
+    g = torch.Generator(device=DEV).manual_seed(M + 7 * N + K)
+    dy, x = _rand(K, M, g=g), _rand(K, N, g=g)
+    init = torch.randn(M, N, device=DEV, generator=g)
+    want = dy.double().t() @ x.double() + beta * init.double()
+    prev = ops.gemm8w_set(-2, 128)
+    try:
+        d8 = init.clone()
+        ops.linear_dw(dy, x, d8, beta=beta)
+    finally:
+        ops.gemm8w_set(-2, prev[1])
+    d4 = init.clone()
+    ops.linear_dw(dy, x, d4, beta=beta)  # gemm_4w (few tiles) or gemm_8ph
+    torch.cuda.synchronize()
+    scale = want.abs().max().item()
+    assert (d8.double() - want).abs().max().item() < 2e-6 * scale * max(1.0, K / 8192)
+    tiles = ((M + 255) // 256) * ((N + 191) // 192)
+    if tiles <= 16 and K % 128 == 0 and K >= 256 and M >= 256 and N >= 192:
+        assert torch.equal(d8, d4)

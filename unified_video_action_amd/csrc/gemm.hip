@@ -1970,6 +1970,9 @@ extern "C" int uva_gemm4_try(int out_dtype, const void* A, const void* B, void* 
 extern "C" int uva_gemm8w_try(int out_dtype, const void* A, const void* B, void* C, int M, int N, int K,
                               long long lda, long long ldb, long long ldc, const float* bias, float alpha,
                               hipStream_t s);
+extern "C" int uva_gemm8w_tt_try(const void* A, const void* B, float* C, int M, int N, int K, long long lda,
+                                 long long ldb, long long ldc, float alpha, float beta, float* ws, long long ws_floats,
+                                 int* reduce, hipStream_t s);
 extern "C" int uva_gemm4_tt_try(const void* A, const void* B, float* C, int M, int N, int K, long long lda,
                                 long long ldb, long long ldc, float alpha, float beta, float* ws, long long ws_floats,
                                 int* reduce, hipStream_t s);
@@ -1995,7 +1998,8 @@ static int launch_mfma(int ta, int tb, const void* A, const void* B, void* C, in
   if (sizeof(TC) == 4 && ta == 1 && tb == 1 && batch == 1 && !ep.bias && !ep.residual && !ep.aux && !ep.gate &&
       ep.act == 0 && ep.drop_thresh == 0 && ep.res_grad == 0) {
     int red = 0;
-    const int r = uva_gemm4_tt_try(A, B, (float*)C, M, N, K, lda, ldb, ldc, ep.alpha, ep.beta, ws, ws_floats, &red, s);
+    int r = uva_gemm8w_tt_try(A, B, (float*)C, M, N, K, lda, ldb, ldc, ep.alpha, ep.beta, ws, ws_floats, &red, s);
+    if (r == 0) r = uva_gemm4_tt_try(A, B, (float*)C, M, N, K, lda, ldb, ldc, ep.alpha, ep.beta, ws, ws_floats, &red, s);
     if (r < 0) return -r;
     if (r > 0) {
       if (red > 0) {

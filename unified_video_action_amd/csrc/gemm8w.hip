@@ -56,6 +56,15 @@ __device__ __forceinline__ int g8_xcd_remap(int bid, int nblk) {
   return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + bid / 8;
 }
 
+// 16-B chunk swizzle of a k-major image row [64 k][W] (TA / TB = 1 operands), as gemm4.hip's: the 8 rows a
+// 32-lane group of ds_read_b64_tr_b16 touches fall on distinct 32-B bank slots
+template <int W>
+__device__ __forceinline__ int g8_kswz(int k) {
+  static_assert(W == 256 || W == 192, "row width");
+  if constexpr (W == 256) return ((k & 3) << 1) | (((k >> 3) & 1) << 3);
+  else return (((k >> 1) & 1) << 1) | (((k >> 3) & 1) << 2);
+}
+
 __device__ __forceinline__ uint32_t pk_bf16(float lo, float hi) {
   typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2_t;
   return __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2){lo, hi}, bf16x2_t));
@@ -83,11 +92,16 @@ struct G8Epi {
 // NW = 8: one workgroup per CU (two waves per SIMD in lockstep: both reach the epilogue together), the bias
 // row in LDS.  NW = 4: a 128 x 192 block tile, two independent workgroups per CU (80 KB of ring each: the
 // bias comes from L2 instead), so one workgroup's epilogue can run beside the other's MFMA loop.
-template <int FM, int FN, int NW, int EPI, int NDEF, typename TC, int DM>
+// TA / TB = 1 (the dW products: A [K][M], B [K][N], M- / N-contiguous; EPI 0, fp32 C): k-major LDS images read
+// by ds_read_b64_tr_b16, and work items (tile, K-slice) writing fp32 partial slabs C + slice * slab_bytes
+// (reduced by splitk_reduce) when splits > 1.
+template <int FM, int FN, int NW, int EPI, int NDEF, typename TC, int DM, int TA = 0, int TB = 0>
 __global__ __launch_bounds__(64 * NW, 8 / NW) void gemm_8w(const bf16* __restrict__ A, const bf16* __restrict__ B,
                                                        TC* __restrict__ C, int M, int N, int K, int lda, int ldb,
-                                                       int ldc, G8Epi ep, int w1ok) {
+                                                       int ldc, G8Epi ep, int w1ok, int splits, int kps,
+                                                       int slab_bytes) {
   using G = G8Cfg<FM, FN, NW>;
+  static_assert((TA == 0 && TB == 0) || (EPI == 0 && NDEF == 0 && sizeof(TC) == 4), "k-major operands: plain fp32");
   static_assert(EPI == 0 || sizeof(TC) == (EPI == 2 ? 4 : 2), "EPI output type");
   // stores per wave per item: one 16-B store per (fragment row, column pair) (fp32: two); EPI 1 also P;
   // EPI 3 the tile's column-sum partials (two per column pair)
@@ -102,10 +116,11 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void gemm_8w(const bf16* __restric
   const int w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
   const int wr = w >> 1, wc = w & 1;
   const int tm = (M + G::BM - 1) / G::BM, tn = (N + G::BN - 1) / G::BN, ntiles = tm * tn;
+  const int nitems = ntiles * splits;
   const int grid = gridDim.x;
   const int slot = g8_xcd_remap(blockIdx.x, grid);
-  if (slot >= ntiles) return;
-  const int my_items = (ntiles - slot + grid - 1) / grid;
+  if (slot >= nitems) return;
+  const int my_items = (nitems - slot + grid - 1) / grid;
 
   float* sbias = (float*)(smem + G::RING);
   const bool has_bias = ep.bias != nullptr;
@@ -118,45 +133,62 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void gemm_8w(const bf16* __restric
   }
 
   constexpr int GROUP = 8;
-  auto item_of = [&](int t, int& m0, int& n0) __attribute__((always_inline)) {
+  // item -> (tile: GROUP-8 raster, K-slice sl: the slow index, so concurrent items share one K range)
+  auto item_of = [&](int pid, int& m0, int& n0) __attribute__((always_inline)) {
+    const int t = pid % ntiles;
     const int group = t / (GROUP * tn), first_m = group * GROUP;
     const int gsz = min(tm - first_m, GROUP);
     m0 = (first_m + (t % (GROUP * tn)) % gsz) * G::BM;
     n0 = ((t % (GROUP * tn)) / gsz) * G::BN;
   };
 
-  const auto rsA = __builtin_amdgcn_make_buffer_rsrc((void*)A, 0, (int)(unsigned)(2ull * (unsigned)M * (unsigned)lda),
-                                                     0x00020000);
-  const auto rsB = __builtin_amdgcn_make_buffer_rsrc((void*)B, 0, (int)(unsigned)(2ull * (unsigned)N * (unsigned)ldb),
-                                                     0x00020000);
+  const auto rsA = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)A, 0, (int)(unsigned)(2ull * (unsigned)(TA ? K : M) * (unsigned)lda), 0x00020000);
+  const auto rsB = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)B, 0, (int)(unsigned)(2ull * (unsigned)(TB ? K : N) * (unsigned)ldb), 0x00020000);
+  // T = 1: the k-major image [64][W] taken 1 KB per DMA instruction in byte order; lane l of piece j: byte
+  // j KB + 16 l -> (k, chunk), global chunk = chunk ^ kswz(k)
+  auto lane_src_k = [&](auto WC, int piece, int ld) __attribute__((always_inline)) -> unsigned {
+    constexpr int W = decltype(WC)::value;
+    const int b = piece * 1024 + lane * 16;
+    const int k = b / (W * 2), c = (b % (W * 2)) >> 4;
+    return (unsigned)k * (unsigned)ld * 2u + (unsigned)((c ^ g8_kswz<W>(k)) * 16);
+  };
+  using WAc = std::integral_constant<int, G::BM>;
+  using WBc = std::integral_constant<int, G::BN>;
+  constexpr int stepA = TA ? 0 : 128, stepB = TB ? 0 : 128;  // bytes per K-tile (T = 1: 64 rows of ld, runtime)
+  const int stA = TA ? 64 * lda * 2 : stepA, stB = TB ? 64 * ldb * 2 : stepB;
   // per-lane DMA sources: instruction i of wave w covers image rows 8 (w G + i) .. +7 of 128 B; lane l: row
   // (l >> 3), LDS chunk (l & 7) <- global chunk (l & 7) ^ (row & 7); the K-tile step is the soffset
   unsigned offA[G::GA], offB[G::GB];
-  auto dma_offsets = [&](int t) __attribute__((always_inline)) {
+  auto dma_offsets = [&](int pid) __attribute__((always_inline)) {
     int m0, n0;
-    item_of(t, m0, n0);
-    const unsigned a0 = (unsigned)__builtin_amdgcn_readfirstlane(m0 * lda * 2);
-    const unsigned b0 = (unsigned)__builtin_amdgcn_readfirstlane(n0 * ldb * 2);
+    item_of(pid, m0, n0);
+    const int kb = (pid / ntiles) * kps;
+    const unsigned a0 = (unsigned)__builtin_amdgcn_readfirstlane(TA ? (kb * lda + m0) * 2 : (m0 * lda + kb) * 2);
+    const unsigned b0 = (unsigned)__builtin_amdgcn_readfirstlane(TB ? (kb * ldb + n0) * 2 : (n0 * ldb + kb) * 2);
 #pragma unroll
     for (int i = 0; i < G::GA; ++i) {
       const int row = 8 * (w * G::GA + i) + (lane >> 3);
-      offA[i] = a0 + (unsigned)row * (unsigned)lda * 2u + (unsigned)(((lane & 7) ^ (row & 7)) * 16);
+      if constexpr (TA != 0) offA[i] = a0 + lane_src_k(WAc{}, w * G::GA + i, lda);
+      else offA[i] = a0 + (unsigned)row * (unsigned)lda * 2u + (unsigned)(((lane & 7) ^ (row & 7)) * 16);
     }
 #pragma unroll
     for (int i = 0; i < G::GB; ++i) {
       const int row = 8 * (w * G::GB + i) + (lane >> 3);
-      offB[i] = b0 + (unsigned)row * (unsigned)ldb * 2u + (unsigned)(((lane & 7) ^ (row & 7)) * 16);
+      if constexpr (TB != 0) offB[i] = b0 + lane_src_k(WBc{}, w * G::GB + i, ldb);
+      else offB[i] = b0 + (unsigned)row * (unsigned)ldb * 2u + (unsigned)(((lane & 7) ^ (row & 7)) * 16);
     }
   };
   auto dma_one = [&](int r, int i, int kt) __attribute__((always_inline)) {
     if (i < G::GA)
       __builtin_amdgcn_raw_ptr_buffer_load_lds(
           rsA, (__attribute__((address_space(3))) void*)(smem + r * G::REGION + (w * G::GA + i) * 1024), 16,
-          (int)offA[i < G::GA ? i : 0], __builtin_amdgcn_readfirstlane(kt * 128), 0, 0);
+          (int)offA[i < G::GA ? i : 0], __builtin_amdgcn_readfirstlane(kt * stA), 0, 0);
     else
       __builtin_amdgcn_raw_ptr_buffer_load_lds(
           rsB, (__attribute__((address_space(3))) void*)(smem + r * G::REGION + G::A_BYTES + (w * G::GB + i - G::GA) * 1024),
-          16, (int)offB[i < G::GA ? 0 : i - G::GA], __builtin_amdgcn_readfirstlane(kt * 128), 0, 0);
+          16, (int)offB[i < G::GA ? 0 : i - G::GA], __builtin_amdgcn_readfirstlane(kt * stB), 0, 0);
   };
   dma_offsets(slot);
 
@@ -164,11 +196,31 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void gemm_8w(const bf16* __restric
   const int lofs0 = lrow * 128 + (((lane >> 4) ^ (lrow & 7)) << 4);
   const int lofs1 = lrow * 128 + (((4 + (lane >> 4)) ^ (lrow & 7)) << 4);
   const int a0o = wr * (FM * 16), b0o = wc * (FN * 16);
+  // T = 1: two ds_read_b64_tr_b16 of the k-major image (rows k and k + 4 of the lane's quad, 4 columns each),
+  // the hardware transpose gathering the lane's 8 consecutive k (the same k order as the T = 0 read).  The
+  // swizzle of rows k, k + 4, k + 32, k + 36 is one lane constant sw (kswz reads bits 0-3 of k, q + 4 < 8) and
+  // the fragment's 8-column chunk c0 / 8 is even and wave-uniform, so an address is lane constant + ((c0 / 8 ^
+  // sw) << 4) + immediate: two VALU per fragment instead of a hoisted address register per (fragment, half)
+  // (those spilled 14 VGPRs).  The empty asm keeps hipcc from hoisting the per-fragment values again.
+  const int kq = (lane >> 4) * 8 + ((lane >> 2) & 3);
+  auto frag_k = [&](auto WC, int base, int c0, int h) __attribute__((always_inline)) -> bf16x8 {
+    constexpr int W = decltype(WC)::value;
+    int sw = g8_kswz<W>(kq);
+    asm volatile("" : "+v"(sw));
+    const int lb = kq * W * 2 + ((lane >> 1) & 1) * 16 + (lane & 1) * 8;
+    const char* a0 = smem + base + h * 32 * W * 2 + lb + (((c0 >> 3) ^ sw) << 4);
+    const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(s16x4, a0));
+    const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(s16x4, a0 + 4 * W * 2));
+    const s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+    return __builtin_bit_cast(bf16x8, v);
+  };
   auto fragA = [&](int r, int f, int h) __attribute__((always_inline)) {
-    return *(const bf16x8*)(smem + r * G::REGION + (a0o + f * 16) * 128 + (h ? lofs1 : lofs0));
+    if constexpr (TA) return frag_k(WAc{}, r * G::REGION, a0o + f * 16, h);
+    else return *(const bf16x8*)(smem + r * G::REGION + (a0o + f * 16) * 128 + (h ? lofs1 : lofs0));
   };
   auto fragB = [&](int r, int g, int h) __attribute__((always_inline)) {
-    return *(const bf16x8*)(smem + r * G::REGION + G::A_BYTES + (b0o + g * 16) * 128 + (h ? lofs1 : lofs0));
+    if constexpr (TB) return frag_k(WBc{}, r * G::REGION + G::A_BYTES, b0o + g * 16, h);
+    else return *(const bf16x8*)(smem + r * G::REGION + G::A_BYTES + (b0o + g * 16) * 128 + (h ? lofs1 : lofs0));
   };
 
   f32x4 acc[FM][FN];
@@ -188,8 +240,10 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void gemm_8w(const bf16* __restric
 
   // ---- epilogue pieces ------------------------------------------------------------------------------
   const int csub = ((lane >> 4) & 1) * 16 + (lane >> 5) * 8;  // the lane's 8 columns in a 32-col pair
-  const unsigned long long cbytes = (unsigned long long)M * (unsigned long long)ldc * sizeof(TC);
+  const unsigned long long cbytes = (unsigned long long)M * (unsigned long long)ldc * sizeof(TC) +
+                                    (unsigned long long)(splits - 1) * (unsigned)slab_bytes;
   const auto rsC = __builtin_amdgcn_make_buffer_rsrc((void*)C, 0, (int)(unsigned)cbytes, 0x00020000);
+  int cslab = 0;  // byte offset of the current item's partial slab
   const auto rsP = __builtin_amdgcn_make_buffer_rsrc((EPI == 1 || EPI == 3) ? ep.C2 : (void*)C, 0,
                                                      (int)(unsigned)((EPI == 1 || EPI == 3) ? 2ull * M * ldc : cbytes),
                                                      0x00020000);
@@ -269,7 +323,7 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void gemm_8w(const bf16* __restric
                     bool have_in) __attribute__((always_inline)) {
     const RowIn in = have_in ? in_ : load_in(row, col);
     const bool ok = row < M && col < N;
-    const int voff = ok ? (row * ldc + col) * (int)sizeof(TC) : 0x7fff8000;
+    const int voff = ok ? (row * ldc + col) * (int)sizeof(TC) + cslab : 0x7fff8000;
     if constexpr (EPI == 0) {
       if constexpr (sizeof(TC) == 2) {
         __builtin_amdgcn_raw_buffer_store_b128((u32x4){pk[0], pk[1], pk[2], pk[3]}, rsC, voff, 0, 0);
@@ -490,7 +544,9 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void gemm_8w(const bf16* __restric
     int m0, n0;
     const int t = slot + ii * grid;
     item_of(t, m0, n0);
-    const int nkt = K / 64;
+    const int sl = t / ntiles, kb = sl * kps;
+    const int nkt = (min(K, kb + kps) - kb) / 64;
+    cslab = sl * slab_bytes;
     const int nxt = ii + 1 < my_items ? t + grid : t;
     const int ngroups = nkt / 2;
     const bool imm = ii > 0 && w1ok && EIMM > 0;
@@ -587,7 +643,8 @@ static int g_gemm8w_mode = 0;     // bit 1: 64 x 64 wave tiles; bits 2..4: defer
                                   // bit 5 / 6: every product on two 4-wave workgroups per CU (NW = 4) / on
                                   // one 8-wave workgroup (NW = 8); neither: EPI 3 on NW = 4, the rest NW = 8
                                   // (fc2 dX + GELU' 222-232 vs 230-237 us, fc1 + GELU 247-250 vs 235-242,
-                                  // profiles/r06/g8w_nw4_final.txt)
+                                  // profiles/r06/g8w_nw4_final.txt); bit 7: the dW products
+                                  // (uva_gemm8w_tt_try)
 
 template <int FN, int EPI, int NDEF, typename TC, int DM, int NW>
 static int g8_launch1(const void* A, const void* B, void* C, int M, int N, int K, int lda, int ldb, int ldc,
@@ -605,9 +662,42 @@ static int g8_launch1(const void* A, const void* B, void* C, int M, int N, int K
   }
   const int w1ok = (M % G::BM == 0) && (N % G::BN == 0);
   gemm_8w<4, FN, NW, EPI, NDEF, TC, DM><<<dim3(grid), 64 * NW, lds, s>>>((const bf16*)A, (const bf16*)B, (TC*)C, M, N,
-                                                                       K, lda, ldb, ldc, ep, w1ok);
+                                                                       K, lda, ldb, ldc, ep, w1ok, 1, K, 0);
   UVA_LAUNCH_CHECK();
   return 0;
+}
+
+// dW products (A [K][M], B [K][N], K = tokens): split-K plan -- enough (tile, K-slice) items for one round of
+// the chip, slices of whole 128-deep pairs, >= 256 deep each
+struct G8Split {
+  int splits, kps, grid;
+};
+static G8Split g8_plan_tt(int M, int N, int K, long long ws_floats, bool need_ws) {
+  G8Split p{0, 0, 0};
+  if (K % 128 != 0 || K < 256 || M < 256 || N < 192) return p;
+  const int cus = g8_cus();
+  const long long tiles = (long long)((M + 255) / 256) * ((N + 191) / 192);
+  int splits = (int)std::max<long long>(1, (cus + tiles / 2) / tiles);
+  if (splits > K / 256) splits = K / 256;
+  while (splits > 1 && (long long)splits * M * N > ws_floats) --splits;
+  if (splits == 1 && need_ws && (long long)M * N > ws_floats) return p;
+  int kps = K;
+  for (; splits > 1; --splits) {
+    kps = ((K + splits - 1) / splits + 127) / 128 * 128;
+    const int sp = (K + kps - 1) / kps;
+    if (K - (sp - 1) * kps >= 256) {
+      splits = sp;
+      break;
+    }
+  }
+  if (splits <= 1) {
+    splits = 1;
+    kps = K;
+  }
+  p.splits = splits;
+  p.kps = kps;
+  p.grid = (int)std::min<long long>(tiles * splits, cus);
+  return p;
 }
 // rows of EPI 3 column-sum partials the launch writes (every wave of every row tile stores its 64 rows)
 static bool g8_nw4(int epi) { return (g_gemm8w_mode & 32) || (!(g_gemm8w_mode & 64) && epi == 3); }
@@ -660,6 +750,41 @@ static bool g8_ok(const void* A, const void* B, const void* C, int M, int N, int
 }
 
 static uint32_t g8_key(unsigned long long seed) { return drop_key(seed); }
+
+// the dW products on gemm_8w (mode bit 7: 128): 1 = launched: *reduce = 0 -> C holds alpha * A^T B; *reduce = s > 0
+// -> ws holds s fp32 partial slabs of M x N (ld N) the caller reduces into C (alpha, beta).  0 = not eligible / off
+extern "C" int uva_gemm8w_tt_try(const void* A, const void* B, float* C, int M, int N, int K, long long lda,
+                                 long long ldb, long long ldc, float alpha, float beta, float* ws, long long ws_floats,
+                                 int* reduce, hipStream_t s) {
+  *reduce = 0;
+  if (!(g_gemm8w_mode & 128)) return 0;
+  if (M <= 0 || N <= 0 || K <= 0) return 0;
+  if (lda % 8 || ldb % 8 || ldc % 8 || M % 8 || N % 8 || lda < M || ldb < N) return 0;
+  if (((uintptr_t)A | (uintptr_t)B | (uintptr_t)C | (uintptr_t)ws) % 16) return 0;
+  if (2.0 * (double)K * (double)lda >= 2147483648.0 || 2.0 * (double)K * (double)ldb >= 2147483648.0) return 0;
+  const G8Split p = g8_plan_tt(M, N, K, ws ? ws_floats : 0, beta != 0.f);
+  if (p.splits == 0) return 0;
+  const bool direct = p.splits == 1 && beta == 0.f;
+  if (direct ? (double)M * (double)ldc * 4.0 > (double)0x7fff0000
+             : (double)p.splits * (double)M * (double)N * 4.0 > (double)0x7fff0000)
+    return 0;
+  if (!direct && !ws) return 0;
+  using G = G8Cfg<4, 6, 8>;
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)gemm_8w<4, 6, 8, 0, 0, float, 0, 1, 1>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
+    attr = true;
+  }
+  const int w1ok = (M % G::BM == 0) && (N % G::BN == 0);
+  G8Epi ep{nullptr, direct ? alpha : 1.f, nullptr, nullptr, nullptr, nullptr, 0u, 0u, 1.f};
+  gemm_8w<4, 6, 8, 0, 0, float, 0, 1, 1><<<dim3(p.grid), 512, G::RING, s>>>(
+      (const bf16*)A, (const bf16*)B, direct ? C : ws, M, N, K, (int)lda, (int)ldb, direct ? (int)ldc : N, ep, w1ok,
+      p.splits, p.kps, (int)((long long)M * N * 4));
+  UVA_LAUNCH_CHECK();
+  if (!direct) *reduce = p.splits;
+  return 1;
+}
 
 // plain product (measurement route): 1 = launched, 0 = not eligible / off, < 0 = -hipError
 extern "C" int uva_gemm8w_try(int out_dtype, const void* A, const void* B, void* C, int M, int N, int K, long long lda,
