@@ -27,6 +27,11 @@ class _Runtime:
         # proj output before the dropout and the fp32 residual add, as autocast) instead of gemm_8ph's fused
         # epilogue (which kept the fp32 accumulator): 59-62 vs 72-75 us at B32 (profiles/r06/g8w_fused.txt)
         self.proj_8w = True
+        # the remaining plain K-contiguous products (qkv forward, the Block's dX products, the DiffLoss MLP) on the
+        # 8-wave GEMM instead of gemm_4w (uva_gemm8w_set; the same bits, tests/test_gemm8w_gpu.py): bench 263.9 /
+        # 264.2 vs 262.3 / 263.7 samples/s, same box interleaved (profiles/r06/ab_gemm8w_plain.txt)
+        self.gemm8w_plain = True
+        self._gemm8w_plain_set = None
         # the proj / fc1 / fc2 dropout masks of a Block as keep-bit planes (one launch each per step) read by the
         # fused epilogues, instead of the counter hash per element inside them (the same bits).  Measured off:
         # the epilogue's plane-word loads expose their latency where the hash was issue-bound VALU (fc1 285-296
@@ -86,6 +91,10 @@ class _Runtime:
         """a new MAR forward: hand-offs of the previous step that found no consumer are dropped"""
         self._drop_pending.clear()
         self._drop_ready.clear()
+        if self._gemm8w_plain_set is not self.gemm8w_plain:
+            from .native import ops
+            ops.gemm8w_set(int(self.gemm8w_plain), -2)
+            self._gemm8w_plain_set = self.gemm8w_plain
 
     def bump_params(self):
         self.param_gen += 1
