@@ -567,6 +567,9 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void gemm_8w(const bf16* __restric
     }
     for (int it = it0; it < ngroups - 1; ++it) group(ZF{}, false, 2 * it + 2, -1, -1);
     dma_offsets(nxt);
+    // (UVA_G8_PREFETCH & 2: row 0's inputs issued before the tile's last K-group, ahead of its refill DMAs:
+    // older than every DMA the group's RAW waits count, so those waits only get stricter)
+    if constexpr ((UVA_G8_PREFETCH & 2) != 0) prefetch_in(0, m0, n0);
     group(ZF{}, false, 0, -1, -1);
     pack_def(n0);
     if constexpr (EPI == 3) {
@@ -575,7 +578,7 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void gemm_8w(const bf16* __restric
 #pragma unroll
         for (int e = 0; e < 8; ++e) cs[p][e] = 0.f;
     }
-    prefetch_in(0, m0, n0);
+    if constexpr ((UVA_G8_PREFETCH & 2) == 0) prefetch_in(0, m0, n0);
 #pragma unroll
     for (int f = 0; f < F0; ++f) {
       __builtin_amdgcn_sched_barrier(0);
