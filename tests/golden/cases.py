@@ -289,7 +289,9 @@ POLICY_VARIANT_MODES = {"libero": ["full_dynamic_model", "policy_model"],
                         "umi": ["full_dynamic_model", "policy_model"],
                         # toolhang's second camera through the policy: wrist frames VAE-encoded with their own
                         # posterior draws (vae_eps_wrist), eef / gripper streams split into history / future
-                        "toolhang_prop": ["full_dynamic_model"]}
+                        "toolhang_prop": ["full_dynamic_model", "policy_model"],
+                        # ... and with the wrist-camera video stream + its loss (predict_wrist_img)
+                        "toolhang_wrist": ["full_dynamic_model"]}
 
 
 def umi_img_indices(tag, B):
@@ -317,7 +319,7 @@ def ref_language_latents(B, start=0):
 def policy_variant_batch(variant, B=POLICY_B):
     """Libero / UMI batches; the language latents are the reference's own CLIP latents (G6)."""
     tag = f"policy/{variant}"
-    if variant == "toolhang_prop":
+    if variant.startswith("toolhang"):
         obs = {"sideview_image": (hash_tensor(tag + "/img", (B, 32, 3, 128, 128)) + 1.0) * 0.5,
                "robot0_eye_in_hand_image": (hash_tensor(tag + "/wrist", (B, 32, 3, 128, 128)) + 1.0) * 0.5}
         for k, d in (("robot0_eef_pos", 3), ("robot0_eef_quat", 4), ("robot0_gripper_qpos", 2)):
@@ -343,7 +345,7 @@ def policy_variant_rng(variant, mode, B=POLICY_B):
     r["vae_eps_x"] = hash_normal(tag + "/eps_x", (B * 4, 16, 16, 16))
     r["vae_eps_c"] = hash_normal(tag + "/eps_c", (B * 4, 16, 16, 16))
     r["task_mode"] = mode
-    if variant == "toolhang_prop":
+    if variant.startswith("toolhang"):
         # the wrist frames' posterior draws, [future half | history half] as the policy encodes them; the
         # reference draws the history half first (get_vae_latent: second_image, then pred_second_image)
         r["vae_eps_wrist"] = hash_normal(tag + "/eps_w", (2 * B * 4, 16, 16, 16))
@@ -363,7 +365,7 @@ def policy_variant_kwargs(variant):
                 task_modes=["policy_model", "full_dynamic_model"] if umi else [],
                 normalizer_type="none" if umi or "toolhang" in variant else "all", selected_training_mode=None, use_history_action=False,
                 use_proprioception=v["use_proprioception"], action_mask_ratio=0.5,
-                different_history_freq=v["different_history_freq"], predict_wrist_img=False,
+                different_history_freq=v["different_history_freq"], predict_wrist_img=v.get("predict_wrist_img", False),
                 predict_proprioception=v["predict_proprioception"])
 
 
