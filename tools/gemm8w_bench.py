@@ -142,14 +142,10 @@ def fused(M, rounds, p=0.1):
             print(f"[{mname}] fc2 dX+drop+dgelu+bias: split {ts4 * 1e3:.1f} us, fused {tf4 * 1e3:.1f} us (dpre diff "
                   f"{d4[0]}, dbias rel {d4[1]:.2g})", flush=True)
             # the same with precomputed keep-bit planes (and the plane kernel's own time)
-            pl1 = ops.dropout_plane(M * 3072, p, 77, dev)
-            pl2 = ops.dropout_plane(M * 768, p, 78, dev)
-            pl4 = ops.dropout_plane(M * 3072, p, 80, dev)
-            tp1 = timeit(lambda: ops.linear_gelu_drop(x, w, b, pre_f, a_f, drop_p=p, seed=77, plane=pl1))
-            tp2 = timeit(lambda: ops.linear_drop_res(h, w2, b2, res, o_f, drop_p=p, seed=78, plane=pl2))
-            tp4 = timeit(lambda: ops.linear_dgelu_drop(dy, wt, pre_s, dp_f, db_f, drop_p=p, seed=80, accum_bias=False,
-                                                       plane=pl4))
-            tpl = timeit(lambda: ops.dropout_plane(M * 3072, p, 81, dev, out=pl1))
+            if p == 0:
+                tp1 = tp2 = tp4 = tpl = float("nan")
+            else:
+                tp1, tp2, tp4, tpl = planes(M, p, x, w, b, pre_f, a_f, h, w2, b2, res, o_f, dy, wt, pre_s, dp_f, db_f)
             print(f"[{mname}] with planes: fc1 {tp1 * 1e3:.1f} us, fc2 {tp2 * 1e3:.1f} us, dgelu {tp4 * 1e3:.1f} us; "
                   f"plane [M, 3072] {tpl * 1e3:.1f} us", flush=True)
             print(f"[{mname}] proj+drop+res: gemm_8ph epilogue {ts3 * 1e3:.1f} us, 8w {tf3 * 1e3:.1f} us (diff {d3})",
@@ -160,9 +156,25 @@ def fused(M, rounds, p=0.1):
     ops.gemm8w_set(0, 0)
 
 
+def planes(M, p, x, w, b, pre_f, a_f, h, w2, b2, res, o_f, dy, wt, pre_s, dp_f, db_f):
+    """fused launches reading precomputed keep-bit planes, and the plane kernel's own time"""
+    dev = x.device
+    pl1 = ops.dropout_plane(M * 3072, p, 77, dev)
+    pl2 = ops.dropout_plane(M * 768, p, 78, dev)
+    pl4 = ops.dropout_plane(M * 3072, p, 80, dev)
+    tp1 = timeit(lambda: ops.linear_gelu_drop(x, w, b, pre_f, a_f, drop_p=p, seed=77, plane=pl1))
+    tp2 = timeit(lambda: ops.linear_drop_res(h, w2, b2, res, o_f, drop_p=p, seed=78, plane=pl2))
+    tp4 = timeit(lambda: ops.linear_dgelu_drop(dy, wt, pre_s, dp_f, db_f, drop_p=p, seed=80, accum_bias=False,
+                                               plane=pl4))
+    tpl = timeit(lambda: ops.dropout_plane(M * 3072, p, 81, dev, out=pl1))
+    return tp1, tp2, tp4, tpl
+
+
 if __name__ == "__main__":
     what = sys.argv[1] if len(sys.argv) > 1 else "all"
     if what in ("all", "plain"):
         plain(32768, 2)
     if what in ("all", "fused"):
         fused(32768, 2)
+    if what == "fused_p0":  # the same without dropout: the counter hash's share of the epilogues
+        fused(32768, 2, p=0.0)
